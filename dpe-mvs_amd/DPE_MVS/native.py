@@ -1,0 +1,135 @@
+"""Python host binding of the HIP library (lib/libdpe_mvs.so) through its C-ABI.
+
+There is no CPU fallback: if the library is missing this module raises at import.  The library
+is built in-tree by `make -C dpe-mvs_amd` (or `__graft_entry__.build()`).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import _abi
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libdpe_mvs.so")
+
+EXPORTED = [
+    "dpe_params_default", "dpe_create", "dpe_destroy", "dpe_last_error", "dpe_pm_stage",
+    "dpe_pm_execute", "dpe_pm_fetch", "dpe_pm_run", "dpe_pm_device_planes", "dpe_pm_export_depth",
+    "dpe_pm_last_timings", "dpe_set_timing",
+]
+
+
+def load_library(path: str = LIB_PATH) -> C.CDLL:
+    if not os.path.exists(path):
+        raise RuntimeError(f"HIP library not built: {path} (run `make -C dpe-mvs_amd`)")
+    lib = C.CDLL(path)
+    lib.dpe_params_default.argtypes = [C.POINTER(_abi.DpePatchMatchParams)]
+    lib.dpe_params_default.restype = None
+    lib.dpe_create.argtypes = [C.c_int]
+    lib.dpe_create.restype = C.c_void_p
+    lib.dpe_destroy.argtypes = [C.c_void_p]
+    lib.dpe_destroy.restype = None
+    lib.dpe_last_error.argtypes = []
+    lib.dpe_last_error.restype = C.c_char_p
+    for fn in ("dpe_pm_stage", "dpe_pm_run"):
+        getattr(lib, fn).argtypes = [C.c_void_p, C.POINTER(_abi.DpePassInput), C.POINTER(_abi.DpePassState)]
+        getattr(lib, fn).restype = C.c_int
+    lib.dpe_pm_execute.argtypes = [C.c_void_p, C.c_void_p]
+    lib.dpe_pm_execute.restype = C.c_int
+    lib.dpe_pm_fetch.argtypes = [C.c_void_p, C.POINTER(_abi.DpePassState)]
+    lib.dpe_pm_fetch.restype = C.c_int
+    lib.dpe_pm_device_planes.argtypes = [C.c_void_p]
+    lib.dpe_pm_device_planes.restype = C.c_void_p
+    lib.dpe_pm_export_depth.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.dpe_pm_export_depth.restype = C.c_int
+    lib.dpe_pm_last_timings.argtypes = [C.c_void_p, C.POINTER(C.c_float), C.c_int]
+    lib.dpe_pm_last_timings.restype = C.c_int
+    lib.dpe_set_timing.argtypes = [C.c_void_p, C.c_int]
+    lib.dpe_set_timing.restype = None
+    return lib
+
+
+_LIB = load_library()
+
+
+class DpeError(RuntimeError):
+    pass
+
+
+def _check(rc: int, what: str):
+    if rc != 0:
+        msg = _LIB.dpe_last_error().decode(errors="replace")
+        raise DpeError(f"{what} failed ({rc}): {msg}")
+
+
+class PatchMatchContext:
+    """One HIP device context (the reference's per-image `DPE` object minus the file I/O)."""
+
+    def __init__(self, device: int = 0):
+        self._ctx = _LIB.dpe_create(int(device))
+        if not self._ctx:
+            raise DpeError("dpe_create failed: " + _LIB.dpe_last_error().decode(errors="replace"))
+        self._bufs = None
+
+    def close(self):
+        if self._ctx:
+            _LIB.dpe_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_timing(self, on: bool):
+        _LIB.dpe_set_timing(self._ctx, 1 if on else 0)
+
+    def stage(self, pass_input: dict, state: dict):
+        self._bufs = _abi.PassBuffers(pass_input, state)
+        _check(_LIB.dpe_pm_stage(self._ctx, C.byref(self._bufs.inp), C.byref(self._bufs.st)), "dpe_pm_stage")
+
+    def execute(self, stream: int | None = None):
+        _check(_LIB.dpe_pm_execute(self._ctx, C.c_void_p(stream or 0)), "dpe_pm_execute")
+
+    def fetch(self) -> dict:
+        _check(_LIB.dpe_pm_fetch(self._ctx, C.byref(self._bufs.st)), "dpe_pm_fetch")
+        return {k: v.copy() for k, v in self._bufs.outputs().items()}
+
+    def run(self, pass_input: dict, state: dict) -> dict:
+        self.stage(pass_input, state)
+        self.execute()
+        return self.fetch()
+
+    def timings(self) -> list[float]:
+        buf = (C.c_float * 8)()
+        n = _LIB.dpe_pm_last_timings(self._ctx, buf, 8)
+        return [float(buf[i]) for i in range(n)]
+
+    def device_planes(self) -> int:
+        return int(_LIB.dpe_pm_device_planes(self._ctx) or 0)
+
+    def export_depth(self, dev_ptr: int, stream: int | None = None):
+        _check(_LIB.dpe_pm_export_depth(self._ctx, C.c_void_p(dev_ptr), C.c_void_p(stream or 0)), "dpe_pm_export_depth")
+
+
+def run_pass(pass_input: dict, state: dict, device: int = 0) -> dict:
+    ctx = PatchMatchContext(device)
+    try:
+        return ctx.run(pass_input, state)
+    finally:
+        ctx.close()
+
+
+def param_struct(**overrides) -> _abi.DpePatchMatchParams:
+    p = _abi.DpePatchMatchParams()
+    _LIB.dpe_params_default(C.byref(p))
+    for k, v in overrides.items():
+        setattr(p, k, v)
+    return p
+
+
+__all__ = ["PatchMatchContext", "run_pass", "param_struct", "DpeError", "LIB_PATH", "EXPORTED", "np"]

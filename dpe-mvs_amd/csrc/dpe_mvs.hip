@@ -1,0 +1,428 @@
+// dpe_mvs.hip — the C-ABI library (include/dpe_mvs.h): context, HBM staging and the launch
+// sequence of one PatchMatch pass on gfx950.
+//
+// Replaces DPE::CudaSpaceInitialization / SetDataPassHelperInCuda / RunPatchMatch / getters
+// (DPE.cpp:916-1121, DPE.cu:3126-3249).  Differences by design:
+//   * no per-launch cudaDeviceSynchronize: the 26 launches are queued on one stream;
+//   * device buffers persist in the context across passes (resized only when W/H/N grow);
+//   * the bilinear texture path is a padded quad-texel image in HBM (one 16-B load per tap);
+//   * cuRAND states (48 B/px + curand_init) are replaced by counter-based Philox;
+//   * errors are return codes (no exit()).
+#include <hip/hip_runtime.h>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "pass_kernels.h"
+
+using namespace dpe;
+
+namespace {
+
+thread_local std::string g_err;
+
+#define HIPC(expr)                                                                  \
+  do {                                                                              \
+    hipError_t e_ = (expr);                                                         \
+    if (e_ != hipSuccess) {                                                         \
+      g_err = std::string(#expr) + ": " + hipGetErrorString(e_);                    \
+      return DPE_ERR_HIP;                                                           \
+    }                                                                               \
+  } while (0)
+
+template <class T>
+struct DevArr {
+  T* p = nullptr;
+  size_t n = 0;
+  hipError_t ensure(size_t count) {
+    if (count <= n && p) return hipSuccess;
+    if (p) { hipFree(p); p = nullptr; n = 0; }
+    hipError_t e = hipMalloc((void**)&p, count * sizeof(T) + 256);
+    if (e == hipSuccess) n = count;
+    return e;
+  }
+  void release() { if (p) hipFree(p); p = nullptr; n = 0; }
+};
+
+}  // namespace
+
+struct DpeContext {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool staged = false;
+  bool timing = false;
+  float timings[8] = {0};
+  hipEvent_t ev[48] = {};
+  PassConst hc;                  // host copy of the pass constants
+  DevArr<PassConst> dc;
+  // inputs
+  DevArr<float> img_plain[DPE_MAX_IMAGES];  // plain f32 images (ref used directly)
+  DevArr<float4> imgq[DPE_MAX_IMAGES];
+  DevArr<float> depth[DPE_MAX_IMAGES];
+  DevArr<uint8_t> edge, edge_low;
+  DevArr<int> label;
+  // staged initial state
+  DevArr<float4> planes0;
+  DevArr<uint8_t> weak0;
+  DevArr<uint32_t> sel0;
+  // working state
+  DevArr<float4> planes, planes_snap, fit_plane;
+  DevArr<float> costs, costs_snap, complex_;
+  DevArr<uint32_t> sel, sel_snap;
+  DevArr<uint8_t> weak, weak_rel, vw;
+  DevArr<short2> nb, nearest, edge_neigh, lab_bound;
+  DevArr<int> radius;
+  DevBufs bufs;
+};
+
+extern "C" {
+
+void dpe_params_default(DpePatchMatchParams* p) {   // main.h:78-106
+  p->max_iterations = 3;
+  p->num_images = 5;
+  p->sigma_spatial = 5.0f;
+  p->sigma_color = 3.0f;
+  p->top_k = 4;
+  p->depth_min = 0.0f;
+  p->depth_max = 1.0f;
+  p->geom_consistency = false;
+  p->strong_radius = 5;
+  p->strong_increment = 2;
+  p->weak_radius = 5;
+  p->weak_increment = 5;
+  p->use_APD = true;
+  p->use_edge = true;
+  p->use_limit = true;
+  p->use_label = true;
+  p->use_radius = true;
+  p->high_res_img = true;
+  p->max_scale_size = 1;
+  p->scale_size = 1;
+  p->weak_peak_radius = 2;
+  p->rotate_time = 4;
+  p->ransac_threshold = 0.005f;
+  p->geom_factor = 0.2f;
+  p->state = DPE_FIRST_INIT;
+}
+
+const char* dpe_last_error(void) { return g_err.c_str(); }
+
+DpeContext* dpe_create(int device) {
+  g_err.clear();
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) {
+    g_err = "dpe_create: no such HIP device";
+    return nullptr;
+  }
+  if (hipSetDevice(device) != hipSuccess) { g_err = "dpe_create: hipSetDevice failed"; return nullptr; }
+  DpeContext* c = new DpeContext();
+  c->device = device;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    g_err = "dpe_create: stream"; delete c; return nullptr;
+  }
+  for (auto& e : c->ev) hipEventCreate(&e);
+  return c;
+}
+
+void dpe_destroy(DpeContext* c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  hipStreamSynchronize(c->stream);
+  for (auto& e : c->ev) hipEventDestroy(e);
+  c->dc.release();
+  for (int i = 0; i < DPE_MAX_IMAGES; ++i) { c->img_plain[i].release(); c->imgq[i].release(); c->depth[i].release(); }
+  c->edge.release(); c->edge_low.release(); c->label.release();
+  c->planes0.release(); c->weak0.release(); c->sel0.release();
+  c->planes.release(); c->planes_snap.release(); c->fit_plane.release();
+  c->costs.release(); c->costs_snap.release(); c->complex_.release();
+  c->sel.release(); c->sel_snap.release();
+  c->weak.release(); c->weak_rel.release(); c->vw.release();
+  c->nb.release(); c->nearest.release(); c->edge_neigh.release(); c->lab_bound.release();
+  c->radius.release();
+  hipStreamDestroy(c->stream);
+  delete c;
+}
+
+void dpe_set_timing(DpeContext* c, int enable) { if (c) c->timing = enable != 0; }
+
+}  // extern "C"
+
+// Per-pass constants (restatement of ComputeHomography's plane-independent part, DPE.cu:455-512,
+// evaluated in double and rounded once; GenNeighbours' angle constants, DPE.cu:2147-2152).
+static void compute_pass_constants(PassConst& pc) {
+  const DpeCamera& rc = pc.cams[0];
+  const double rK0 = rc.K[0], rK2 = rc.K[2], rK4 = rc.K[4], rK5 = rc.K[5];
+  double refC[3];
+  for (int j = 0; j < 3; ++j)
+    refC[j] = -((double)rc.R[0 + j] * rc.t[0] + (double)rc.R[3 + j] * rc.t[1] + (double)rc.R[6 + j] * rc.t[2]);
+  for (int v = 1; v < pc.N; ++v) {
+    const DpeCamera& sc = pc.cams[v];
+    double srcC[3], Rrel[9], Crel[3], trel[3], T[9];
+    for (int j = 0; j < 3; ++j)
+      srcC[j] = -((double)sc.R[0 + j] * sc.t[0] + (double)sc.R[3 + j] * sc.t[1] + (double)sc.R[6 + j] * sc.t[2]);
+    for (int r = 0; r < 3; ++r)
+      for (int c = 0; c < 3; ++c)
+        Rrel[r * 3 + c] = (double)sc.R[r * 3 + 0] * rc.R[c * 3 + 0] + (double)sc.R[r * 3 + 1] * rc.R[c * 3 + 1] +
+                          (double)sc.R[r * 3 + 2] * rc.R[c * 3 + 2];
+    for (int j = 0; j < 3; ++j) Crel[j] = refC[j] - srcC[j];
+    for (int r = 0; r < 3; ++r)
+      trel[r] = (double)sc.R[r * 3 + 0] * Crel[0] + (double)sc.R[r * 3 + 1] * Crel[1] + (double)sc.R[r * 3 + 2] * Crel[2];
+    for (int r = 0; r < 3; ++r) {
+      T[r * 3 + 0] = Rrel[r * 3 + 0] / rK0;
+      T[r * 3 + 1] = Rrel[r * 3 + 1] / rK4;
+      T[r * 3 + 2] = -Rrel[r * 3 + 0] * rK2 / rK0 - Rrel[r * 3 + 1] * rK5 / rK4 + Rrel[r * 3 + 2];
+    }
+    const double sK0 = sc.K[0], sK2 = sc.K[2], sK4 = sc.K[4], sK5 = sc.K[5], sK8 = sc.K[8];
+    for (int c = 0; c < 3; ++c) {
+      pc.vc[v].M[0 + c] = (float)(sK0 * T[0 + c] + sK2 * T[6 + c]);
+      pc.vc[v].M[3 + c] = (float)(sK4 * T[3 + c] + sK5 * T[6 + c]);
+      pc.vc[v].M[6 + c] = (float)(sK8 * T[6 + c]);
+    }
+    pc.vc[v].b[0] = (float)(sK0 * trel[0] + sK2 * trel[2]);
+    pc.vc[v].b[1] = (float)(sK4 * trel[1] + sK5 * trel[2]);
+    pc.vc[v].b[2] = (float)(sK8 * trel[2]);
+  }
+  pc.kinv0 = (float)(1.0 / rK0);
+  pc.kinv4 = (float)(1.0 / rK4);
+  pc.kc2 = (float)(rK2 / rK0);
+  pc.kc5 = (float)(rK5 / rK4);
+  const float angle = 45.0f / pc.P.rotate_time;
+  pc.gn_cos = (float)cos((double)angle * M_PI / 180.f);
+  pc.gn_sin = (float)sin((double)angle * M_PI / 180.f);
+  pc.gn_thr = (float)cos((double)(angle / 2.0f) * M_PI / 180.0f);
+  const double sr = tan((double)(angle / 2.0f) * M_PI / 180.0f) * 20;
+  const int sri = (sr != sr) ? 0 : (int)sr;
+  pc.gn_shift = sri < 1 ? 1 : sri;
+  pc.half_rows = std::min(pc.H, 2 * 16 * (((pc.H / 2) + 15) / 16));
+}
+
+extern "C" int dpe_pm_stage(DpeContext* c, const DpePassInput* in, const DpePassState* st) {
+  g_err.clear();
+  if (!c || !in || !st || !in->images || !in->cams || !st->planes || !st->weak_info || !st->selected_views) {
+    g_err = "dpe_pm_stage: null argument"; return DPE_ERR_ARG;
+  }
+  if (in->num_images > DPE_MAX_IMAGES) { g_err = "dpe_pm_stage: num_images > 32 (DPE.cpp:762)"; return DPE_ERR_TOO_MANY; }
+  if (in->num_images < 2 || in->width <= 0 || in->height <= 0) { g_err = "dpe_pm_stage: bad shape"; return DPE_ERR_ARG; }
+  if (in->width > 32000 || in->height > 32000) { g_err = "dpe_pm_stage: image too large for short2 coordinates"; return DPE_ERR_ARG; }
+  const DpePatchMatchParams& P = in->params;
+  if (P.rotate_time < 1 || P.rotate_time > 4) { g_err = "dpe_pm_stage: rotate_time must be in [1,4]"; return DPE_ERR_ARG; }
+  if (P.strong_increment <= 0 || P.weak_increment <= 0) { g_err = "dpe_pm_stage: increments must be > 0"; return DPE_ERR_ARG; }
+  for (int i = 0; i < in->num_images; ++i) if (!in->images[i]) { g_err = "dpe_pm_stage: missing image"; return DPE_ERR_ARG; }
+  if (P.geom_consistency) {
+    if (!in->depths) { g_err = "dpe_pm_stage: geom_consistency needs depths"; return DPE_ERR_ARG; }
+    for (int i = 1; i < in->num_images; ++i) if (!in->depths[i]) { g_err = "dpe_pm_stage: missing source depth"; return DPE_ERR_ARG; }
+  }
+  if ((P.use_edge || P.use_limit) && (!in->edge || !in->edge_low_res || in->low_width <= 0 || in->low_height <= 0)) {
+    g_err = "dpe_pm_stage: use_edge/use_limit need edge and edge_low_res"; return DPE_ERR_ARG;
+  }
+  if (P.use_label && !in->label) { g_err = "dpe_pm_stage: use_label needs label"; return DPE_ERR_ARG; }
+  HIPC(hipSetDevice(c->device));
+  const int W = in->width, H = in->height, N = in->num_images;
+  const size_t L = (size_t)W * H;
+  PassConst& pc = c->hc;
+  std::memset(&pc, 0, sizeof(pc));
+  pc.W = W; pc.H = H; pc.N = N;
+  pc.P = P; pc.P.num_images = N;
+  pc.seed32 = (uint32_t)in->seed ^ (uint32_t)(in->seed >> 32);
+  pc.salt = in->pass_salt;
+  for (int i = 0; i < N; ++i) pc.cams[i] = in->cams[i];
+  compute_pass_constants(pc);
+  HIPC(c->dc.ensure(1));
+  HIPC(hipMemcpyAsync(c->dc.p, &pc, sizeof(PassConst), hipMemcpyHostToDevice, c->stream));
+
+  DevBufs& B = c->bufs;
+  std::memset(&B, 0, sizeof(B));
+  const dim3 qb(16, 16), qg((W + 2 + 15) / 16, (H + 2 + 15) / 16);
+  for (int i = 0; i < N; ++i) {
+    HIPC(c->img_plain[i].ensure(L));
+    HIPC(c->imgq[i].ensure((size_t)(W + 2) * (H + 2)));
+    HIPC(hipMemcpyAsync(c->img_plain[i].p, in->images[i], L * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    k_build_quad<<<qg, qb, 0, c->stream>>>(c->img_plain[i].p, c->imgq[i].p, W, H);
+    HIPC(hipGetLastError());
+    B.imgq[i] = c->imgq[i].p;
+  }
+  B.ref = c->img_plain[0].p;
+  if (P.geom_consistency) {
+    for (int i = 1; i < N; ++i) {
+      HIPC(c->depth[i].ensure(L));
+      HIPC(hipMemcpyAsync(c->depth[i].p, in->depths[i], L * sizeof(float), hipMemcpyHostToDevice, c->stream));
+      B.depth[i] = c->depth[i].p;
+    }
+  }
+  if (P.use_edge || P.use_limit) {
+    pc.LW = in->low_width; pc.LH = in->low_height;
+    HIPC(c->edge.ensure(L));
+    HIPC(c->edge_low.ensure((size_t)pc.LW * pc.LH));
+    HIPC(hipMemcpyAsync(c->edge.p, in->edge, L, hipMemcpyHostToDevice, c->stream));
+    HIPC(hipMemcpyAsync(c->edge_low.p, in->edge_low_res, (size_t)pc.LW * pc.LH, hipMemcpyHostToDevice, c->stream));
+    B.edge = c->edge.p; B.edge_low = c->edge_low.p;
+    HIPC(hipMemcpyAsync(c->dc.p, &pc, sizeof(PassConst), hipMemcpyHostToDevice, c->stream));
+  }
+  if (P.use_label) {
+    HIPC(c->label.ensure(L));
+    HIPC(hipMemcpyAsync(c->label.p, in->label, L * sizeof(int), hipMemcpyHostToDevice, c->stream));
+    B.label = c->label.p;
+  }
+  HIPC(c->planes0.ensure(L)); HIPC(c->weak0.ensure(L)); HIPC(c->sel0.ensure(L));
+  HIPC(hipMemcpyAsync(c->planes0.p, st->planes, L * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+  if (P.use_APD) HIPC(hipMemcpyAsync(c->weak0.p, st->weak_info, L, hipMemcpyHostToDevice, c->stream));
+  else HIPC(hipMemsetAsync(c->weak0.p, DPE_STRONG, L, c->stream));   // DPE.cpp:873-881
+  HIPC(hipMemcpyAsync(c->sel0.p, st->selected_views, L * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+  HIPC(c->planes.ensure(L)); HIPC(c->planes_snap.ensure(L)); HIPC(c->fit_plane.ensure(L));
+  HIPC(c->costs.ensure(L)); HIPC(c->costs_snap.ensure(L)); HIPC(c->complex_.ensure(L));
+  HIPC(c->sel.ensure(L)); HIPC(c->sel_snap.ensure(L));
+  HIPC(c->weak.ensure(L)); HIPC(c->weak_rel.ensure(L)); HIPC(c->vw.ensure(L * DPE_MAX_IMAGES));
+  HIPC(c->nb.ensure(L * 9)); HIPC(c->nearest.ensure(L)); HIPC(c->edge_neigh.ensure(L * 8)); HIPC(c->lab_bound.ensure(L * 8));
+  HIPC(c->radius.ensure(L));
+  B.planes = c->planes.p; B.planes_snap = c->planes_snap.p; B.fit_plane = c->fit_plane.p;
+  B.costs = c->costs.p; B.costs_snap = c->costs_snap.p; B.complex_ = c->complex_.p;
+  B.sel = c->sel.p; B.sel_snap = c->sel_snap.p;
+  B.weak = c->weak.p; B.weak_rel = c->weak_rel.p; B.vw = c->vw.p;
+  B.nb = c->nb.p; B.nearest = c->nearest.p; B.edge_neigh = c->edge_neigh.p; B.lab_bound = c->lab_bound.p;
+  B.radius = c->radius.p;
+  HIPC(hipStreamSynchronize(c->stream));
+  c->staged = true;
+  return DPE_OK;
+}
+
+extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
+  g_err.clear();
+  if (!c) { g_err = "dpe_pm_execute: null context"; return DPE_ERR_ARG; }
+  if (!c->staged) { g_err = "dpe_pm_execute: call dpe_pm_stage first"; return DPE_ERR_STATE; }
+  HIPC(hipSetDevice(c->device));
+  hipStream_t s = stream_ ? (hipStream_t)stream_ : c->stream;
+  const PassConst& pc = c->hc;
+  const DevBufs& B = c->bufs;
+  const PassConst* dpc = c->dc.p;
+  const int W = pc.W, H = pc.H, nv = pc.N - 1;
+  const size_t L = (size_t)W * H;
+  hipEvent_t* ev = c->ev;
+  int ei = 0;
+  const bool timing = c->timing && (5 + 4 * pc.P.max_iterations) <= 48;
+  auto mark = [&]() { if (timing) hipEventRecord(ev[ei++], s); };
+
+  mark();   // 0
+  // initial state (the reference uploads it in CudaSpaceInitialization, DPE.cpp:964-1015)
+  HIPC(hipMemcpyAsync(B.planes, c->planes0.p, L * sizeof(float4), hipMemcpyDeviceToDevice, s));
+  HIPC(hipMemcpyAsync(B.weak, c->weak0.p, L, hipMemcpyDeviceToDevice, s));
+  HIPC(hipMemcpyAsync(B.sel, c->sel0.p, L * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+  HIPC(hipMemsetAsync(B.costs, 0, L * sizeof(float), s));
+  HIPC(hipMemsetAsync(B.fit_plane, 0, L * sizeof(float4), s));
+  HIPC(hipMemsetAsync(B.complex_, 0, L * sizeof(float), s));
+  HIPC(hipMemsetAsync(B.weak_rel, 0, L, s));
+  HIPC(hipMemsetAsync(B.vw, 0, L * DPE_MAX_IMAGES, s));
+  HIPC(hipMemsetAsync(B.nb, 0xFF, L * 9 * sizeof(short2), s));
+  HIPC(hipMemsetAsync(B.nearest, 0xFF, L * sizeof(short2), s));
+  HIPC(hipMemsetAsync(B.edge_neigh, 0xFF, L * 8 * sizeof(short2), s));
+  HIPC(hipMemsetAsync(B.lab_bound, 0xFF, L * 8 * sizeof(short2), s));
+  HIPC(hipMemsetAsync(B.radius, 0, L * sizeof(int), s));
+
+  const dim3 fb(16, 16), fg((W + 15) / 16, (H + 15) / 16);
+  const dim3 hb(32, 4), hg((((W + 1) / 2) + 31) / 32, (pc.half_rows + 3) / 4);
+  const size_t sweep_lds = (size_t)10 * nv * 128 * sizeof(float) + (size_t)nv * 128;
+  const size_t d2w_lds = (size_t)61 * 256 * sizeof(float);
+
+  k_gen_edge_inform<<<fg, fb, 0, s>>>(dpc, B);
+  k_find_nearest_strong<<<fg, fb, 0, s>>>(dpc, B);
+  k_gen_neighbours<<<fg, fb, 0, s>>>(dpc, B);
+  k_neighbour_update<<<fg, fb, 0, s>>>(dpc, B);
+  k_random_init<<<fg, fb, 0, s>>>(dpc, B);
+  HIPC(hipGetLastError());
+  mark();   // 1: setup done
+  float t_strong = 0, t_weak = 0, t_ransac = 0;
+  for (int it = 0; it < pc.P.max_iterations; ++it) {
+    const int e0 = ei; mark();
+    for (int colour = 0; colour < 2; ++colour) {
+      HIPC(hipMemcpyAsync(B.planes_snap, B.planes, L * sizeof(float4), hipMemcpyDeviceToDevice, s));
+      HIPC(hipMemcpyAsync(B.costs_snap, B.costs, L * sizeof(float), hipMemcpyDeviceToDevice, s));
+      HIPC(hipMemcpyAsync(B.sel_snap, B.sel, L * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+      k_strong_sweep<<<hg, hb, sweep_lds, s>>>(dpc, B, it, colour);
+    }
+    HIPC(hipGetLastError());
+    mark();
+    k_ransac_fit<<<fg, fb, 0, s>>>(dpc, B, it);
+    mark();
+    for (int colour = 0; colour < 2; ++colour) k_weak_sweep<<<hg, hb, sweep_lds, s>>>(dpc, B, it, colour);
+    HIPC(hipGetLastError());
+    mark();
+    (void)e0;
+  }
+  k_depth_normal<<<fg, fb, 0, s>>>(dpc, B);
+  for (int colour = 0; colour < 2; ++colour) k_filter<<<hg, hb, 0, s>>>(dpc, B, colour);
+  mark();
+  k_depth_to_weak<<<fg, fb, d2w_lds, s>>>(dpc, B);
+  mark();
+  k_local_refine<<<fg, fb, 0, s>>>(dpc, B);
+  mark();
+  HIPC(hipGetLastError());
+  if (timing) {
+    HIPC(hipEventSynchronize(ev[ei - 1]));
+    float t;
+    auto el = [&](int a, int b) { float ms = 0; hipEventElapsedTime(&ms, ev[a], ev[b]); return ms; };
+    t = el(0, ei - 1); c->timings[0] = t;
+    c->timings[5] = el(0, 1);
+    int k = 2;
+    for (int it = 0; it < pc.P.max_iterations; ++it) {
+      t_strong += el(k, k + 1); t_ransac += el(k + 1, k + 2); t_weak += el(k + 2, k + 3);
+      k += 4;
+    }
+    // k now points one past the last iteration's final mark
+    const int base = 2 + 4 * pc.P.max_iterations - 1;
+    c->timings[1] = t_strong; c->timings[2] = t_weak; c->timings[6] = t_ransac;
+    c->timings[7] = el(base, base + 1);
+    c->timings[3] = el(base + 1, base + 2);
+    c->timings[4] = el(base + 2, base + 3);
+  }
+  return DPE_OK;
+}
+
+extern "C" int dpe_pm_fetch(DpeContext* c, const DpePassState* st) {
+  g_err.clear();
+  if (!c || !st) { g_err = "dpe_pm_fetch: null argument"; return DPE_ERR_ARG; }
+  if (!c->staged) { g_err = "dpe_pm_fetch: nothing staged"; return DPE_ERR_STATE; }
+  HIPC(hipSetDevice(c->device));
+  const size_t L = (size_t)c->hc.W * c->hc.H;
+  HIPC(hipStreamSynchronize(c->stream));
+  HIPC(hipDeviceSynchronize());
+  if (st->planes) HIPC(hipMemcpy(st->planes, c->bufs.planes, L * sizeof(float4), hipMemcpyDeviceToHost));
+  if (st->weak_info) HIPC(hipMemcpy(st->weak_info, c->bufs.weak, L, hipMemcpyDeviceToHost));
+  if (st->selected_views) HIPC(hipMemcpy(st->selected_views, c->bufs.sel, L * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  if (st->costs) HIPC(hipMemcpy(st->costs, c->bufs.costs, L * sizeof(float), hipMemcpyDeviceToHost));
+  return DPE_OK;
+}
+
+extern "C" int dpe_pm_run(DpeContext* c, const DpePassInput* in, const DpePassState* st) {
+  int r = dpe_pm_stage(c, in, st);
+  if (r) return r;
+  r = dpe_pm_execute(c, nullptr);
+  if (r) return r;
+  return dpe_pm_fetch(c, st);
+}
+
+extern "C" void* dpe_pm_device_planes(DpeContext* c) { return (c && c->staged) ? (void*)c->bufs.planes : nullptr; }
+
+__global__ void k_export_depth(const float4* __restrict__ p, float* __restrict__ d, size_t L) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < L) d[i] = p[i].w;
+}
+
+extern "C" int dpe_pm_export_depth(DpeContext* c, float* dev_dst, void* stream_) {
+  g_err.clear();
+  if (!c || !dev_dst) { g_err = "dpe_pm_export_depth: null argument"; return DPE_ERR_ARG; }
+  if (!c->staged) { g_err = "dpe_pm_export_depth: nothing staged"; return DPE_ERR_STATE; }
+  HIPC(hipSetDevice(c->device));
+  hipStream_t s = stream_ ? (hipStream_t)stream_ : c->stream;
+  const size_t L = (size_t)c->hc.W * c->hc.H;
+  k_export_depth<<<(unsigned)((L + 255) / 256), 256, 0, s>>>(c->bufs.planes, dev_dst, L);
+  HIPC(hipGetLastError());
+  return DPE_OK;
+}
+
+extern "C" int dpe_pm_last_timings(DpeContext* c, float* out, int n) {
+  if (!c || !out) return 0;
+  const int m = n < 8 ? n : 8;
+  for (int i = 0; i < m; ++i) out[i] = c->timings[i];
+  return m;
+}

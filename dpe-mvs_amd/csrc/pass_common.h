@@ -1,0 +1,450 @@
+// pass_common.h — device-side data model and shared device functions of the PatchMatch pass.
+//
+// HBM layout (one reference image, pass resolution W x H, L = W*H, N images):
+//   imgq[v]     float4 [(H+2)*(W+2)]  padded quad-texel image: element (X,Y) holds the four texels
+//                                     (X-1,Y-1),(X,Y-1),(X-1,Y),(X,Y) with clamp -> one 16-B load per
+//                                     bilinear tap (replaces the CUDA texture unit, DPE.cpp:919-935)
+//   ref         f32 [L]               reference grey levels (exact texels, DPE.cu:585/722/734)
+//   depth[v]    f32 [L]               source depth maps for the geometric term (DPE.cpp:826-843)
+//   planes      float4 [L]            (n, d) hypotheses; snapshot copy for red/black reads
+//   costs, sel  f32/u32 [L]           + snapshots
+//   weak        u8 [L]                PixelState
+//   vw          u8 [L*32]             view weights of the last sweep (DPE.cu:1548)
+//   nb          short2 [L*9]          deformable neighbours, per pixel (reference: compacted by
+//                                     neighbours_map, DPE.cpp:859-870; per-pixel costs 36 B/px
+//                                     of the 288 GB and removes one indirection)
+//   nearest, edge_neigh[8], lab_bound[8] short2 per pixel; complex f32, radius i32, fit float4
+#pragma once
+#include "device_math.h"
+#include "../../include/dpe_mvs.h"
+
+namespace dpe {
+
+struct ViewConst { float M[9]; float b[3]; };
+
+struct PassConst {
+  int W, H, N, LW, LH;
+  int half_rows;             // rows visited by the red/black grids (DPE.cu:3143)
+  uint32_t seed32, salt;
+  float kinv0, kinv4, kc2, kc5;
+  float gn_cos, gn_sin, gn_thr;
+  int gn_shift;
+  DpePatchMatchParams P;
+  DpeCamera cams[DPE_MAX_IMAGES];
+  ViewConst vc[DPE_MAX_IMAGES];
+};
+
+struct DevBufs {
+  const float4* imgq[DPE_MAX_IMAGES];
+  const float* depth[DPE_MAX_IMAGES];
+  const float* ref;
+  float4* planes; float4* planes_snap; float4* fit_plane;
+  float* costs; float* costs_snap; float* complex_;
+  uint32_t* sel; uint32_t* sel_snap;
+  uint8_t* weak; uint8_t* weak_rel; uint8_t* vw;
+  short2* nb; short2* nearest; short2* edge_neigh; short2* lab_bound;
+  int* radius;
+  const uint8_t* edge; const uint8_t* edge_low; const int* label;
+};
+
+// ------------------------------------------------------------------------------ bits
+DEV void setBit(uint32_t& v, unsigned n) { v |= (1u << n); }
+DEV void unSetBit(uint32_t& v, unsigned n) { v &= (0xFFFFFFFEu << n); }   // clears bits 0..n (DPE.cu:77-80)
+DEV int isSet(uint32_t v, unsigned n) { return (v >> n) & 1; }
+
+// ------------------------------------------------------------------------------ geometry
+DEV void normalize3(float4& v) {
+  const float n2 = v.x * v.x + v.y * v.y + v.z * v.z;
+  const float inv = d_rsqrtf(n2);
+  v.x *= inv; v.y *= inv; v.z *= inv;
+}
+DEV void normalize2(float2& v) {
+  const float n2 = v.x * v.x + v.y * v.y;
+  const float inv = d_rsqrtf(n2);
+  v.x *= inv; v.y *= inv;
+}
+DEV void get3d(const DpeCamera& c, int px, int py, float depth, float X[3]) {
+  X[0] = depth * ((float)px - c.K[2]) / c.K[0];
+  X[1] = depth * ((float)py - c.K[5]) / c.K[4];
+  X[2] = depth;
+}
+DEV float4 view_direction(const DpeCamera& c, int px, int py, float depth) {
+  float X[3]; get3d(c, px, py, depth, X);
+  const float norm = __builtin_sqrtf(X[0] * X[0] + X[1] * X[1] + X[2] * X[2]);
+  return make_float4(X[0] / norm, X[1] / norm, X[2] / norm, 0.0f);
+}
+DEV float dist2origin(const DpeCamera& c, int px, int py, float depth, const float4& n) {
+  float X[3]; get3d(c, px, py, depth, X);
+  return -(n.x * X[0] + n.y * X[1] + n.z * X[2]);
+}
+DEV float depth_from_plane(const DpeCamera& c, const float4& pl, int px, int py) {
+  return -pl.w * c.K[0] / (((float)px - c.K[2]) * pl.x + (c.K[0] / c.K[4]) * ((float)py - c.K[5]) * pl.y + c.K[0] * pl.z);
+}
+DEV float4 transform_normal(const DpeCamera& c, const float4& p) {      // R^T n (DPE.cu:524-532)
+  return make_float4(c.R[0] * p.x + c.R[3] * p.y + c.R[6] * p.z,
+                     c.R[1] * p.x + c.R[4] * p.y + c.R[7] * p.z,
+                     c.R[2] * p.x + c.R[5] * p.y + c.R[8] * p.z, p.w);
+}
+DEV float4 transform_normal_ref(const DpeCamera& c, const float4& p) {  // R n (DPE.cu:534-542)
+  return make_float4(c.R[0] * p.x + c.R[1] * p.y + c.R[2] * p.z,
+                     c.R[3] * p.x + c.R[4] * p.y + c.R[5] * p.z,
+                     c.R[6] * p.x + c.R[7] * p.y + c.R[8] * p.z, p.w);
+}
+DEV float3 world_point(float x, float y, float depth, const DpeCamera& c) {   // DPE.cu:881-901
+  float3 X, T;
+  X.x = depth * (x - c.K[2]) / c.K[0];
+  X.y = depth * (y - c.K[5]) / c.K[4];
+  X.z = depth;
+  T.x = c.R[0] * X.x + c.R[3] * X.y + c.R[6] * X.z;
+  T.y = c.R[1] * X.x + c.R[4] * X.y + c.R[7] * X.z;
+  T.z = c.R[2] * X.x + c.R[5] * X.y + c.R[8] * X.z;
+  return make_float3(T.x + c.c[0], T.y + c.c[1], T.z + c.c[2]);
+}
+DEV float2 project_cam(const float3& X, const DpeCamera& c) {                 // DPE.cu:903-913
+  const float tx = c.R[0] * X.x + c.R[1] * X.y + c.R[2] * X.z + c.t[0];
+  const float ty = c.R[3] * X.x + c.R[4] * X.y + c.R[5] * X.z + c.t[1];
+  const float tz = c.R[6] * X.x + c.R[7] * X.y + c.R[8] * X.z + c.t[2];
+  const float d = c.K[6] * tx + c.K[7] * ty + c.K[8] * tz;
+  return make_float2((c.K[0] * tx + c.K[1] * ty + c.K[2] * tz) / d, (c.K[3] * tx + c.K[4] * ty + c.K[5] * tz) / d);
+}
+
+// GenerateRandomNormal (DPE.cu:361-387)
+DEV float4 random_normal(const DpeCamera& c, int px, int py, Rng& rs, float depth) {
+  float q1 = 1.0f, q2 = 1.0f, s = 2.0f;
+  while (s >= 1.0f) {
+    q1 = 2.0f * rng_uniform(rs) - 1.0f;
+    q2 = 2.0f * rng_uniform(rs) - 1.0f;
+    s = q1 * q1 + q2 * q2;
+  }
+  const float sq = __builtin_sqrtf(1.0f - s);
+  float4 n = make_float4(2.0f * q1 * sq, 2.0f * q2 * sq, 1.0f - 2.0f * s, 0.0f);
+  const float4 vd = view_direction(c, px, py, depth);
+  if (n.x * vd.x + n.y * vd.y + n.z * vd.z > 0.0f) { n.x = -n.x; n.y = -n.y; n.z = -n.z; }
+  normalize3(n);
+  return n;
+}
+// GeneratePerturbedNormal (DPE.cu:389-424)
+DEV float4 perturbed_normal(const DpeCamera& c, int px, int py, const float4& normal, Rng& rs, float pert) {
+  const float4 vd = view_direction(c, px, py, 1.0f);
+  const float a1 = (rng_uniform(rs) - 0.5f) * pert;
+  const float a2 = (rng_uniform(rs) - 0.5f) * pert;
+  const float a3 = (rng_uniform(rs) - 0.5f) * pert;
+  float s1, c1, s2, c2, s3, c3;
+  d_sincosf(a1, &s1, &c1); d_sincosf(a2, &s2, &c2); d_sincosf(a3, &s3, &c3);
+  const float R0 = c2 * c3, R1 = c3 * s1 * s2 - c1 * s3, R2 = s1 * s3 + c1 * c3 * s2;
+  const float R3 = c2 * s3, R4 = c1 * c3 + s1 * s2 * s3, R5 = c1 * s2 * s3 - c3 * s1;
+  const float R6 = -s2, R7 = c2 * s1, R8 = c1 * c2;
+  float4 np = make_float4(R0 * normal.x + R1 * normal.y + R2 * normal.z,
+                          R3 * normal.x + R4 * normal.y + R5 * normal.z,
+                          R6 * normal.x + R7 * normal.y + R8 * normal.z, normal.w);
+  if (np.x * vd.x + np.y * vd.y + np.z * vd.z >= 0.0f) np = normal;
+  normalize3(np);
+  return np;
+}
+
+// ------------------------------------------------------------------------------ homography
+// H = M_v - b_v g^T, g = Kref^-T (n/w) (restatement of ComputeHomography, DPE.cu:453-513).
+struct Homog { float h[9]; };
+DEV Homog make_homography(const PassConst& pc, int v, const float4& pl) {
+  const float iw = 1.0f / pl.w;
+  const float qx = pl.x * iw, qy = pl.y * iw, qz = pl.z * iw;
+  const float g0 = qx * pc.kinv0;
+  const float g1 = qy * pc.kinv4;
+  const float g2 = __builtin_fmaf(-qx, pc.kc2, __builtin_fmaf(-qy, pc.kc5, qz));
+  const ViewConst& vc = pc.vc[v];
+  Homog H;
+  H.h[0] = __builtin_fmaf(-vc.b[0], g0, vc.M[0]);
+  H.h[1] = __builtin_fmaf(-vc.b[0], g1, vc.M[1]);
+  H.h[2] = __builtin_fmaf(-vc.b[0], g2, vc.M[2]);
+  H.h[3] = __builtin_fmaf(-vc.b[1], g0, vc.M[3]);
+  H.h[4] = __builtin_fmaf(-vc.b[1], g1, vc.M[4]);
+  H.h[5] = __builtin_fmaf(-vc.b[1], g2, vc.M[5]);
+  H.h[6] = __builtin_fmaf(-vc.b[2], g0, vc.M[6]);
+  H.h[7] = __builtin_fmaf(-vc.b[2], g1, vc.M[7]);
+  H.h[8] = __builtin_fmaf(-vc.b[2], g2, vc.M[8]);
+  return H;
+}
+DEV float2 project_h(const Homog& H, float x, float y) {   // ComputeCorrespondingPoint (DPE.cu:515-522)
+  const float px = __builtin_fmaf(H.h[1], y, __builtin_fmaf(H.h[0], x, H.h[2]));
+  const float py = __builtin_fmaf(H.h[4], y, __builtin_fmaf(H.h[3], x, H.h[5]));
+  const float pz = __builtin_fmaf(H.h[7], y, __builtin_fmaf(H.h[6], x, H.h[8]));
+  const float iz = 1.0f / pz;
+  return make_float2(px * iz, py * iz);
+}
+
+// ------------------------------------------------------------------------------ sampling
+DEV float ref_texel(const float* ref, int W, int H, int x, int y) {
+  x = x < 0 ? 0 : (x > W - 1 ? W - 1 : x);
+  y = y < 0 ? 0 : (y > H - 1 ? H - 1 : y);
+  return ref[y * W + x];
+}
+// Bilinear sample with 8-bit weights on the padded quad image (see oracle OracleSample).
+DEV float sample_quad(const float4* __restrict__ q, int W, int H, float sx, float sy) {
+  const float xb = __builtin_fminf(__builtin_fmaxf(sx, -1.0f), (float)W);
+  const float yb = __builtin_fminf(__builtin_fmaxf(sy, -1.0f), (float)H);
+  const int ux = (int)__builtin_fmaf(xb, 256.0f, 256.5f);
+  const int uy = (int)__builtin_fmaf(yb, 256.0f, 256.5f);
+  const float ax = (float)(ux & 255) * 0.00390625f;
+  const float ay = (float)(uy & 255) * 0.00390625f;
+  const float4 t = q[(uy >> 8) * (W + 2) + (ux >> 8)];
+  const float r0 = __builtin_fmaf(ax, t.y - t.x, t.x);
+  const float r1 = __builtin_fmaf(ax, t.w - t.z, t.z);
+  return __builtin_fmaf(ay, r1 - r0, r0);
+}
+DEV float depth_texel(const float* d, int W, int H, float x, float y) {   // DPE.cu:936
+  return ref_texel(d, W, H, f2i(x), f2i(y));
+}
+
+// ComputeBilateralWeight (DPE.cu:550-555)
+DEV float bilateral_weight(int i, int j, float pix, float cpix, float ss, float sc) {
+  const float xd = (float)i, yd = (float)j;
+  const float sd = __builtin_sqrtf(xd * xd + yd * yd);
+  const float cd = __builtin_fabsf(pix - cpix);
+  return d_expf(-sd / (2.0f * ss * ss) - cd / (2.0f * sc * sc));
+}
+
+DEV float ncc_finalize(float s_ref, float s_rr, float s_w, float s_src, float s_ss, float s_rs) {
+  const float inv = 1.0f / s_w;
+  s_ref *= inv; s_rr *= inv; s_src *= inv; s_ss *= inv; s_rs *= inv;
+  const float var_ref = s_rr - s_ref * s_ref;
+  const float var_src = s_ss - s_src * s_src;
+  if (var_ref < 1e-5f || var_src < 1e-5f) return 2.0f;
+  const float cov = s_rs - s_ref * s_src;
+  const float vrs = __builtin_sqrtf(var_ref * var_src);
+  return __builtin_fmaxf(0.0f, __builtin_fminf(2.0f, 1.0f - cov / vrs));
+}
+
+// Generic bilateral NCC of one patch, weights computed per tap (NCC-New neighbour patches and
+// non-default radius/increment).  Same arithmetic order as the oracle's PatchNCC.
+DEV float patch_ncc_generic(const PassConst& pc, const DevBufs& B, const float4* __restrict__ src, const Homog& H,
+                            int cx, int cy, float rcp, int radius, int increment) {
+  const int W = pc.W, Hh = pc.H;
+  const float ss = pc.P.sigma_spatial, sc = pc.P.sigma_color;
+  float s_ref = 0, s_rr = 0, s_src = 0, s_ss = 0, s_rs = 0, s_w = 0;
+  for (int i = -radius; i <= radius; i += increment) {
+    float r_ref = 0, r_src = 0, r_rr = 0, r_ss = 0, r_rs = 0, r_w = 0;
+    const int x = cx + i;
+    for (int j = -radius; j <= radius; j += increment) {
+      const int y = cy + j;
+      const float rp = ref_texel(B.ref, W, Hh, x, y);
+      const float2 sp_ = project_h(H, (float)x, (float)y);
+      const float sp = sample_quad(src, W, Hh, sp_.x, sp_.y);
+      const float w = bilateral_weight(i, j, rp, rcp, ss, sc);
+      const float wr = w * rp;
+      r_ref = r_ref + wr;
+      r_rr = __builtin_fmaf(wr, rp, r_rr);
+      r_src = __builtin_fmaf(w, sp, r_src);
+      const float ws = w * sp;
+      r_ss = __builtin_fmaf(ws, sp, r_ss);
+      r_rs = __builtin_fmaf(wr, sp, r_rs);
+      r_w = r_w + w;
+    }
+    s_ref += r_ref; s_rr += r_rr; s_src += r_src; s_ss += r_ss; s_rs += r_rs; s_w += r_w;
+  }
+  return ncc_finalize(s_ref, s_rr, s_w, s_src, s_ss, s_rs);
+}
+
+DEV bool center_outside(const PassConst& pc, int v, const Homog& H, int px, int py) {
+  const float2 pt = project_h(H, (float)px, (float)py);
+  const DpeCamera& sc = pc.cams[v];
+  return pt.x >= (float)sc.width || pt.x < 0.0f || pt.y >= (float)sc.height || pt.y < 0.0f;
+}
+
+// ComputeBilateralNCCOld (DPE.cu:692-778), weights per tap.
+DEV float ncc_old_generic(const PassConst& pc, const DevBufs& B, int px, int py, int v, const float4& pl) {
+  const Homog H = make_homography(pc, v, pl);
+  if (center_outside(pc, v, H, px, py)) return 2.0f;
+  const float rc = ref_texel(B.ref, pc.W, pc.H, px, py);
+  return patch_ncc_generic(pc, B, B.imgq[v], H, px, py, rc, pc.P.strong_radius, pc.P.strong_increment);
+}
+
+// Reference patch of the Old NCC with the default radius 5 / increment 2 (36 taps), precomputed
+// once per pixel: weights and weight*ref are view- and plane-independent.
+struct Patch36 {
+  float w[36], wr[36];
+  float s_ref, s_rr, s_w;
+  int px, py;
+};
+DEV void make_patch36(Patch36& P, const PassConst& pc, const DevBufs& B, int px, int py) {
+  const int W = pc.W, Hh = pc.H;
+  const float ss = pc.P.sigma_spatial, sc = pc.P.sigma_color;
+  const float rc = ref_texel(B.ref, W, Hh, px, py);
+  P.px = px; P.py = py;
+  float s_ref = 0, s_rr = 0, s_w = 0;
+#pragma unroll
+  for (int a = 0; a < 6; ++a) {
+    const int i = -5 + 2 * a;
+    float r_ref = 0, r_rr = 0, r_w = 0;
+#pragma unroll
+    for (int b = 0; b < 6; ++b) {
+      const int j = -5 + 2 * b;
+      const float rp = ref_texel(B.ref, W, Hh, px + i, py + j);
+      const float w = bilateral_weight(i, j, rp, rc, ss, sc);
+      const float wr = w * rp;
+      r_ref = r_ref + wr;
+      r_rr = __builtin_fmaf(wr, rp, r_rr);
+      r_w = r_w + w;
+      P.w[a * 6 + b] = w;
+      P.wr[a * 6 + b] = wr;
+    }
+    s_ref += r_ref; s_rr += r_rr; s_w += r_w;
+  }
+  P.s_ref = s_ref; P.s_rr = s_rr; P.s_w = s_w;
+}
+DEV float ncc_old_patch36(const Patch36& P, const PassConst& pc, const DevBufs& B, int v, const float4& pl) {
+  const Homog H = make_homography(pc, v, pl);
+  if (center_outside(pc, v, H, P.px, P.py)) return 2.0f;
+  const float4* __restrict__ src = B.imgq[v];
+  const int W = pc.W, Hh = pc.H;
+  float s_src = 0, s_ss = 0, s_rs = 0;
+#pragma unroll
+  for (int a = 0; a < 6; ++a) {
+    const float x = (float)(P.px - 5 + 2 * a);
+    const float bx = __builtin_fmaf(H.h[0], x, H.h[2]);
+    const float by = __builtin_fmaf(H.h[3], x, H.h[5]);
+    const float bz = __builtin_fmaf(H.h[6], x, H.h[8]);
+    float r_src = 0, r_ss = 0, r_rs = 0;
+#pragma unroll
+    for (int b = 0; b < 6; ++b) {
+      const float y = (float)(P.py - 5 + 2 * b);
+      const float qx = __builtin_fmaf(H.h[1], y, bx);
+      const float qy = __builtin_fmaf(H.h[4], y, by);
+      const float qz = __builtin_fmaf(H.h[7], y, bz);
+      const float iz = 1.0f / qz;
+      const float sp = sample_quad(src, W, Hh, qx * iz, qy * iz);
+      const float w = P.w[a * 6 + b], wr = P.wr[a * 6 + b];
+      r_src = __builtin_fmaf(w, sp, r_src);
+      const float ws = w * sp;
+      r_ss = __builtin_fmaf(ws, sp, r_ss);
+      r_rs = __builtin_fmaf(wr, sp, r_rs);
+    }
+    s_src += r_src; s_ss += r_ss; s_rs += r_rs;
+  }
+  return ncc_finalize(P.s_ref, P.s_rr, P.s_w, s_src, s_ss, s_rs);
+}
+
+// Old NCC through the cached patch when the pass uses the default 5/2 patch, else generic.
+DEV float ncc_old(const Patch36& P, bool fast, const PassConst& pc, const DevBufs& B, int v, const float4& pl) {
+  if (fast) return ncc_old_patch36(P, pc, B, v, pl);
+  return ncc_old_generic(pc, B, P.px, P.py, v, pl);
+}
+
+// ComputeBilateralNCCNew (DPE.cu:557-690)
+DEV float ncc_new(const PassConst& pc, const DevBufs& B, int px, int py, int v, const float4& pl) {
+  const int W = pc.W, Hh = pc.H;
+  const int center = px + py * W;
+  const Homog H = make_homography(pc, v, pl);
+  if (center_outside(pc, v, H, px, py)) return 2.0f;
+  float cost = 0.0f;
+  if (B.weak[center] != DPE_WEAK) return cost;
+  const float rc = ref_texel(B.ref, W, Hh, px, py);
+  float center_cost = 0.0f, strong_cost = 0.0f;
+  int strong_count = 0;
+  const short2* nb = B.nb + (size_t)center * 9;
+  for (int k = 0; k < DPE_NEIGHBOUR_NUM; ++k) {
+    const short2 np = nb[k];
+    if (np.x == -1 || np.y == -1) continue;
+    const float2 nsp = project_h(H, (float)np.x, (float)np.y);
+    if (nsp.x < 0 || nsp.y < 0 || nsp.x >= (float)W || nsp.y >= (float)Hh) {
+      if (k != 0) {
+        const uint32_t vi = B.sel[np.x + np.y * W];
+        if (isSet(vi, v - 1)) { strong_cost += 2.0f; strong_count++; }
+        continue;
+      }
+      return 2.0f;
+    }
+    int radius = (k == 0 ? pc.P.strong_radius : pc.P.weak_radius);
+    int increment = (k == 0 ? pc.P.strong_increment : pc.P.weak_increment);
+    if (pc.P.use_radius && k == 0) {
+      radius = B.radius[center];
+      increment = MAXo(2, d2i(2.0 * radius / 5.0));
+    }
+    const float tc = patch_ncc_generic(pc, B, B.imgq[v], H, np.x, np.y, rc, radius, increment);
+    if (k == 0) center_cost = tc;
+    else { strong_cost += tc; strong_count++; }
+  }
+  if (strong_count == 0) cost = center_cost;
+  else {
+    strong_cost /= (float)strong_count;
+    strong_cost = MINo(strong_cost, 2.0f);
+    cost = (float)(0.25 * (double)center_cost + 0.75 * (double)strong_cost);
+  }
+  return cost;
+}
+
+// ComputeGeomConsistencyCost (DPE.cu:915-953)
+DEV float geom_cost(const PassConst& pc, const DevBufs& B, int px, int py, int v, const float4& pl) {
+  const DpeCamera& rc = pc.cams[0];
+  const DpeCamera& sc = pc.cams[v];
+  const float depth = depth_from_plane(rc, pl, px, py);
+  const float3 fw = world_point((float)px, (float)py, depth, rc);
+  const float2 sp = project_cam(fw, sc);
+  const float src_depth = depth_texel(B.depth[v], pc.W, pc.H, sp.x, sp.y);
+  if (src_depth == 0.0f) return 3.0f;
+  const float3 s3 = world_point(sp.x, sp.y, src_depth, sc);
+  const float2 bp = project_cam(s3, rc);
+  const float dc = (float)px - bp.x, dr = (float)py - bp.y;
+  const float cc = __builtin_sqrtf(dc * dc + dr * dr);
+  return __builtin_fminf(3.0f, cc);
+}
+
+// ------------------------------------------------------------------------------ edges / triangles
+DEV uint8_t low_edge_at(const PassConst& pc, const DevBufs& B, int idx) {
+  if (idx < 0 || idx >= pc.LW * pc.LH) return 0;
+  return B.edge_low[idx];
+}
+// BresenhamLine (DPE.cu:158-244)
+DEV bool bresenham(const PassConst& pc, const DevBufs& B, int Ax, int Ay, int Bx, int By) {
+  const int W = pc.W;
+  if (B.edge[Ax + Ay * W] || B.edge[Bx + By * W]) return false;
+  const float scale_x = 1.0f * pc.LW / (float)pc.W;
+  const float scale_y = 1.0f * pc.LH / (float)pc.H;
+  const int height = pc.LH, width = pc.LW;
+  const int max_step = pc.P.high_res_img ? (int)__builtin_round(MAXo(height, width) / 60.0) : MAXo(height, width);
+  for (int pass = 0; pass < 2; ++pass) {
+    const int fx = pass == 0 ? Bx : Ax, fy = pass == 0 ? By : Ay;
+    const int tx = pass == 0 ? Ax : Bx, ty = pass == 0 ? Ay : By;
+    int x0 = (int)MINo(__builtin_roundf(fx * scale_x), (float)(width - 1));
+    int y0 = (int)MINo(__builtin_roundf(fy * scale_y), (float)(height - 1));
+    const int x1 = (int)MINo(__builtin_roundf(tx * scale_x), (float)(width - 1));
+    const int y1 = (int)MINo(__builtin_roundf(ty * scale_y), (float)(height - 1));
+    const int dx = abs(x1 - x0), sx = x0 < x1 ? 1 : -1;
+    const int dy = abs(y1 - y0), sy = y0 < y1 ? 1 : -1;
+    int erro = (dx > dy ? dx : dy) / 2;
+    int step = 0;
+    bool tagx = true, tagy = true;
+    while (tagx || tagy) {
+      if (x0 == x1) tagx = false;
+      if (y0 == y1) tagy = false;
+      const int e2 = erro;
+      if (e2 > -dx) { erro -= dy; x0 += sx; }
+      if (e2 < dy) { erro += dx; y0 += sy; }
+      if (low_edge_at(pc, B, x0 + y0 * width)) return true;
+      step += 1;
+      if (step >= max_step) break;
+    }
+  }
+  return false;
+}
+// PointinTriangle (DPE.cu:135-156)
+DEV bool point_in_triangle(short2 A, short2 Bp, short2 C, int Px, int Py) {
+  const float ABx = (float)(Bp.x - A.x), ABy = (float)(Bp.y - A.y);
+  const float BCx = (float)(C.x - Bp.x), BCy = (float)(C.y - Bp.y);
+  const float CAx = (float)(A.x - C.x), CAy = (float)(A.y - C.y);
+  const float AB_ = __builtin_sqrtf(ABx * ABx + ABy * ABy);
+  const float BC_ = __builtin_sqrtf(BCx * BCx + BCy * BCy);
+  const float CA_ = __builtin_sqrtf(CAx * CAx + CAy * CAy);
+  if (AB_ <= 2 || BC_ <= 2 || CA_ <= 2) return false;
+  if (!(AB_ + BC_ > CA_ && BC_ + CA_ > AB_ && AB_ + CA_ > BC_)) return false;
+  const float PAx = (float)(A.x - Px), PAy = (float)(A.y - Py);
+  const float PBx = (float)(Bp.x - Px), PBy = (float)(Bp.y - Py);
+  const float PCx = (float)(C.x - Px), PCy = (float)(C.y - Py);
+  const float t1 = PAx * PBy - PAy * PBx;
+  const float t2 = PBx * PCy - PBy * PCx;
+  const float t3 = PCx * PAy - PCy * PAx;
+  return t1 * t2 >= 0 && t1 * t3 >= 0;
+}
+
+__device__ __constant__ static const int kDir[8][2] = {{0, -1}, {0, 1}, {-1, 0}, {1, 0}, {-1, -1}, {1, 1}, {-1, 1}, {1, -1}};
+
+}  // namespace dpe

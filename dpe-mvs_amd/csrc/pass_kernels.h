@@ -1,0 +1,1199 @@
+// pass_kernels.h — the kernels of one PatchMatch pass (DPE::RunPatchMatch, DPE.cu:3126-3249).
+//
+// Launch structure: full-grid kernels run one thread per pixel on 16x16 workgroups; the red/black
+// sweeps run one thread per pixel of the colour on 32x4 workgroups (a wave covers two rows of 64
+// columns).  Per-pixel arrays that the reference keeps in registers/local memory
+// (cost_array[8][32], DPE.cu:1236/1690; p_costs[61], :2660) are staged in LDS, view-major with the
+// thread index fastest, so every access is bank-conflict free.  The 36-tap Old-NCC reference patch
+// (weights and weight*grey, view- and plane-independent) is computed once per pixel and kept in
+// registers for every NCC the pixel evaluates in that launch.
+#pragma once
+#include "pass_common.h"
+
+namespace dpe {
+
+#define PIX2D_FULL()                                                   \
+  const int x = blockIdx.x * blockDim.x + threadIdx.x;                 \
+  const int y = blockIdx.y * blockDim.y + threadIdx.y;                 \
+  if (x >= pc.W || y >= pc.H) return;                                  \
+  const int center = x + y * pc.W;
+
+// half-sweep pixel of colour `colour` (0 = black: (x+y) even, 1 = red), DPE.cu:1864-1938
+#define PIX2D_HALF()                                                   \
+  const int y = blockIdx.y * blockDim.y + threadIdx.y;                 \
+  const int x = 2 * (blockIdx.x * blockDim.x + threadIdx.x) + ((y + colour) & 1); \
+  if (x >= pc.W || y >= pc.H || y >= pc.half_rows) return;             \
+  const int center = x + y * pc.W;
+
+// ------------------------------------------------------------------------------ GenEdgeInform
+__global__ void k_gen_edge_inform(const PassConst* __restrict__ pcp, DevBufs B) {   // DPE.cu:2483-2591
+  const PassConst& pc = *pcp;
+  PIX2D_FULL();
+  const int W = pc.W, H = pc.H;
+  if (pc.P.use_edge) {
+    short2* en = B.edge_neigh + (size_t)center * 8;
+    for (int i = 0; i < 8; i++) {
+      short2 r = make_short2(-1, -1);
+      const int dx = kDir[i][0], dy = kDir[i][1];
+      int nx = x + dx, ny = y + dy;
+      while (true) {
+        if (nx < 0 || nx >= W || ny < 0 || ny >= H) break;
+        if (B.edge[nx + ny * W]) { r = make_short2((short)nx, (short)ny); break; }
+        nx += dx; ny += dy;
+      }
+      en[i] = r;
+    }
+    const int radius = pc.P.strong_radius;
+    int edge_pix = 0, tot_pix = 0, bound_pix = 0;
+    for (int i = -radius; i <= radius; i++)
+      for (int j = -radius; j <= radius; j++) {
+        const int nx = x + i, ny = y + j;
+        if (nx < 0 || nx >= W || ny < 0 || ny >= H) continue;
+        if (B.edge[ny * W + nx]) edge_pix++;
+        if (pc.P.use_label && B.label[ny * W + nx] == 0) bound_pix++;
+        tot_pix++;
+      }
+    float density = 1.0f * edge_pix / tot_pix;
+    if (pc.P.use_label) density = MAXo(density, (float)(bound_pix / tot_pix));   // integer division (:2551)
+    B.complex_[center] = (float)(1.0f / (1.0f + d_exp_d(-25.0 * ((double)density - 0.35))));
+  }
+  if (pc.P.use_label && B.weak[center] == DPE_WEAK) {
+    const int cl = B.label[center];
+    if (cl > 0) {
+      short2* lb = B.lab_bound + (size_t)center * 8;
+      for (int i = 0; i < 8; i++) {
+        const int dx = kDir[i][0], dy = kDir[i][1];
+        int nx = x + dx, ny = y + dy, lx = -1, ly = -1;
+        while (true) {
+          if (nx < 0 || nx >= W || ny < 0 || ny >= H) break;
+          const int nl = B.label[nx + ny * W];
+          if (nl == cl) { lx = nx; ly = ny; }
+          else if (nl == -1) break;
+          nx += dx; ny += dy;
+        }
+        lb[i] = make_short2((short)lx, (short)ly);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------ FindNearestStrongPoint
+__global__ void k_find_nearest_strong(const PassConst* __restrict__ pcp, DevBufs B) {   // DPE.cu:2855-2889
+  const PassConst& pc = *pcp;
+  PIX2D_FULL();
+  const int W = pc.W, H = pc.H;
+  short2 res = make_short2(-1, -1);
+  if (B.weak[center] == DPE_WEAK) {
+    bool found = false;
+    for (int r = 0; r <= 100 && !found; ++r)
+      for (int dx = -r; dx <= r && !found; ++dx) {
+        const int nx = x + dx;
+        if (nx < 0 || nx >= W) continue;
+        const bool edge_col = (dx == -r || dx == r);
+        // ring order: every y for the two edge columns, else only the top and bottom cells
+        for (int dy = -r; dy <= r; dy += (edge_col ? 1 : (r > 0 ? 2 * r : 1))) {
+          const int ny = y + dy;
+          if (ny < 0 || ny >= H) continue;
+          if (B.weak[nx + ny * W] == DPE_STRONG) { res = make_short2((short)nx, (short)ny); found = true; break; }
+        }
+      }
+  }
+  B.nearest[center] = res;
+}
+
+// ------------------------------------------------------------------------------ GenNeighbours
+__global__ void __launch_bounds__(256) k_gen_neighbours(const PassConst* __restrict__ pcp, DevBufs B) {   // DPE.cu:2103-2463
+  const PassConst& pc = *pcp;
+  PIX2D_FULL();
+  const int W = pc.W, H = pc.H;
+  if (B.weak[center] != DPE_WEAK) return;
+  const int min_margin = 6;
+  const float depth_diff = pc.P.depth_max - pc.P.depth_min;
+  const DpeCamera& camera = pc.cams[0];
+  Rng rs; rng_init(rs, (uint32_t)center, pc.seed32, STREAM_GEN_NEIGHBOURS, pc.salt);
+  short2* nb = B.nb + (size_t)center * 9;
+  nb[0] = make_short2((short)x, (short)y);
+  for (int i = 1; i < 9; ++i) nb[i] = make_short2(-1, -1);
+  short2 strong_points[64];
+  uint64_t dir_valid = 0;
+  int origin_direction_index = -1, strong_point_size = 0;
+  const int rotate_time = pc.P.rotate_time;
+  const float cos_angle = pc.gn_cos, sin_angle = pc.gn_sin, threshhold = pc.gn_thr;
+  const int shift_range = pc.gn_shift;
+  const float ransac_threshold = pc.P.ransac_threshold * depth_diff;
+  bool edge_limit = false;
+  if (pc.P.use_limit) {
+    edge_limit = true;
+    if (pc.P.use_edge) {
+      const float cv = B.complex_[center];
+      const float rp = rng_uniform(rs) - 1.1920929e-07f;
+      if (rp < cv) edge_limit = false;
+      else B.complex_[center] = MAXo(0.99f, cv);
+    }
+  }
+  for (int odx = -1; odx <= 1; ++odx) {
+    for (int ody = -1; ody <= 1; ++ody) {
+      if (odx == 0 && ody == 0) continue;
+      float2 od = make_float2((float)odx, (float)ody);
+      normalize2(od);
+      origin_direction_index++;
+      for (int rotate_iter = 0; rotate_iter < rotate_time; ++rotate_iter) {
+        const int dir_index = origin_direction_index * 4 + rotate_iter;
+        for (int radius = 2; radius <= 4096; radius = MINo(radius * 2, radius + 25)) {
+          const float tpx = (float)x + od.x * radius, tpy = (float)y + od.y * radius;
+          if (tpx < 0 || tpy < 0 || tpx >= W || tpy >= H) break;
+          for (int radius_iter = 0; radius_iter < 4; ++radius_iter) {
+            const uint32_t r1 = rng_u32(rs); const uint32_t r2 = rng_u32(rs);
+            const int rxs = (int)(((r1 % 2 == 0) ? 1u : 0xFFFFFFFFu) * r2 % (uint32_t)shift_range);
+            const uint32_t r3 = rng_u32(rs); const uint32_t r4 = rng_u32(rs);
+            const int rys = (int)(((r3 % 2 == 0) ? 1u : 0xFFFFFFFFu) * r4 % (uint32_t)shift_range);
+            float2 dir = make_float2(od.x * 20 + (float)rxs, od.y * 20 + (float)rys);
+            normalize2(dir);
+            short2 np = make_short2((short)f2i((float)x + dir.x * radius), (short)f2i((float)y + dir.y * radius));
+            if (np.x < min_margin || np.y < min_margin || np.x >= W - min_margin || np.y >= H - min_margin) continue;
+            int npc = np.x + np.y * W;
+            if (B.weak[npc] != DPE_STRONG) {
+              np = B.nearest[npc];
+              if (np.x == -1 || np.y == -1) continue;
+              npc = np.x + np.y * W;
+            }
+            float2 td = make_float2((float)(np.x - x), (float)(np.y - y));
+            normalize2(td);
+            const float ca = td.x * od.x + td.y * od.y;
+            if (ca > threshhold && (!edge_limit || !bresenham(pc, B, x, y, np.x, np.y))) {
+              strong_points[dir_index] = np;
+              dir_valid |= (1ull << dir_index);
+              strong_point_size++;
+              break;
+            }
+          }
+          if ((dir_valid >> dir_index) & 1ull) break;
+        }
+        float2 rd = make_float2(od.x * cos_angle - od.y * sin_angle, od.x * sin_angle + od.y * cos_angle);
+        normalize2(rd);
+        od = rd;
+      }
+    }
+  }
+  int extend_index = 31;
+  if (pc.P.use_label && B.label[center] > 0) {
+    const short2* lb = B.lab_bound + (size_t)center * 8;
+    float bound_dist[8];
+    int dir_step[8];
+    for (int i = 0; i < 8; ++i) {
+      const short2 bp = lb[i];
+      float dist = 0.0f;
+      if (bp.x != -1 && bp.y != -1) {
+        const double dxx = (double)(x - bp.x), dyy = (double)(y - bp.y);
+        dist = (float)__builtin_sqrt(dxx * dxx + dyy * dyy);
+        if (i >= 4) dist = (float)((double)dist / 1.4142135623730951);
+      }
+      bound_dist[i] = dist;
+      if (i % 2 == 1) { dir_step[i - 1] = 2 * rotate_time - 1; dir_step[i] = 1; }
+    }
+    for (int i = 0; i < 8; ++i) {
+      const float dist = bound_dist[i];
+      const int gap_num = dir_step[i] + 1;
+      const int step_len = MAXo(1, d2i(__builtin_floor(1.0 * dist / gap_num)));
+      for (int step = 1; step <= dir_step[i]; ++step) {
+        short2 np = make_short2((short)(x + step * step_len * kDir[i][0]), (short)(y + step * step_len * kDir[i][1]));
+        if (np.x < min_margin || np.y < min_margin || np.x >= W - min_margin || np.y >= H - min_margin) continue;
+        int npc = np.x + np.y * W;
+        if (B.weak[npc] != DPE_STRONG) {
+          np = B.nearest[npc];
+          if (np.x == -1 || np.y == -1) continue;
+          npc = np.x + np.y * W;
+        }
+        if (B.label[npc] != 0 && B.label[npc] != B.label[center]) continue;
+        extend_index++;
+        strong_points[extend_index] = np;
+        dir_valid |= (1ull << extend_index);
+        strong_point_size++;
+      }
+    }
+  }
+  if (strong_point_size <= 3) { B.weak_rel[center] = 0; return; }
+
+  short2 spv[64];
+  float3 spv3[64];
+  float3 spvn[64];
+  int valid_count = 0;
+  float X[3];
+  get3d(camera, x, y, B.planes[center].w, X);
+  const float cpz = X[2];
+  for (int i = 0; i < 64; ++i) {
+    spv[i] = make_short2(-1, -1);
+    if ((dir_valid >> i) & 1ull) {
+      const short2 sp = strong_points[i];
+      const int spc = sp.x + sp.y * W;
+      spv[valid_count] = sp;
+      const float4 pl = B.planes[spc];
+      get3d(camera, sp.x, sp.y, pl.w, X);
+      spv3[valid_count] = make_float3(X[0], X[1], X[2]);
+      const float4 n4 = transform_normal_ref(camera, pl);
+      spvn[valid_count] = make_float3(n4.x, n4.y, n4.z);
+      valid_count++;
+    }
+  }
+  float4 best_plane = make_float4(0, 0, 0, 0);
+  bool has_valid_plane = false;
+  {
+    int iteration = 50, max_iter = pc.P.high_res_img ? 200 : 125, max_count = 3;
+    float min_cost = 3.40282347e+38f, residuals[64];
+    for (int i = 0; i < 64; ++i) residuals[i] = 0.0f;
+    float temp_thr = ransac_threshold;
+    // edge_test[64][64] (DPE.cu:2307) as two bit matrices: tested / crosses-an-edge
+    uint64_t tested[64], crosses[64];
+    for (int i = 0; i < 64; ++i) { tested[i] = 0; crosses[i] = 0; }
+    bool has_consist_normal_plane = false;
+    bool must_in_triangle = (pc.P.use_label && B.label[center] > 0 && edge_limit) ? false : true;
+    auto edge_pair = [&](int a, int b) -> bool {   // returns edge_test[a][b] == 1
+      if (!((tested[a] >> b) & 1ull)) {
+        const bool c = bresenham(pc, B, spv[a].x, spv[a].y, spv[b].x, spv[b].y);
+        tested[a] |= 1ull << b; tested[b] |= 1ull << a;
+        if (c) { crosses[a] |= 1ull << b; crosses[b] |= 1ull << a; }
+      }
+      return (crosses[a] >> b) & 1ull;
+    };
+    while (iteration > 0 && max_iter > 0) {
+      max_iter--;
+      const int a = (int)(rng_u32(rs) % (uint32_t)valid_count);
+      const int b = (int)(rng_u32(rs) % (uint32_t)valid_count);
+      const int c = (int)(rng_u32(rs) % (uint32_t)valid_count);
+      if (a == b || b == c || a == c) continue;
+      if (must_in_triangle && !point_in_triangle(spv[a], spv[b], spv[c], x, y)) continue;
+      if (edge_limit) {
+        const bool eab = edge_pair(a, b);
+        const bool ebc = edge_pair(b, c);
+        const bool eca = edge_pair(c, a);
+        if (eab || ebc || eca) continue;
+      }
+      bool normal_consistency = false;
+      if (pc.P.geom_consistency && edge_limit) {
+        const float3 AN = spvn[a], BN = spvn[b], CN = spvn[c];
+        normal_consistency = true;
+        if ((double)(AN.x * BN.x + AN.y * BN.y + AN.z * BN.z) < 0.8660254 ||
+            (double)(AN.x * CN.x + AN.y * CN.y + AN.z * CN.z) < 0.8660254 ||
+            (double)(BN.x * CN.x + BN.y * CN.y + BN.z * CN.z) < 0.8660254)
+          normal_consistency = false;
+        if (has_consist_normal_plane && !normal_consistency) continue;
+      }
+      iteration--;
+      const float3 A = spv3[a], Bq = spv3[b], C = spv3[c];
+      const float ACx = A.x - C.x, ACy = A.y - C.y, ACz = A.z - C.z;
+      const float BCx = Bq.x - C.x, BCy = Bq.y - C.y, BCz = Bq.z - C.z;
+      float4 cv;
+      cv.x = ACy * BCz - BCy * ACz;
+      cv.y = -(ACx * BCz - BCx * ACz);
+      cv.z = ACx * BCy - BCx * ACy;
+      if ((cv.x == 0 && cv.y == 0 && cv.z == 0) || cv.x != cv.x || cv.y != cv.y || cv.z != cv.z) continue;
+      normalize3(cv);
+      cv.w = -(cv.x * A.x + cv.y * A.y + cv.z * A.z);
+      int temp_count = 0;
+      for (int si = 0; si < valid_count; ++si) {
+        const float fx = ((float)spv[si].x - camera.K[2]) / camera.K[0];
+        const float fy = ((float)spv[si].y - camera.K[5]) / camera.K[4];
+        const float fd = -cv.w / (cv.x * fx + cv.y * fy + cv.z);
+        const float dist = __builtin_fabsf(fd - spv3[si].z);
+        residuals[si] = dist;
+        if (dist < temp_thr) temp_count++;
+      }
+      if (temp_count < 6) continue;
+      if (temp_count > max_count) {
+        if (!must_in_triangle && point_in_triangle(spv[a], spv[b], spv[c], x, y)) must_in_triangle = true;
+        if (!has_consist_normal_plane && normal_consistency) has_consist_normal_plane = true;
+        const float fx = ((float)x - camera.K[2]) / camera.K[0];
+        const float fy = ((float)y - camera.K[5]) / camera.K[4];
+        const float fd = -cv.w / (cv.x * fx + cv.y * fy + cv.z);
+        const float cd = __builtin_fabsf(fd - cpz);
+        best_plane = cv; max_count = temp_count; min_cost = cd; has_valid_plane = true;
+        if ((double)temp_thr > (pc.P.high_res_img ? 0.05 : 0.005)) {
+          // sort_small(residuals, valid_count) (DPE.cu:5-14)
+          for (int i = 1; i < valid_count; i++) {
+            const float tmp = residuals[i];
+            int j = i;
+            for (; j >= 1 && tmp < residuals[j - 1]; j--) residuals[j] = residuals[j - 1];
+            residuals[j] = tmp;
+          }
+          if (temp_thr < residuals[DPE_NEIGHBOUR_NUM]) continue;
+          temp_thr = (float)((double)residuals[DPE_NEIGHBOUR_NUM] - 1e-6);
+          temp_count = 0;
+          for (int i = 0; i < valid_count; ++i) {
+            if (residuals[i] < temp_thr) temp_count++;
+            else break;
+          }
+          max_count = temp_count;
+        }
+      } else if (temp_count == max_count) {
+        if (!must_in_triangle && point_in_triangle(spv[a], spv[b], spv[c], x, y)) must_in_triangle = true;
+        const float fx = ((float)x - camera.K[2]) / camera.K[0];
+        const float fy = ((float)y - camera.K[5]) / camera.K[4];
+        const float fd = -cv.w / (cv.x * fx + cv.y * fy + cv.z);
+        const float cd = __builtin_fabsf(fd - cpz);
+        if (cd < min_cost) { best_plane = cv; max_count = temp_count; min_cost = cd; }
+      }
+    }
+  }
+  if (!has_valid_plane) { B.weak_rel[center] = 0; return; }
+  float weight[64];
+  for (int i = 0; i < valid_count; ++i) {
+    const float fx = ((float)spv[i].x - camera.K[2]) / camera.K[0];
+    const float fy = ((float)spv[i].y - camera.K[5]) / camera.K[4];
+    const float fd = -best_plane.w / (best_plane.x * fx + best_plane.y * fy + best_plane.z);
+    const float dist = __builtin_fabsf(fd - spv3[i].z);
+    if (dist >= ransac_threshold) { spv[i] = make_short2(-1, -1); weight[i] = 3.40282347e+38f; continue; }
+    weight[i] = dist;
+  }
+  // sort_small_weighted (DPE.cu:16-29)
+  for (int i = 1; i < valid_count; i++) {
+    const short2 tp = spv[i]; const float tw = weight[i];
+    int j = i;
+    for (; j >= 1 && tw < weight[j - 1]; j--) { spv[j] = spv[j - 1]; weight[j] = weight[j - 1]; }
+    spv[j] = tp; weight[j] = tw;
+  }
+  for (int i = 1; i < DPE_NEIGHBOUR_NUM; ++i) nb[i] = spv[i - 1];
+  B.weak_rel[center] = 1;
+}
+
+// ------------------------------------------------------------------------------ NeigbourUpdate
+__global__ void k_neighbour_update(const PassConst* __restrict__ pcp, DevBufs B) {   // DPE.cu:2465-2481
+  const PassConst& pc = *pcp;
+  PIX2D_FULL();
+  if (B.weak[center] != DPE_WEAK) return;
+  if (B.weak_rel[center] != 1) B.weak[center] = DPE_UNKNOWN;
+}
+
+// ------------------------------------------------------------------------------ RandomInitialization
+__global__ void __launch_bounds__(256) k_random_init(const PassConst* __restrict__ pcp, DevBufs B) {   // DPE.cu:1035-1063
+  const PassConst& pc = *pcp;
+  PIX2D_FULL();
+  const DpeCamera& c0 = pc.cams[0];
+  const int N = pc.N;
+  const bool fast = pc.P.strong_radius == 5 && pc.P.strong_increment == 2;
+  Patch36 P;
+  if (fast) make_patch36(P, pc, B, x, y); else { P.px = x; P.py = y; }
+  if (pc.P.state == DPE_FIRST_INIT) {
+    Rng rs; rng_init(rs, (uint32_t)center, pc.seed32, STREAM_RANDOM_INIT, pc.salt);
+    const float depth = rng_uniform(rs) * (pc.P.depth_max - pc.P.depth_min) + pc.P.depth_min;
+    float4 ph = random_normal(c0, x, y, rs, depth);
+    ph.w = dist2origin(c0, x, y, depth, ph);
+    B.planes[center] = ph;
+    // ComputeMultiViewInitialCostandSelectedViews (DPE.cu:780-826): sorted copy kept in registers
+    float sorted[DPE_MAX_IMAGES];
+    int cost_count = 0, num_valid = 0;
+    for (int i = 1; i < N; ++i) {
+      const float c = ncc_old(P, fast, pc, B, i, ph);
+      // insertion into the sorted prefix == sort_small of the full vector afterwards
+      int j = cost_count;
+      for (; j >= 1 && c < sorted[j - 1]; j--) sorted[j] = sorted[j - 1];
+      sorted[j] = c;
+      cost_count++;
+      if (c < 2.0f) num_valid++;
+    }
+    uint32_t sel = 0;
+    const int top_k = MINo(num_valid, pc.P.top_k);
+    float cost = 2.0f;
+    if (top_k > 0) {
+      float s = 0.0f;
+      for (int i = 0; i < top_k; ++i) s += sorted[i];
+      const float thr = sorted[top_k - 1];
+      // second pass recomputes the (deterministic) per-view costs instead of keeping a copy
+      for (int i = 1; i < N; ++i) if (ncc_old(P, fast, pc, B, i, ph) <= thr) setBit(sel, i - 1);
+      cost = s / top_k;
+    }
+    B.sel[center] = sel;
+    B.costs[center] = cost;
+  } else {
+    float4 ph = transform_normal_ref(c0, B.planes[center]);
+    const float depth = ph.w;
+    ph.w = dist2origin(c0, x, y, depth, ph);
+    B.planes[center] = ph;
+    // ComputeMultiViewInitialCost (DPE.cu:828-857)
+    uint32_t sel = B.sel[center];
+    int cc = 0; float cost = 0.0f;
+    for (int i = 1; i < N; ++i) {
+      if (isSet(sel, i - 1)) {
+        const float c = ncc_old(P, fast, pc, B, i, ph);
+        if (c < 2.0f) { cc++; cost += c; }
+        else unSetBit(sel, i - 1);
+      }
+    }
+    B.sel[center] = sel;
+    B.costs[center] = cc == 0 ? 2.0f : cost / cc;
+  }
+}
+
+// ------------------------------------------------------------------------------ view selection
+// Multi-hypothesis joint view selection (DPE.cu:1547-1615 / 1710-1779).  `ca` = LDS cost slots
+// (slot-major, [slot][view][thread]), `cdf` = LDS [view][thread], `vwl` = LDS u8 [view][thread].
+struct LdsView {
+  float* ca; float* cdf; uint8_t* vwl; int bs; int tid; int nv;
+  DEV float& cost(int slot, int v) const { return ca[(slot * nv + v) * bs + tid]; }
+  DEV float& prob(int v) const { return cdf[v * bs + tid]; }
+  DEV uint8_t& vw(int v) const { return vwl[v * bs + tid]; }
+};
+
+template <class PriorF>
+DEV void view_selection(const LdsView& L, int iter, PriorF prior, Rng& rs, uint32_t& tsv, float& wnorm) {
+  const int nv = L.nv;
+  for (int i = 0; i < nv; ++i) L.vw(i) = 0;
+  const float cost_threshold = (float)(0.8 * (double)d_expf((float)(iter * iter) / (-90.0f)));
+  float psum = 0.0f;
+  for (int i = 0; i < nv; i++) {
+    float count = 0; int count_false = 0; float tmpw = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const float c = L.cost(j, i);
+      if (c < cost_threshold) { tmpw += d_expf(c * c / (-0.18f)); count++; }
+      if (c > 1.2f) count_false++;
+    }
+    float sp = 0.0f;
+    if (count > 2 && count_false < 3) sp = tmpw / count;
+    else if (count_false < 3) sp = d_expf(cost_threshold * cost_threshold / (-0.32f));
+    sp = sp * prior(i);
+    L.prob(i) = sp;
+    psum += sp;
+  }
+  // TransformPDFToCDF (DPE.cu:293-307)
+  const float inv = 1.0f / psum;
+  float cum = 0.0f;
+  for (int i = 0; i < nv; ++i) { const float q = L.prob(i) * inv; cum += q; L.prob(i) = cum; }
+  for (int s = 0; s < 15; ++s) {
+    const float rp = rng_uniform(rs) - 1.1920929e-07f;
+    for (int id = 0; id < nv; ++id) {
+      if (L.prob(id) > rp) { L.vw(id) = L.vw(id) + 1; break; }
+    }
+  }
+  uint32_t t = 0; float wn = 0;
+  for (int i = 0; i < nv; ++i) { const int w = L.vw(i); if (w > 0) { setBit(t, i); wn += w; } }
+  tsv = t; wnorm = wn;
+}
+
+// ------------------------------------------------------------------------------ strong sweep
+// CheckerboardPropagationStrong (DPE.cu:1214-1666) + PlaneHypothesisRefinementStrong (:1065-1118).
+// Neighbour reads come from the snapshot taken before the half-sweep (same-colour semantics).
+__global__ void __launch_bounds__(128) k_strong_sweep(const PassConst* __restrict__ pcp, DevBufs B, int iter, int colour) {
+  extern __shared__ float lds[];
+  const PassConst& pc = *pcp;
+  PIX2D_HALF();
+  if (B.weak[center] == DPE_WEAK) return;
+  const int W = pc.W, H = pc.H, N = pc.N, nv = N - 1;
+  const DpeCamera& c0 = pc.cams[0];
+  const int bs = blockDim.x * blockDim.y, tid = threadIdx.y * blockDim.x + threadIdx.x;
+  LdsView L{lds, lds + 9 * nv * bs, (uint8_t*)(lds + 10 * nv * bs), bs, tid, nv};
+  Rng rs; rng_init(rs, (uint32_t)center, pc.seed32, STREAM_ITER_BASE + 4 * iter + 0, pc.salt);
+  const bool fast = pc.P.strong_radius == 5 && pc.P.strong_increment == 2;
+  Patch36 P;
+  if (fast) make_patch36(P, pc, B, x, y); else { P.px = x; P.py = y; }
+  const float* __restrict__ costs = B.costs_snap;
+  const float4* __restrict__ planes = B.planes_snap;
+
+  for (int d = 0; d < 8; ++d) for (int v = 0; v < nv; ++v) L.cost(d, v) = 0.0f;
+  L.cost(0, 0) = 2.0f;   // cost_array[8][32] = {2.0f} (DPE.cu:1236)
+  uint32_t flags = 0;
+  int positions[8];
+#pragma unroll
+  for (int d = 0; d < 8; ++d) positions[d] = 0;
+
+  auto costvec = [&](const float4& pl, int slot) {
+    for (int v = 1; v < N; ++v) L.cost(slot, v - 1) = ncc_old(P, fast, pc, B, v, pl);
+  };
+
+  if (pc.P.use_edge) {
+    const short2* en = B.edge_neigh + (size_t)center * 8;
+    const float max_edge_dist = MAXo(H, W) / 30.0f;
+    const int min_step_len = 2;
+    const bool on_edge = B.edge[center] != 0;
+#pragma unroll
+    for (int d = 0; d < 8; ++d) {
+      const int dx = kDir[d][0], dy = kDir[d][1];
+      const int s0 = MAXo(1, 5 - 2 * iter);
+      const short2 ep = en[d];
+      const double ex = (double)(ep.x - x), ey = (double)(ep.y - y);
+      float dist = (float)__builtin_sqrt(ex * ex + ey * ey);
+      if (d >= 4) dist = (float)((double)dist / 1.4142135623730951);
+      if (on_edge) dist = 11 * min_step_len;
+      else if (ep.x == -1 || ep.y == -1 || dist > max_edge_dist) {
+        dist = max_edge_dist;
+        if (d >= 4) dist = (float)((double)dist / 1.4142135623730951);
+      }
+      const int step_num = MINo(MAXo(11, f2i(1.0f * dist / min_step_len)), 22);
+      int step_len = MAXo(f2i(1.0f * dist / step_num), min_step_len);
+      if (d < 4 && step_len % 2 == 1) step_len -= 1;
+      int fx = 0, fy = 0;
+      if (d > 4) { if (d % 2) fx = dx; else fy = dy; }
+      int mpos = 0; float mc = 3.40282347e+38f;
+      for (int step = 0; step < step_num; ++step) {
+        const int tx = x + s0 * dx + step * step_len * dx + fx, ty = y + s0 * dy + step * step_len * dy + fy;
+        if (!(tx >= 0 && ty >= 0 && tx < W && ty < H)) continue;
+        const int ptc = tx + ty * W;
+        const float c = costs[ptc];
+        if (mc > c) { mpos = ptc; mc = c; }
+      }
+      if (mc < 3.40282347e+38f) { flags |= 1u << d; positions[d] = mpos; costvec(planes[mpos], d); }
+    }
+    if (!on_edge) {
+      const float good_threshold = 0.8f * d_expf((float)(iter * iter) / (-90.0f));
+      const float bad_threshold = 1.2f;
+#pragma unroll
+      for (int d = 0; d < 8; ++d) {
+        const int dx = kDir[d][0], dy = kDir[d][1];
+        const int s0 = MAXo(1, 5 - 2 * iter);
+        const bool had = (flags >> d) & 1u;
+        int fx = 0, fy = 0;
+        if (d > 4) { if (d % 2) fx = dx; else fy = dy; }
+        int mpos = 0; float mc = 3.40282347e+38f;
+        for (int step = 0; step < 11; ++step) {
+          const int tx = x + s0 * dx + step * min_step_len * dx + fx, ty = y + s0 * dy + step * min_step_len * dy + fy;
+          if (!(tx >= 0 && ty >= 0 && tx < W && ty < H)) continue;
+          const int ptc = tx + ty * W;
+          const float c = costs[ptc];
+          if (mc > c) { mpos = ptc; mc = c; }
+        }
+        if (mc < 3.40282347e+38f) {
+          flags |= 1u << d;
+          costvec(planes[mpos], 8);
+          int g0 = 0, g1 = 0, b0 = 0, b1 = 0;
+          for (int j = 0; j < nv; j++) {
+            const float v0 = L.cost(d, j);
+            if (v0 < good_threshold) g0++;
+            if (v0 > bad_threshold) b0++;
+          }
+          for (int j = 0; j < nv; j++) {
+            const float v1 = L.cost(8, j);
+            if (v1 < good_threshold) g1++;
+            if (v1 > bad_threshold) b1++;
+          }
+          if (!had || g1 > g0 || (g1 == g0 && b1 < b0)) {
+            positions[d] = mpos;
+            for (int j = 0; j < nv; j++) L.cost(d, j) = L.cost(8, j);
+          }
+        }
+      }
+    }
+  } else {
+    // ACMH-style near/far candidates (DPE.cu:1346-1544); slot order 0 up_near, 1 up_far,
+    // 2 down_near, 3 down_far, 4 left_near, 5 left_far, 6 right_near, 7 right_far
+    float costMin; int cmp;
+    int left_near = center - 1, left_far = center - 3, right_near = center + 1, right_far = center + 3;
+    int up_near = center - W, up_far = center - 3 * W, down_near = center + W, down_far = center + 3 * W;
+    if (y > 2) {
+      flags |= 1u << 1; costMin = costs[up_far]; cmp = up_far;
+      for (int i = 1; i < 11; ++i) if (y > 2 + 2 * i) { const int pt = up_far - 2 * i * W; if (costs[pt] < costMin) { costMin = costs[pt]; cmp = pt; } }
+      up_far = cmp; costvec(planes[up_far], 1);
+    }
+    if (y < H - 3) {
+      flags |= 1u << 3; costMin = costs[down_far]; cmp = down_far;
+      for (int i = 1; i < 11; ++i) if (y < H - 3 - 2 * i) { const int pt = down_far + 2 * i * W; if (costs[pt] < costMin) { costMin = costs[pt]; cmp = pt; } }
+      down_far = cmp; costvec(planes[down_far], 3);
+    }
+    if (x > 2) {
+      flags |= 1u << 5; costMin = costs[left_far]; cmp = left_far;
+      for (int i = 1; i < 11; ++i) if (x > 2 + 2 * i) { const int pt = left_far - 2 * i; if (costs[pt] < costMin) { costMin = costs[pt]; cmp = pt; } }
+      left_far = cmp; costvec(planes[left_far], 5);
+    }
+    if (x < W - 3) {
+      flags |= 1u << 7; costMin = costs[right_far]; cmp = right_far;
+      for (int i = 1; i < 11; ++i) if (x < W - 3 - 2 * i) { const int pt = right_far + 2 * i; if (costs[pt] < costMin) { costMin = costs[pt]; cmp = pt; } }
+      right_far = cmp; costvec(planes[right_far], 7);
+    }
+    if (y > 0) {
+      flags |= 1u << 0; costMin = costs[up_near]; cmp = up_near;
+      for (int i = 0; i < 3; ++i) {
+        if (y > 1 + i && x > i) { const int pt = up_near - (1 + i) * W - (1 + i); if (costs[pt] < costMin) { costMin = costs[pt]; cmp = pt; } }
+        if (y > 1 + i && x < W - 1 - i) { const int pt = up_near - (1 + i) * W + (1 + i); if (costs[pt] < costMin) { costMin = costs[pt]; cmp = pt; } }
+      }
+      up_near = cmp; costvec(planes[up_near], 0);
+    }
+    if (y < H - 1) {
+      flags |= 1u << 2; costMin = costs[down_near]; cmp = down_near;
+      for (int i = 0; i < 3; ++i) {
+        if (y < H - 2 - i && x > i) { const int pt = down_near + (1 + i) * W - (1 + i); if (costs[pt] < costMin) { costMin = costs[pt]; cmp = pt; } }
+        if (y < H - 2 - i && x < W - 1 - i) { const int pt = down_near + (1 + i) * W + (1 + i); if (costs[pt] < costMin) { costMin = costs[pt]; cmp = pt; } }
+      }
+      down_near = cmp; costvec(planes[down_near], 2);
+    }
+    if (x > 0) {
+      flags |= 1u << 4; costMin = costs[left_near]; cmp = left_near;
+      for (int i = 0; i < 3; ++i) {
+        if (x > 1 + i && y > i) { const int pt = left_near - (1 + i) - (1 + i) * W; if (costs[pt] < costMin) { costMin = costs[pt]; cmp = pt; } }
+        if (x > 1 + i && y < H - 1 - i) { const int pt = left_near - (1 + i) + (1 + i) * W; if (costs[pt] < costMin) { costMin = costs[pt]; cmp = pt; } }
+      }
+      left_near = cmp; costvec(planes[left_near], 4);
+    }
+    if (x < W - 1) {
+      flags |= 1u << 6; costMin = costs[right_near]; cmp = right_near;
+      for (int i = 0; i < 3; ++i) {
+        if (x < W - 2 - i && y > i) { const int pt = right_near + (1 + i) - (1 + i) * W; if (costs[pt] < costMin) { costMin = costs[pt]; cmp = pt; } }
+        if (x < W - 2 - i && y < H - 1 - i) { const int pt = right_near + (1 + i) + (1 + i) * W; if (costs[pt] < costMin) { costMin = costs[pt]; cmp = pt; } }
+      }
+      right_near = cmp; costvec(planes[right_near], 6);
+    }
+    positions[0] = up_near; positions[1] = up_far; positions[2] = down_near; positions[3] = down_far;
+    positions[4] = left_near; positions[5] = left_far; positions[6] = right_near; positions[7] = right_far;
+  }
+
+  // priors from the 4-neighbourhood (DPE.cu:1552-1566), snapshot reads, out-of-array -> 0
+  const long Lp = (long)W * H;
+  uint32_t nsv[4];
+  const long npos[4] = {(long)center - W, (long)center + W, (long)center - 1, (long)center + 1};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) nsv[i] = ((flags >> (2 * i)) & 1u) && npos[i] >= 0 && npos[i] < Lp ? B.sel_snap[npos[i]] : 0u;
+  auto prior = [&](int j) {
+    float p = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) if ((flags >> (2 * i)) & 1u) p += isSet(nsv[i], j) == 1 ? 0.9f : 0.1f;
+    return p;
+  };
+  uint32_t tsv; float wnorm;
+  view_selection(L, iter, prior, rs, tsv, wnorm);
+  uint8_t* vwg = B.vw + (size_t)center * DPE_MAX_IMAGES;
+  for (int j = 0; j < DPE_MAX_IMAGES; ++j) vwg[j] = j < nv ? L.vw(j) : 0;
+
+  float final_costs[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    float f = 0.0f;
+    for (int j = 0; j < nv; ++j) { const int w = L.vw(j); if (w > 0) f += w * L.cost(i, j); }
+    final_costs[i] = f / wnorm;
+  }
+  int mi = 0; float mcost = final_costs[0];
+#pragma unroll
+  for (int i = 1; i < 8; ++i) if (final_costs[i] <= mcost) { mcost = final_costs[i]; mi = i; }   // FindMinCostIndex
+
+  const float4 cur = planes[center];
+  float cost_now = 0.0f;
+  for (int i = 0; i < nv; ++i) { const int w = L.vw(i); if (w > 0) cost_now += w * ncc_old(P, fast, pc, B, i + 1, cur); }
+  cost_now /= wnorm;
+  const float cost_written = cost_now;
+  B.costs[center] = cost_now;
+  float depth_now = depth_from_plane(c0, cur, x, y);
+  float4 pnow = cur;
+  int mpos = 0; float mfc = 0.0f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) if (i == mi) { mpos = positions[i]; mfc = final_costs[i]; }
+  if ((flags >> mi) & 1u) {
+    const float4 cand = planes[mpos];
+    const float db = depth_from_plane(c0, cand, x, y);
+    if (db >= pc.P.depth_min && db <= pc.P.depth_max && mfc < cost_now) {
+      depth_now = db; pnow = cand; cost_now = mfc; B.sel[center] = tsv;
+    }
+  }
+  // PlaneHypothesisRefinementStrong (DPE.cu:1065-1118)
+  {
+    const float dmin = pc.P.depth_min, dmax = pc.P.depth_max;
+    const float depth_rand = rng_uniform(rs) * (dmax - dmin) + dmin;
+    const float4 prand = random_normal(c0, x, y, rs, depth_now);
+    const float dminp = (1 - 0.02f) * depth_now, dmaxp = (1 + 0.02f) * depth_now;
+    const float depth_perturbed = rng_uniform(rs) * (dmaxp - dminp) + dminp;
+    const float4 ppert = perturbed_normal(c0, x, y, pnow, rs, (float)(0.02f * 3.14159265358979323846));
+    const float dep0 = depth_now;
+    const float4 pl0 = pnow;
+    for (int h = 0; h < 5; ++h) {
+      float dh; float4 tp;
+      if (h == 0) { dh = depth_rand; tp = pl0; }
+      else if (h == 1) { dh = dep0; tp = prand; }
+      else if (h == 2) { dh = depth_rand; tp = prand; }
+      else if (h == 3) { dh = dep0; tp = ppert; }
+      else { dh = depth_perturbed; tp = pl0; }
+      tp.w = dist2origin(c0, x, y, dh, tp);
+      float tc = 0.0f;
+      for (int j = 0; j < nv; ++j) { const int w = L.vw(j); if (w > 0) tc += w * ncc_old(P, fast, pc, B, j + 1, tp); }
+      tc /= wnorm;
+      const float db = depth_from_plane(c0, tp, x, y);
+      if (db >= dmin && db <= dmax && tc < cost_now) { depth_now = db; pnow = tp; cost_now = tc; }
+    }
+  }
+  if (pc.P.state == DPE_REFINE_INIT) {
+    if ((double)cost_now < (double)cost_written - 0.1) { B.costs[center] = cost_now; B.planes[center] = pnow; }
+  } else {
+    B.costs[center] = cost_now;
+    B.planes[center] = pnow;
+  }
+}
+
+// ------------------------------------------------------------------------------ RANSACToGetFitPlane
+__global__ void __launch_bounds__(256) k_ransac_fit(const PassConst* __restrict__ pcp, DevBufs B, int iter) {   // DPE.cu:2891-3124
+  const PassConst& pc = *pcp;
+  PIX2D_FULL();
+  const int W = pc.W;
+  if (B.weak[center] != DPE_WEAK) return;
+  Rng rs; rng_init(rs, (uint32_t)center, pc.seed32, STREAM_ITER_BASE + 4 * iter + 1, pc.salt);
+  const DpeCamera& camera = pc.cams[0];
+  bool edge_limit = false;
+  if (pc.P.use_limit) {
+    edge_limit = true;
+    if (pc.P.use_edge) {
+      const float cv = B.complex_[center];
+      const float rp = rng_uniform(rs) - 1.1920929e-07f;
+      if (rp < cv) edge_limit = false;
+    }
+  }
+  short2 sp[8]; float3 sp3[8]; float3 spn[8];
+  int sc = 0;
+  float X[3];
+  const short2* nb = B.nb + (size_t)center * 9;
+  for (int i = 1; i < DPE_NEIGHBOUR_NUM; ++i) {
+    const short2 tp = nb[i];
+    if (tp.x == -1 || tp.y == -1) continue;
+    sp[sc] = tp;
+    const float4 pl = B.planes[tp.x + tp.y * W];
+    const float depth = depth_from_plane(camera, pl, tp.x, tp.y);
+    get3d(camera, tp.x, tp.y, depth, X);
+    sp3[sc] = make_float3(X[0], X[1], X[2]);
+    spn[sc] = make_float3(pl.x, pl.y, pl.z);
+    sc++;
+  }
+  if (sc < 3) { B.fit_plane[center] = B.planes[center]; return; }
+  int iteration = 50;
+  int ua = -1, ub = -1, uc = -1;
+  float min_cost = 3.40282347e+38f;
+  float4 best = make_float4(0, 0, 0, 0);
+  bool has_best = false, has_strong_plane = false;
+  bool must_in_triangle = (pc.P.use_label && B.label[center] > 0 && edge_limit) ? false : true;
+  uint8_t tested[8] = {0, 0, 0, 0, 0, 0, 0, 0}, crosses[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  auto edge_pair = [&](int a, int b) -> bool {
+    if (!((tested[a] >> b) & 1)) {
+      const bool c = bresenham(pc, B, sp[a].x, sp[a].y, sp[b].x, sp[b].y);
+      tested[a] |= 1 << b; tested[b] |= 1 << a;
+      if (c) { crosses[a] |= 1 << b; crosses[b] |= 1 << a; }
+    }
+    return (crosses[a] >> b) & 1;
+  };
+  while (iteration--) {
+    const int a = (int)(rng_u32(rs) % (uint32_t)sc);
+    const int b = (int)(rng_u32(rs) % (uint32_t)sc);
+    const int c = (int)(rng_u32(rs) % (uint32_t)sc);
+    if (a == b || b == c || a == c) continue;
+    bool is_strong_plane = false;
+    if (pc.P.geom_consistency && edge_limit) {
+      const float3 AN = spn[a], BN = spn[b], CN = spn[c];
+      is_strong_plane = true;
+      if ((double)(AN.x * BN.x + AN.y * BN.y + AN.z * BN.z) < 0.8660254 ||
+          (double)(AN.x * CN.x + AN.y * CN.y + AN.z * CN.z) < 0.8660254 ||
+          (double)(BN.x * CN.x + BN.y * CN.y + BN.z * CN.z) < 0.8660254)
+        is_strong_plane = false;
+      if (has_strong_plane && !is_strong_plane) continue;
+    }
+    if (must_in_triangle && !point_in_triangle(sp[a], sp[b], sp[c], x, y)) continue;
+    if (edge_limit) {
+      const bool eab = edge_pair(a, b);
+      const bool ebc = edge_pair(b, c);
+      const bool eca = edge_pair(c, a);
+      if (eab || ebc || eca) continue;
+    }
+    const float3 A = sp3[a], Bq = sp3[b], C = sp3[c];
+    const float ACx = A.x - C.x, ACy = A.y - C.y, ACz = A.z - C.z;
+    const float BCx = Bq.x - C.x, BCy = Bq.y - C.y, BCz = Bq.z - C.z;
+    float4 cv;
+    cv.x = ACy * BCz - BCy * ACz;
+    cv.y = -(ACx * BCz - BCx * ACz);
+    cv.z = ACx * BCy - BCx * ACy;
+    if ((cv.x == 0 && cv.y == 0 && cv.z == 0) || cv.x != cv.x || cv.y != cv.y || cv.z != cv.z) continue;
+    normalize3(cv);
+    cv.w = -(cv.x * A.x + cv.y * A.y + cv.z * A.z);
+    if (!has_strong_plane && is_strong_plane) has_strong_plane = true;
+    float tcost = 0.0f;
+    for (int si = 0; si < sc; ++si) {
+      if (si == a || si == b || si == c) continue;
+      const float fx = ((float)sp[si].x - camera.K[2]) / camera.K[0];
+      const float fy = ((float)sp[si].y - camera.K[5]) / camera.K[4];
+      const float fd = -cv.w / (cv.x * fx + cv.y * fy + cv.z);
+      tcost += __builtin_fabsf(fd - sp3[si].z);
+    }
+    if (tcost < min_cost) {
+      if (!must_in_triangle && point_in_triangle(sp[a], sp[b], sp[c], x, y)) must_in_triangle = true;
+      min_cost = tcost; best = cv; has_best = true; ua = a; ub = b; uc = c;
+    }
+  }
+  if (has_best) {
+    const float depth = depth_from_plane(camera, B.planes[center], x, y);
+    const float4 vd = view_direction(camera, x, y, depth);
+    if (best.x * vd.x + best.y * vd.y + best.z * vd.z > 0) { best.x = -best.x; best.y = -best.y; best.z = -best.z; best.w = -best.w; }
+    B.fit_plane[center] = best;
+    if (pc.P.use_radius) {
+      if (must_in_triangle) {
+        const short2 A = sp[ua], Bq = sp[ub], C = sp[uc];
+        const float a = __builtin_sqrtf((float)((A.x - Bq.x) * (A.x - Bq.x) + (A.y - Bq.y) * (A.y - Bq.y)));
+        const float b = __builtin_sqrtf((float)((Bq.x - C.x) * (Bq.x - C.x) + (Bq.y - C.y) * (Bq.y - C.y)));
+        const float c = __builtin_sqrtf((float)((C.x - A.x) * (C.x - A.x) + (C.y - A.y) * (C.y - A.y)));
+        const float p = (float)((double)(a + b + c) / 2.0);
+        const float Sarea = __builtin_sqrtf(p * (p - a) * (p - b) * (p - c));
+        int radius = d2i(__builtin_floor((double)__builtin_sqrtf(Sarea) / 2.0));
+        const float Ad = __builtin_sqrtf((float)((A.x - x) * (A.x - x) + (A.y - y) * (A.y - y)));
+        const float Bd = __builtin_sqrtf((float)((Bq.x - x) * (Bq.x - x) + (Bq.y - y) * (Bq.y - y)));
+        const float Cd = __builtin_sqrtf((float)((C.x - x) * (C.x - x) + (C.y - y) * (C.y - y)));
+        const float min_dis = MINo(MINo(Ad, Bd), Cd);
+        if (2.5 * (double)min_dis < (double)radius) radius = f2i(min_dis);
+        if (edge_limit) {
+          if (pc.P.use_edge) {
+            float med = 3.40282347e+38f;
+            const short2* en = B.edge_neigh + (size_t)center * 8;
+            for (int d = 0; d < 8; ++d) {
+              const short2 ep = en[d];
+              if (ep.x == -1 || ep.y == -1) continue;
+              const float dist = __builtin_sqrtf((float)((ep.x - x) * (ep.x - x) + (ep.y - y) * (ep.y - y)));
+              med = MINo(med, dist);
+            }
+            if (med < (float)radius) radius = f2i(med);
+          }
+          if (pc.P.use_label && B.label[center] > 0) {
+            float mbd = 3.40282347e+38f;
+            const short2* lb = B.lab_bound + (size_t)center * 8;
+            for (int d = 0; d < 8; ++d) {
+              const short2 bp = lb[d];
+              if (bp.x == -1 || bp.y == -1) continue;
+              const double dxx = (double)(x - bp.x), dyy = (double)(y - bp.y);
+              const float dist = (float)__builtin_sqrt(dxx * dxx + dyy * dyy);
+              mbd = MINo(mbd, dist);
+            }
+            if (mbd < (float)radius) radius = f2i(mbd);
+          }
+        }
+        while ((radius << 1) % 5 != 0) radius--;
+        if (!edge_limit) B.radius[center] = radius > pc.P.strong_radius ? 0 : pc.P.strong_radius;
+        else B.radius[center] = radius > pc.P.strong_radius ? radius : pc.P.strong_radius;
+      } else {
+        B.radius[center] = pc.P.strong_radius;
+      }
+    }
+  } else {
+    B.fit_plane[center] = make_float4(0, 0, 0, 0);
+    if (pc.P.use_radius) B.radius[center] = pc.P.strong_radius;
+  }
+}
+
+// ------------------------------------------------------------------------------ weak sweep
+// CheckerboardPropagationWeak (DPE.cu:1668-1862) + PlaneHypothesisRefinementWeak (:1120-1212).
+__global__ void __launch_bounds__(128) k_weak_sweep(const PassConst* __restrict__ pcp, DevBufs B, int iter, int colour) {
+  extern __shared__ float lds[];
+  const PassConst& pc = *pcp;
+  PIX2D_HALF();
+  if (B.weak[center] != DPE_WEAK) return;
+  const int W = pc.W, N = pc.N, nv = N - 1;
+  const DpeCamera& c0 = pc.cams[0];
+  const int bs = blockDim.x * blockDim.y, tid = threadIdx.y * blockDim.x + threadIdx.x;
+  LdsView L{lds, lds + 9 * nv * bs, (uint8_t*)(lds + 10 * nv * bs), bs, tid, nv};
+  Rng rs; rng_init(rs, (uint32_t)center, pc.seed32, STREAM_ITER_BASE + 4 * iter + 2, pc.salt);
+  const bool geom = pc.P.geom_consistency;
+  const float gf = pc.P.geom_factor;
+  for (int d = 0; d < 8; ++d) for (int v = 0; v < nv; ++v) L.cost(d, v) = 0.0f;
+  L.cost(0, 0) = 2.0f;
+  const short2* nb = B.nb + (size_t)center * 9;
+  uint32_t flags = 0;
+  int positions[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    positions[i] = 0;
+    const short2 np = nb[i + 1];
+    if (np.x == -1 || np.y == -1 || B.weak[np.x + np.y * W] != DPE_STRONG) continue;
+    positions[i] = np.x + np.y * W;
+    flags |= 1u << i;
+    const float4 pl = B.planes[positions[i]];
+    for (int v = 1; v < N; ++v) L.cost(i, v - 1) = ncc_new(pc, B, x, y, v, pl);
+  }
+  uint32_t nsv[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const short2 np = nb[i + 1];
+    nsv[i] = (np.x == -1 || np.y == -1) ? 0u : B.sel[np.x + np.y * W];
+  }
+  auto prior = [&](int j) {
+    float p = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const short2 np = nb[i + 1];
+      if (np.x == -1 || np.y == -1) continue;
+      p += isSet(nsv[i], j) == 1 ? 0.9f : 0.1f;
+    }
+    return p;
+  };
+  uint32_t tsv; float wnorm;
+  view_selection(L, iter, prior, rs, tsv, wnorm);
+  uint8_t* vwg = B.vw + (size_t)center * DPE_MAX_IMAGES;
+  for (int j = 0; j < DPE_MAX_IMAGES; ++j) vwg[j] = j < nv ? L.vw(j) : 0;
+
+  float final_costs[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    float f = 0.0f;
+    const bool fl = (flags >> i) & 1u;
+    const float4 cpl = B.planes[positions[i]];
+    for (int j = 0; j < nv; ++j) {
+      const int w = L.vw(j);
+      if (w > 0) {
+        if (geom) {
+          if (fl) f += w * (L.cost(i, j) + gf * geom_cost(pc, B, x, y, j + 1, cpl));
+          else f += w * (L.cost(i, j) + gf * 3.0f);
+        } else {
+          f += w * L.cost(i, j);
+        }
+      }
+    }
+    final_costs[i] = f / wnorm;
+  }
+  int mi = 0; float mcost = final_costs[0];
+#pragma unroll
+  for (int i = 1; i < 8; ++i) if (final_costs[i] <= mcost) { mcost = final_costs[i]; mi = i; }
+
+  const float4 cur = B.planes[center];
+  auto hyp_cost = [&](const float4& tp) {
+    float tc = 0.0f;
+    for (int j = 0; j < nv; ++j) {
+      const int w = L.vw(j);
+      if (w > 0) {
+        const float c = ncc_new(pc, B, x, y, j + 1, tp);
+        if (geom) tc += w * (c + gf * geom_cost(pc, B, x, y, j + 1, tp));
+        else tc += w * c;
+      }
+    }
+    return tc;
+  };
+  float cost_now = hyp_cost(cur) / wnorm;
+  const float cost_written = cost_now;
+  B.costs[center] = cost_now;
+  float depth_now = depth_from_plane(c0, cur, x, y);
+  float4 pnow = cur;
+  int mpos = 0; float mfc = 0.0f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) if (i == mi) { mpos = positions[i]; mfc = final_costs[i]; }
+  if ((flags >> mi) & 1u) {
+    const float4 cand = B.planes[mpos];
+    const float db = depth_from_plane(c0, cand, x, y);
+    if (db >= pc.P.depth_min && db <= pc.P.depth_max && mfc < cost_now) {
+      depth_now = db; pnow = cand; cost_now = mfc; B.sel[center] = tsv;
+    }
+  }
+  // PlaneHypothesisRefinementWeak (DPE.cu:1120-1212)
+  {
+    const float dmin = pc.P.depth_min, dmax = pc.P.depth_max;
+    bool skip = false;
+    const float4 fp = B.fit_plane[center];
+    if (fp.x == 0 && fp.y == 0 && fp.z == 0) skip = true;
+    else {
+      const float tc = hyp_cost(fp) / wnorm;
+      const float db = depth_from_plane(c0, fp, x, y);
+      if (db >= dmin && db <= dmax && tc < cost_now) { depth_now = db; pnow = fp; cost_now = tc; }
+    }
+    if (!skip) {
+      const float depth_rand = rng_uniform(rs) * (dmax - dmin) + dmin;
+      const float4 prand = random_normal(c0, x, y, rs, depth_now);
+      const float dminp = (1 - 0.02f) * depth_now, dmaxp = (1 + 0.02f) * depth_now;
+      const float depth_perturbed = rng_uniform(rs) * (dmaxp - dminp) + dminp;
+      const float4 ppert = perturbed_normal(c0, x, y, pnow, rs, (float)(0.02f * 3.14159265358979323846));
+      const float dep0 = depth_now;
+      const float4 pl0 = pnow;
+      for (int h = 0; h < 5; ++h) {
+        float dh; float4 tp;
+        if (h == 0) { dh = depth_rand; tp = pl0; }
+        else if (h == 1) { dh = dep0; tp = prand; }
+        else if (h == 2) { dh = depth_rand; tp = prand; }
+        else if (h == 3) { dh = dep0; tp = ppert; }
+        else { dh = depth_perturbed; tp = pl0; }
+        tp.w = dist2origin(c0, x, y, dh, tp);
+        const float tc = hyp_cost(tp) / wnorm;
+        const float db = depth_from_plane(c0, tp, x, y);
+        if (db >= dmin && db <= dmax && tc < cost_now) { depth_now = db; pnow = tp; cost_now = tc; }
+      }
+    }
+  }
+  float4 fin = cur;
+  if (pc.P.state == DPE_REFINE_INIT) {
+    if ((double)cost_now < (double)cost_written - 0.1) { fin = pnow; B.planes[center] = pnow; }
+  } else {
+    fin = pnow;
+    B.planes[center] = pnow;
+  }
+  // final cost with the Old NCC (DPE.cu:1845-1861)
+  {
+    const bool fast = pc.P.strong_radius == 5 && pc.P.strong_increment == 2;
+    Patch36 P;
+    if (fast) make_patch36(P, pc, B, x, y); else { P.px = x; P.py = y; }
+    float c2 = 0.0f;
+    for (int i = 0; i < nv; ++i) { const int w = L.vw(i); if (w > 0) c2 += w * ncc_old(P, fast, pc, B, i + 1, fin); }
+    B.costs[center] = c2 / wnorm;
+  }
+}
+
+// ------------------------------------------------------------------------------ GetDepthandNormal
+__global__ void k_depth_normal(const PassConst* __restrict__ pcp, DevBufs B) {   // DPE.cu:1940-1955
+  const PassConst& pc = *pcp;
+  PIX2D_FULL();
+  float4 p = B.planes[center];
+  p.w = depth_from_plane(pc.cams[0], p, x, y);
+  B.planes[center] = transform_normal(pc.cams[0], p);
+}
+
+// ------------------------------------------------------------------------------ CheckerboardFilterStrong
+__global__ void k_filter(const PassConst* __restrict__ pcp, DevBufs B, int colour) {   // DPE.cu:1957-2101
+  const PassConst& pc = *pcp;
+  PIX2D_HALF();
+  const int W = pc.W, H = pc.H;
+  if (B.weak[center] == DPE_WEAK) return;
+  const float4* P = B.planes;
+  float filter[21];
+  int n = 0;
+  filter[n++] = P[center].w;
+  if (B.costs[center] < 0.001f) return;
+  const int left = center - 1, leftleft = center - 3, up = center - W, upup = center - 3 * W;
+  const int down = center + W, downdown = center + 3 * W, right = center + 1, rightright = center + 3;
+  auto add = [&](bool cond, int idx) { if (cond && B.weak[idx] == DPE_STRONG) filter[n++] = P[idx].w; };
+  add(y > 0, up); add(y > 2, upup); add(y > 4, upup - W * 2);
+  add(y < H - 1, down); add(y < H - 3, downdown); add(y < H - 5, downdown + W * 2);
+  add(x > 0, left); add(x > 2, leftleft); add(x > 4, leftleft - 2);
+  add(x < W - 1, right); add(x < W - 3, rightright); add(x < W - 5, rightright + 2);
+  add(y > 0 && x < W - 2, up + 2); add(y < H - 1 && x < W - 2, down + 2);
+  add(y > 0 && x > 1, up - 2); add(y < H - 1 && x > 1, down - 2);
+  add(x > 0 && y > 2, left - W * 2); add(x < W - 1 && y > 2, right - W * 2);
+  add(x > 0 && y < H - 2, left + W * 2); add(x < W - 1 && y < H - 2, right + W * 2);
+  for (int i = 1; i < n; i++) {
+    const float tmp = filter[i];
+    int j = i;
+    for (; j >= 1 && tmp < filter[j - 1]; j--) filter[j] = filter[j - 1];
+    filter[j] = tmp;
+  }
+  const int m = n / 2;
+  B.planes[center].w = (n % 2 == 0) ? (filter[m - 1] + filter[m]) / 2 : filter[m];
+}
+
+// ------------------------------------------------------------------------------ DepthToWeak / LocalRefine
+struct CostBase { float cost_now, base_line, weight_normal; int valid; };
+
+DEV CostBase cost_and_baseline(const PassConst& pc, const DevBufs& B, const Patch36& P, bool fast, int x, int y,
+                               uint32_t sel, const uint8_t* vw, const float4& op, float od) {
+  CostBase r = {0.0f, 0.0f, 0.0f, 0};
+  const DpeCamera& c0 = pc.cams[0];
+  for (int si = 1; si < pc.N; ++si) {
+    const int vi = si - 1;
+    if (isSet(sel, vi)) {
+      float4 tp = op;
+      tp.w = dist2origin(c0, x, y, od, tp);
+      float tc = ncc_old(P, fast, pc, B, si, tp);
+      if (pc.P.geom_consistency) tc += pc.P.geom_factor * geom_cost(pc, B, x, y, si, tp);
+      r.cost_now += (tc * vw[vi]);
+      r.weight_normal += vw[vi];
+      const DpeCamera& cs = pc.cams[si];
+      const float d0 = c0.c[0] - cs.c[0], d1 = c0.c[1] - cs.c[1], d2 = c0.c[2] - cs.c[2];
+      const float tv = d0 * d0 + d1 * d1 + d2 * d2;
+      r.base_line += __builtin_sqrtf(tv);
+      r.valid++;
+    }
+  }
+  return r;
+}
+
+__global__ void __launch_bounds__(256) k_depth_to_weak(const PassConst* __restrict__ pcp, DevBufs B) {   // DPE.cu:2593-2747
+  extern __shared__ float lds[];
+  const PassConst& pc = *pcp;
+  PIX2D_FULL();
+  const int W = pc.W, H = pc.H;
+  const int min_margin = 6;
+  if (x < min_margin || y < min_margin || x >= W - min_margin || y >= H - min_margin) { B.weak[center] = DPE_UNKNOWN; return; }
+  const DpeCamera& c0 = pc.cams[0];
+  const uint8_t* vw = B.vw + (size_t)DPE_MAX_IMAGES * center;
+  const float4 op = transform_normal_ref(c0, B.planes[center]);
+  const float od = op.w;
+  if (od == 0) { B.weak[center] = DPE_UNKNOWN; return; }
+  const uint32_t sel = B.sel[center];
+  const bool fast = pc.P.strong_radius == 5 && pc.P.strong_increment == 2;
+  Patch36 P;
+  if (fast) make_patch36(P, pc, B, x, y); else { P.px = x; P.py = y; }
+  CostBase cn = cost_and_baseline(pc, B, P, fast, x, y, sel, vw, op, od);
+  if (cn.valid == 0) { B.weak[center] = DPE_UNKNOWN; return; }
+  cn.cost_now /= cn.weight_normal;
+  cn.base_line /= cn.valid;
+  const float disp = c0.K[0] * cn.base_line / od;
+  const int bs = blockDim.x * blockDim.y, tid = threadIdx.y * blockDim.x + threadIdx.x;
+  float* pcs = lds;   // p_costs[61] as [61][bs]
+  const int radius = 30;
+  for (int pd = -radius; pd <= radius; ++pd) {
+    const float p_depth = c0.K[0] * cn.base_line / (disp + (float)pd);
+    float val;
+    if (p_depth < pc.P.depth_min || p_depth > pc.P.depth_max) val = 2.0f;
+    else {
+      float4 tp = op;
+      tp.w = dist2origin(c0, x, y, p_depth, tp);
+      float p_cost = 0.0f;
+      for (int si = 1; si < pc.N; ++si) {
+        const int vi = si - 1;
+        if (isSet(sel, vi)) {
+          float tcst = 0.0f;
+          tcst += ncc_old(P, fast, pc, B, si, tp);
+          if (pc.P.geom_consistency) tcst += pc.P.geom_factor * geom_cost(pc, B, x, y, si, tp);
+          p_cost += (tcst * vw[vi]);
+        }
+      }
+      p_cost /= cn.weight_normal;
+      val = MINo(2.0f, p_cost);
+    }
+    pcs[(pd + radius) * bs + tid] = val;
+  }
+  auto pcv = [&](int i) { return pcs[i * bs + tid]; };
+  int peak_count = 0, min_peak = 0;
+  float min_cost = 2.0f;
+  uint64_t is_peak = 0;
+  for (int i = 2; i < 59; ++i) {
+    const float c = pcv(i);
+    if (pcv(i - 1) > c && pcv(i + 1) > c) {
+      is_peak |= 1ull << i; peak_count++;
+      if (c < min_cost) { min_peak = i; min_cost = c; }
+    }
+  }
+  if (abs(min_peak - radius) > pc.P.weak_peak_radius || pcv(min_peak) > 0.5f) { B.weak[center] = DPE_WEAK; return; }
+  if (peak_count == 1) { B.weak[center] = pcv(min_peak) <= 0.15f ? DPE_STRONG : DPE_WEAK; return; }
+  float var = 0.0f;
+  for (int i = 2; i < 59; ++i) if (((is_peak >> i) & 1ull) && i != min_peak) { const float d = pcv(i) - min_cost; var += d * d; }
+  var = __builtin_sqrtf(var);
+  var /= (peak_count - 1);
+  B.weak[center] = var > 0.2f ? DPE_STRONG : DPE_WEAK;
+}
+
+__global__ void __launch_bounds__(256) k_local_refine(const PassConst* __restrict__ pcp, DevBufs B) {   // DPE.cu:2749-2835
+  const PassConst& pc = *pcp;
+  PIX2D_FULL();
+  const DpeCamera& c0 = pc.cams[0];
+  const uint8_t* vw = B.vw + (size_t)DPE_MAX_IMAGES * center;
+  const float4 op = transform_normal_ref(c0, B.planes[center]);
+  const float od = op.w;
+  if (od == 0) return;
+  const uint32_t sel = B.sel[center];
+  const bool fast = pc.P.strong_radius == 5 && pc.P.strong_increment == 2;
+  Patch36 P;
+  if (fast) make_patch36(P, pc, B, x, y); else { P.px = x; P.py = y; }
+  CostBase cn = cost_and_baseline(pc, B, P, fast, x, y, sel, vw, op, od);
+  if (cn.weight_normal == 0 || cn.valid == 0) return;
+  cn.cost_now /= cn.weight_normal;
+  cn.base_line /= cn.valid;
+  const float disp = c0.K[0] * cn.base_line / od;
+  float min_cost = 2.0f, best_depth = od;
+  for (int pd = -5; pd <= 5; ++pd) {
+    const float p_depth = c0.K[0] * cn.base_line / (disp + (float)pd);
+    if (p_depth < pc.P.depth_min || p_depth > pc.P.depth_max) continue;
+    float4 tp = op;
+    tp.w = dist2origin(c0, x, y, p_depth, tp);
+    float tc = 0.0f;
+    for (int si = 1; si < pc.N; ++si) {
+      const int vi = si - 1;
+      if (isSet(sel, vi)) {
+        tc += (ncc_old(P, fast, pc, B, si, tp) * vw[vi]);
+        if (pc.P.geom_consistency) tc += (pc.P.geom_factor * geom_cost(pc, B, x, y, si, tp) * vw[vi]);
+      }
+    }
+    tc /= cn.weight_normal;
+    if (tc < min_cost) { min_cost = tc; best_depth = p_depth; }
+  }
+  if ((double)(cn.cost_now - min_cost) > 0.1) B.planes[center].w = best_depth;
+}
+
+// ------------------------------------------------------------------------------ staging kernels
+// padded quad-texel image (see pass_common.h)
+__global__ void k_build_quad(const float* __restrict__ img, float4* __restrict__ q, int W, int H) {
+  const int X = blockIdx.x * blockDim.x + threadIdx.x;
+  const int Y = blockIdx.y * blockDim.y + threadIdx.y;
+  if (X > W + 1 || Y > H + 1) return;
+  auto cl = [](int v, int n) { return v < 0 ? 0 : (v > n - 1 ? n - 1 : v); };
+  const int x0 = cl(X - 1, W), x1 = cl(X, W), y0 = cl(Y - 1, H), y1 = cl(Y, H);
+  q[Y * (W + 2) + X] = make_float4(img[y0 * W + x0], img[y0 * W + x1], img[y1 * W + x0], img[y1 * W + x1]);
+}
+
+}  // namespace dpe

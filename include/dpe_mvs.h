@@ -1,0 +1,181 @@
+/*
+ * dpe_mvs.h — C-ABI of the MI355X-native PatchMatch pass (the DPE-MVS hot path).
+ *
+ * This header is the drop-in boundary.  It replaces the inner seam of the reference's
+ * per-image host object `class DPE`:
+ *
+ *   reference                                   replaced by
+ *   ------------------------------------------  ------------------------------------------
+ *   DPE::CudaSpaceInitialization  DPE.cpp:916   dpe_pm_stage()   (H2D, layout, workspaces)
+ *   DPE::SetDataPassHelperInCuda  DPE.cpp:1054  (internal: device pointer bundle)
+ *   DPE::RunPatchMatch            DPE.cu:3126   dpe_pm_execute() (the 26-launch pass)
+ *   DPE::GetPlaneHypothesis       DPE.cpp:1091  dpe_pm_fetch()   (D2H of planes /
+ *   DPE::GetPixelStates           DPE.cpp:1099                     weak_info / selected_views)
+ *   DPE::GetSelectedViews         DPE.cpp:1103
+ *   DPE::~DPE                     DPE.cpp:679   dpe_destroy()
+ *   CudaSafeCall -> exit()        DPE.cpp:633   return codes + dpe_last_error()
+ *
+ * The caller (host orchestration, the reference's ProcessProblem main.cpp:411-446) keeps
+ * doing InuputInitialization (DPE.cpp:733-914: image decode/resize, camera read, depth range
+ * x0.6/x1.2, prior rescale) and the epilogue (main.cpp:427-446).
+ *
+ * Types are plain C: no torch, no HIP types.  `DpeCamera` and `DpePatchMatchParams` are
+ * layout-compatible with the reference's `Camera` (main.h:50-59) and `PatchMatchParams`
+ * (main.h:78-106); enum values match `RunState` / `PixelState` (main.h:66-76).
+ */
+#ifndef DPE_MVS_H_
+#define DPE_MVS_H_
+
+#include <stdint.h>
+#include <stddef.h>
+#ifndef __cplusplus
+#include <stdbool.h>
+#endif
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DPE_ABI_VERSION 1
+#define DPE_MAX_IMAGES 32      /* main.h:40  MAX_IMAGES     */
+#define DPE_NEIGHBOUR_NUM 9    /* main.h:41  NEIGHBOUR_NUM  */
+
+/* main.h:66-70 RunState */
+enum { DPE_FIRST_INIT = 0, DPE_REFINE_INIT = 1, DPE_REFINE_ITER = 2 };
+/* main.h:72-76 PixelState */
+enum { DPE_WEAK = 0, DPE_STRONG = 1, DPE_UNKNOWN = 2 };
+
+/* Error codes (the reference exits the process instead, DPE.cpp:633-641, :762-765). */
+enum {
+  DPE_OK = 0,
+  DPE_ERR_ARG = -1,       /* bad argument / shape */
+  DPE_ERR_HIP = -2,       /* HIP runtime error */
+  DPE_ERR_NOMEM = -3,     /* allocation failed */
+  DPE_ERR_STATE = -4,     /* call order (execute before stage, ...) */
+  DPE_ERR_TOO_MANY = -5   /* num_images > DPE_MAX_IMAGES (DPE.cpp:762) */
+};
+
+/* main.h:50-59 struct Camera (112 bytes) */
+typedef struct DpeCamera {
+  float K[9];
+  float R[9];
+  float t[3];
+  float c[3];
+  int height;
+  int width;
+  float depth_min;
+  float depth_max;
+} DpeCamera;
+
+/* main.h:78-106 struct PatchMatchParams, same field order and C types. */
+typedef struct DpePatchMatchParams {
+  int max_iterations;     /* 3 */
+  int num_images;         /* 1 ref + Ns src */
+  float sigma_spatial;    /* 5 */
+  float sigma_color;      /* 3 */
+  int top_k;              /* 4 */
+  float depth_min;
+  float depth_max;
+  bool geom_consistency;
+  int strong_radius;      /* 5 */
+  int strong_increment;   /* 2 */
+  int weak_radius;        /* 5 */
+  int weak_increment;     /* 5 */
+  bool use_APD;
+  bool use_edge;
+  bool use_limit;
+  bool use_label;
+  bool use_radius;
+  bool high_res_img;
+  int max_scale_size;
+  int scale_size;
+  int weak_peak_radius;   /* 2 */
+  int rotate_time;        /* 4 */
+  float ransac_threshold; /* 0.005 */
+  float geom_factor;      /* 0.2 */
+  int state;              /* RunState */
+} DpePatchMatchParams;
+
+/* Fills `p` with the defaults of main.h:78-106. */
+void dpe_params_default(DpePatchMatchParams* p);
+
+/*
+ * Inputs of one PatchMatch pass for one reference image, all HOST pointers, row-major.
+ * Index 0 is the reference image, 1..num_images-1 the source images (DPE.cpp:743-761).
+ */
+typedef struct DpePassInput {
+  int width, height;               /* pass resolution (after the caller's rescale) */
+  int num_images;                  /* <= DPE_MAX_IMAGES */
+  const float* const* images;      /* [num_images] -> f32 [H][W] grey levels (DPE.cpp:745-757) */
+  const DpeCamera* cams;           /* [num_images], K already scale-adjusted (DPE.cpp:814-819) */
+  const float* const* depths;      /* [num_images] -> f32 [H][W], NULL unless geom (DPE.cpp:826-843);
+                                      entry 0 may be NULL (the ref depth is never sampled) */
+  const uint8_t* edge;             /* [H][W] {0,255} edges_<scale>.dmb, or NULL (DPE.cpp:1032) */
+  int low_width, low_height;       /* size of edge_low_res */
+  const uint8_t* edge_low_res;     /* [lh][lw] edges_<max_scale>.dmb (DPE.cpp:1042), or NULL */
+  const int32_t* label;            /* [H][W] labels_<scale>.dmb, or NULL (DPE.cpp:1049) */
+  DpePatchMatchParams params;      /* params.num_images / depth_min / depth_max set by caller */
+  uint64_t seed;                   /* Philox key (the reference seeds cuRAND from clock64()) */
+  uint32_t pass_salt;              /* distinguishes passes that reuse a seed */
+} DpePassInput;
+
+/*
+ * Per-pixel state, in/out, HOST pointers.
+ *  planes:         float4 [H][W]; in: (world normal xyz, depth w) prior unless FIRST_INIT
+ *                  (DPE.cpp:896-903); out: (world normal xyz, depth w) (DPE.cu:1940-1955).
+ *  weak_info:      u8 [H][W] PixelState; in: weak.bin (ignored, all STRONG, when !use_APD,
+ *                  DPE.cpp:873-881); out: DepthToWeak classification (DPE.cu:2593-2747).
+ *  selected_views: u32 [H][W] view bit-mask, in/out (DPE.cpp:906-911).
+ *  costs:          f32 [H][W] optional output (NULL to skip); not in the reference's readback.
+ */
+typedef struct DpePassState {
+  float* planes;
+  uint8_t* weak_info;
+  uint32_t* selected_views;
+  float* costs;
+} DpePassState;
+
+typedef struct DpeContext DpeContext;
+
+/* Context = one HIP device + its workspaces.  One context per thread. */
+DpeContext* dpe_create(int device);
+void dpe_destroy(DpeContext* ctx);
+
+/* Last error message of the calling thread ("" if none). */
+const char* dpe_last_error(void);
+
+/* Uploads inputs and the initial state (H2D), builds the device layouts. Synchronous. */
+int dpe_pm_stage(DpeContext* ctx, const DpePassInput* in, const DpePassState* state);
+
+/*
+ * Runs the whole pass (DPE.cu:3150-3226) on device-resident data on `stream` (a hipStream_t,
+ * NULL = the context's stream).  Every call starts from the staged initial state, so repeated
+ * calls are idempotent.  Asynchronous w.r.t. the host.
+ */
+int dpe_pm_execute(DpeContext* ctx, void* stream);
+
+/* D2H of the outputs (DPE.cu:3245-3247).  Synchronous. */
+int dpe_pm_fetch(DpeContext* ctx, const DpePassState* state);
+
+/* stage + execute + fetch. */
+int dpe_pm_run(DpeContext* ctx, const DpePassInput* in, const DpePassState* state);
+
+/* Device pointer of the working planes buffer (float4 [H][W]) for device-side consumers
+ * (e.g. the depth all-gather of the multi-GPU schedule).  NULL before dpe_pm_stage. */
+void* dpe_pm_device_planes(DpeContext* ctx);
+
+/* Copies depth (planes.w) into a caller device buffer f32 [H][W] on `stream`. */
+int dpe_pm_export_depth(DpeContext* ctx, float* dev_dst, void* stream);
+
+/* Milliseconds of GPU time of the last dpe_pm_execute, per launch class (hipEvents):
+ * out[0] = whole pass, out[1] = strong sweeps, out[2] = weak sweeps, out[3] = DepthToWeak,
+ * out[4] = LocalRefine, out[5] = setup (edge/nearest/neighbours/init), out[6] = RANSAC fit,
+ * out[7] = filter+depth/normal.  Returns the number of entries written (<= n).
+ * Only valid when timing was enabled with dpe_set_timing(ctx, 1). */
+int dpe_pm_last_timings(DpeContext* ctx, float* out, int n);
+void dpe_set_timing(DpeContext* ctx, int enable);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DPE_MVS_H_ */

@@ -1,0 +1,171 @@
+// oracle_math.h — TEST INFRASTRUCTURE (oracle only; never linked into the product).
+//
+// Scalar arithmetic primitives of the CPU restatement of DPE-MVS's PatchMatch pass.
+// The reference (csrc/DPE-MVS/DPE.cu) is compiled with nvcc --use_fast_math
+// (CMakeLists.txt:72), so its expf/sin/cos/division bits are not IEEE and not reproducible;
+// cuRAND XORWOW is seeded from clock64() (DPE.cu:1032).  The restatement therefore fixes
+// every primitive to an exactly specified sequence of IEEE-754 binary32/binary64 operations
+// (add, mul, fma, div, sqrt, floor, rint) so that a CPU and a GPU evaluation are bit-equal:
+//   * expf / sinf / cosf / exp(double): Cody-Waite range reduction + fixed polynomials;
+//   * rsqrtf(x) (DPE.cu:271)            := 1.0f / sqrtf(x);
+//   * curand_uniform (DPE.cu:368...)    := Philox4x32-10 word u -> (float)u * 2^-32 + 2^-33
+//     (cuRAND's published uint->float conversion) ;
+//   * tex2D linear filter (DPE.cpp:927-933, CUDA texture semantics: clamp addressing for
+//     unnormalised coordinates, weights with 8 fractional bits) -> OracleSample().
+// This file is compiled with -ffp-contract=off: every fmaf below is explicit.
+#pragma once
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <climits>
+
+namespace oracle {
+
+static inline float bits_to_f(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
+static inline double bits_to_d(uint64_t u) { double f; std::memcpy(&f, &u, 8); return f; }
+
+// 2^k for k in [-126, 127]
+static inline float pow2i(int k) { return bits_to_f((uint32_t)(k + 127) << 23); }
+static inline double pow2i_d(int k) { return bits_to_d((uint64_t)(k + 1023) << 52); }
+
+// expf restatement (CUDA expf / __expf under fast-math, DPE.cu:554, 1576, 1587, 1295).
+static inline float o_expf(float x) {
+  if (x != x) return x;
+  if (x > 88.7228394f) return INFINITY;
+  if (x < -103.972084f) return 0.0f;
+  float k = rintf(x * 1.44269502f);
+  float r = fmaf(k, -0.693145752f, x);
+  r = fmaf(k, -1.42860677e-06f, r);
+  float p = 1.98412698e-4f;             // 1/5040
+  p = fmaf(p, r, 1.38888889e-3f);       // 1/720
+  p = fmaf(p, r, 8.33333377e-3f);       // 1/120
+  p = fmaf(p, r, 4.16666679e-2f);       // 1/24
+  p = fmaf(p, r, 1.66666672e-1f);       // 1/6
+  p = fmaf(p, r, 0.5f);
+  p = fmaf(p, r, 1.0f);
+  p = fmaf(p, r, 1.0f);
+  int ki = (int)k;
+  if (ki < -125) { p = p * 5.42101086e-20f; ki += 64; }   // 2^-64
+  if (ki > 127) { p = p * 2.0f; ki -= 1; }
+  return p * pow2i(ki);
+}
+
+// sin/cos restatement (DPE.cu:397-402, fast-math __sinf/__cosf).
+static inline void o_sincosf(float x, float* s, float* c) {
+  float k = rintf(x * 0.636619747f);
+  float r = fmaf(k, -1.5703125f, x);          // pi/2 split in three parts (Cody-Waite)
+  r = fmaf(k, -4.83751297e-04f, r);
+  r = fmaf(k, -7.54978995e-08f, r);
+  float r2 = r * r;
+  float ps = -1.98412698e-4f;          // -1/5040
+  ps = fmaf(ps, r2, 8.33333377e-3f);   // 1/120
+  ps = fmaf(ps, r2, -1.66666672e-1f);  // -1/6
+  ps = ps * r2;
+  float sr = fmaf(ps, r, r);
+  float pc = 2.48015876e-5f;           // 1/40320
+  pc = fmaf(pc, r2, -1.38888892e-3f);  // -1/720
+  pc = fmaf(pc, r2, 4.16666679e-2f);   // 1/24
+  pc = fmaf(pc, r2, -0.5f);
+  float cr = fmaf(pc, r2, 1.0f);
+  int q = ((int)k) & 3;
+  float so, co;
+  if (q == 0) { so = sr; co = cr; }
+  else if (q == 1) { so = cr; co = -sr; }
+  else if (q == 2) { so = -sr; co = -cr; }
+  else { so = -cr; co = sr; }
+  *s = so; *c = co;
+}
+static inline float o_sinf(float x) { float s, c; o_sincosf(x, &s, &c); return s; }
+static inline float o_cosf(float x) { float s, c; o_sincosf(x, &s, &c); return c; }
+
+// exp(double) restatement (DPE.cu:2554: 1/(1+exp(-25*(density-0.35)))).
+static inline double o_exp_d(double x) {
+  if (x != x) return x;
+  if (x > 709.0) return INFINITY;
+  if (x < -708.0) return 0.0;
+  double k = rint(x * 1.4426950408889634);
+  double r = fma(k, -6.93147180369123816490e-01, x);
+  r = fma(k, -1.90821492927058770002e-10, r);
+  double p = 1.0 / 479001600.0;   // 1/12!
+  p = fma(p, r, 1.0 / 39916800.0);
+  p = fma(p, r, 1.0 / 3628800.0);
+  p = fma(p, r, 1.0 / 362880.0);
+  p = fma(p, r, 1.0 / 40320.0);
+  p = fma(p, r, 1.0 / 5040.0);
+  p = fma(p, r, 1.0 / 720.0);
+  p = fma(p, r, 1.0 / 120.0);
+  p = fma(p, r, 1.0 / 24.0);
+  p = fma(p, r, 1.0 / 6.0);
+  p = fma(p, r, 0.5);
+  p = fma(p, r, 1.0);
+  p = fma(p, r, 1.0);
+  return p * pow2i_d((int)k);
+}
+
+static inline float o_rsqrtf(float x) { return 1.0f / sqrtf(x); }
+
+// float -> int truncation with CUDA cvt.rzi.s32 semantics (saturating, NaN -> 0).
+static inline int o_f2i(float f) {
+  if (f != f) return 0;
+  if (f >= 2147483520.0f) return INT_MAX;
+  if (f <= -2147483648.0f) return INT_MIN;
+  return (int)f;
+}
+static inline int o_d2i(double f) {
+  if (f != f) return 0;
+  if (f >= 2147483647.0) return INT_MAX;
+  if (f <= -2147483648.0) return INT_MIN;
+  return (int)f;
+}
+
+// reference macros (OpenCV cvdef.h): MIN(a,b) ((a) > (b) ? (b) : (a)), MAX(a,b) ((a) < (b) ? (b) : (a))
+template <class A, class B> static inline auto MINo(A a, B b) -> decltype(a + b) { return (a > b) ? b : a; }
+template <class A, class B> static inline auto MAXo(A a, B b) -> decltype(a + b) { return (a < b) ? b : a; }
+
+// ---------------------------------------------------------------- Philox4x32-10
+struct Philox {
+  uint32_t k0, k1;       // key: pixel index, seed
+  uint32_t stream, salt; // counter words 1, 2
+  uint32_t ctr;          // counter word 0 (block index)
+  uint32_t buf[4];
+  int idx;
+};
+
+static inline void philox_block(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1, uint32_t out[4]) {
+  for (int r = 0; r < 10; ++r) {
+    uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    uint32_t n0 = hi1 ^ c1 ^ k0;
+    uint32_t n2 = hi0 ^ c3 ^ k1;
+    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+  out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+static inline void rng_init(Philox* s, uint32_t pixel, uint64_t seed, uint32_t stream, uint32_t salt) {
+  s->k0 = pixel;
+  s->k1 = (uint32_t)seed ^ (uint32_t)(seed >> 32);
+  s->stream = stream; s->salt = salt; s->ctr = 0; s->idx = 4;
+}
+// curand(state) restatement
+static inline uint32_t rng_u32(Philox* s) {
+  if (s->idx == 4) { philox_block(s->ctr, s->stream, s->salt, 0u, s->k0, s->k1, s->buf); s->ctr++; s->idx = 0; }
+  return s->buf[s->idx++];
+}
+// curand_uniform(state) restatement: (0, 1]
+static inline float rng_uniform(Philox* s) {
+  uint32_t u = rng_u32(s);
+  return (float)u * 2.32830644e-10f + 1.16415322e-10f;
+}
+
+// RNG stream ids (the reference keeps one cuRAND state per pixel across all kernels).
+enum {
+  STREAM_GEN_NEIGHBOURS = 1,
+  STREAM_RANDOM_INIT = 2,
+  STREAM_ITER_BASE = 16   // + 4*iter + {0: strong sweep, 1: RANSAC fit, 2: weak sweep}
+};
+
+}  // namespace oracle
