@@ -18,8 +18,10 @@ LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libdpe_mvs.so")
 EXPORTED = [
     "dpe_params_default", "dpe_create", "dpe_destroy", "dpe_last_error", "dpe_pm_stage",
     "dpe_pm_execute", "dpe_pm_fetch", "dpe_pm_run", "dpe_pm_device_planes", "dpe_pm_export_depth",
-    "dpe_pm_last_timings", "dpe_set_timing",
+    "dpe_pm_last_timings", "dpe_set_timing", "dpe_set_counting", "dpe_pm_last_counts",
 ]
+
+CLASSES = ["setup", "init", "strong", "ransac", "weak", "filter", "depth_to_weak", "local_refine"]
 
 
 def load_library(path: str = LIB_PATH) -> C.CDLL:
@@ -49,6 +51,10 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.dpe_pm_last_timings.restype = C.c_int
     lib.dpe_set_timing.argtypes = [C.c_void_p, C.c_int]
     lib.dpe_set_timing.restype = None
+    lib.dpe_set_counting.argtypes = [C.c_void_p, C.c_int]
+    lib.dpe_set_counting.restype = None
+    lib.dpe_pm_last_counts.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_int]
+    lib.dpe_pm_last_counts.restype = C.c_int
     return lib
 
 
@@ -104,10 +110,25 @@ class PatchMatchContext:
         self.execute()
         return self.fetch()
 
-    def timings(self) -> list[float]:
-        buf = (C.c_float * 8)()
-        n = _LIB.dpe_pm_last_timings(self._ctx, buf, 8)
-        return [float(buf[i]) for i in range(n)]
+    def set_counting(self, on: bool):
+        _LIB.dpe_set_counting(self._ctx, 1 if on else 0)
+
+    def timings(self) -> dict:
+        """{'total': ms, <class>: summed kernel ms} of the last execute (timing enabled)."""
+        buf = (C.c_float * 9)()
+        n = _LIB.dpe_pm_last_timings(self._ctx, buf, 9)
+        out = {"total": float(buf[0])}
+        for i, name in enumerate(CLASSES):
+            if 1 + i < n:
+                out[name] = float(buf[1 + i])
+        return out
+
+    def counts(self) -> dict:
+        """{<class>: {'ncc', 'taps', 'geom', 'launches'}} of the last execute (counting enabled)."""
+        buf = (C.c_ulonglong * 32)()
+        _LIB.dpe_pm_last_counts(self._ctx, buf, 32)
+        return {name: {"ncc": int(buf[4 * i]), "taps": int(buf[4 * i + 1]), "geom": int(buf[4 * i + 2]),
+                       "launches": int(buf[4 * i + 3])} for i, name in enumerate(CLASSES)}
 
     def device_planes(self) -> int:
         return int(_LIB.dpe_pm_device_planes(self._ctx) or 0)

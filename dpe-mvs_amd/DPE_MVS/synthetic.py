@@ -108,22 +108,24 @@ def render_view(surfs, K, R, C, W, H, pix_world: float):
     d = rays_cam @ R                                                   # world directions (R^T r)
     best_t = np.full((H, W), np.inf)
     sid = np.full((H, W), -1, np.int32)
-    tex = np.zeros((H, W))
-    for k, s in enumerate(surfs):
+    for k, s in enumerate(surfs):            # visibility first: nearest surface per ray
         denom = d @ s.n
         with np.errstate(divide="ignore", invalid="ignore"):
             t = ((s.p0 - C) @ s.n) / denom
-        hit = C + t[..., None] * d
-        rel = hit - s.p0
-        u, v = rel @ s.a1, rel @ s.a2
         ok = (t > 0) & np.isfinite(t)
         if s.hu is not None:
-            ok &= (np.abs(u) <= s.hu) & (np.abs(v) <= s.hv)
+            rel = C + t[..., None] * d - s.p0
+            ok &= (np.abs(rel @ s.a1) <= s.hu) & (np.abs(rel @ s.a2) <= s.hv)
         take = ok & (t < best_t)
-        if not take.any():
-            continue
         best_t = np.where(take, t, best_t)
         sid = np.where(take, k, sid)
+    tex = np.zeros((H, W))
+    for k, s in enumerate(surfs):            # then texture only where surface k is visible
+        m = sid == k
+        if not m.any():
+            continue
+        rel = C + best_t[m][:, None] * d[m] - s.p0
+        u, v = rel @ s.a1, rel @ s.a2
         n = (0.42 * _value_noise(u, v, 2.5 * pix_world, s.salt) + 0.38 * _value_noise(u, v, 6.0 * pix_world, s.salt + 101)
              + 0.3 * _value_noise(u, v, 15.0 * pix_world, s.salt + 202))
         val = 128.0 + 95.0 * n
@@ -131,8 +133,10 @@ def render_view(surfs, K, R, C, W, H, pix_world: float):
             u0, u1, v0, v1 = s.flat_region
             flat = (u >= u0) & (u <= u1) & (v >= v0) & (v <= v1)
             val = np.where(flat, 140.0, val)
-            sid = np.where(take & flat, 100 + k, sid)
-        tex = np.where(take, val, tex)
+            ids = sid[m]
+            ids[flat] = 100 + k
+            sid[m] = ids
+        tex[m] = val
     normals = np.zeros((H, W, 3))
     for k, s in enumerate(surfs):
         for key in (k, 100 + k):

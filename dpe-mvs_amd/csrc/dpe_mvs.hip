@@ -53,8 +53,12 @@ struct DpeContext {
   hipStream_t stream = nullptr;
   bool staged = false;
   bool timing = false;
-  float timings[8] = {0};
-  hipEvent_t ev[48] = {};
+  bool counting = false;
+  float timings[DPE_NUM_CLASSES + 1] = {0};
+  int launches[DPE_NUM_CLASSES + 1] = {0};
+  unsigned long long counts[DPE_NUM_CLASSES * 4] = {0};
+  hipEvent_t ev[2 * 64] = {};
+  DevArr<unsigned long long> cnt;
   PassConst hc;                  // host copy of the pass constants
   DevArr<PassConst> dc;
   // inputs
@@ -141,6 +145,7 @@ void dpe_destroy(DpeContext* c) {
   c->weak.release(); c->weak_rel.release(); c->vw.release();
   c->nb.release(); c->nearest.release(); c->edge_neigh.release(); c->lab_bound.release();
   c->radius.release();
+  c->cnt.release();
   hipStreamDestroy(c->stream);
   delete c;
 }
@@ -294,16 +299,30 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   HIPC(hipSetDevice(c->device));
   hipStream_t s = stream_ ? (hipStream_t)stream_ : c->stream;
   const PassConst& pc = c->hc;
-  const DevBufs& B = c->bufs;
   const PassConst* dpc = c->dc.p;
   const int W = pc.W, H = pc.H, nv = pc.N - 1;
   const size_t L = (size_t)W * H;
-  hipEvent_t* ev = c->ev;
-  int ei = 0;
-  const bool timing = c->timing && (5 + 4 * pc.P.max_iterations) <= 48;
-  auto mark = [&]() { if (timing) hipEventRecord(ev[ei++], s); };
+  DevBufs B = c->bufs;
+  B.cnt = nullptr;
+  if (c->counting) {
+    HIPC(c->cnt.ensure(DPE_NUM_CLASSES * 4));
+    HIPC(hipMemsetAsync(c->cnt.p, 0, DPE_NUM_CLASSES * 4 * sizeof(unsigned long long), s));
+  }
+  // per-launch events: slot pairs (start, end) + class id
+  int nev = 0;
+  int ev_class[64];
+  const bool timing = c->timing;
+  for (int k = 0; k <= DPE_NUM_CLASSES; ++k) c->launches[k] = 0;
+  auto begin = [&](int cls) -> DevBufs {
+    DevBufs Bc = B;
+    if (c->counting) Bc.cnt = c->cnt.p + 4 * cls;
+    c->launches[cls]++;
+    if (timing && nev < 64) { ev_class[nev] = cls; hipEventRecord(c->ev[2 * nev], s); }
+    return Bc;
+  };
+  auto end = [&]() { if (timing && nev < 64) { hipEventRecord(c->ev[2 * nev + 1], s); nev++; } };
 
-  mark();   // 0
+  if (timing) hipEventRecord(c->ev[2 * 64 - 2], s);
   // initial state (the reference uploads it in CudaSpaceInitialization, DPE.cpp:964-1015)
   HIPC(hipMemcpyAsync(B.planes, c->planes0.p, L * sizeof(float4), hipMemcpyDeviceToDevice, s));
   HIPC(hipMemcpyAsync(B.weak, c->weak0.p, L, hipMemcpyDeviceToDevice, s));
@@ -323,57 +342,65 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   const dim3 hb(32, 4), hg((((W + 1) / 2) + 31) / 32, (pc.half_rows + 3) / 4);
   const size_t sweep_lds = (size_t)10 * nv * 128 * sizeof(float) + (size_t)nv * 128;
   const size_t d2w_lds = (size_t)61 * 256 * sizeof(float);
+  DevBufs Bc;
 
-  k_gen_edge_inform<<<fg, fb, 0, s>>>(dpc, B);
-  k_find_nearest_strong<<<fg, fb, 0, s>>>(dpc, B);
-  k_gen_neighbours<<<fg, fb, 0, s>>>(dpc, B);
-  k_neighbour_update<<<fg, fb, 0, s>>>(dpc, B);
-  k_random_init<<<fg, fb, 0, s>>>(dpc, B);
+  // RunPatchMatch launch sequence (DPE.cu:3150-3226)
+  Bc = begin(DPE_CLASS_SETUP);
+  k_gen_edge_inform<<<fg, fb, 0, s>>>(dpc, Bc);
+  k_find_nearest_strong<<<fg, fb, 0, s>>>(dpc, Bc);
+  k_gen_neighbours<<<fg, fb, 0, s>>>(dpc, Bc);
+  k_neighbour_update<<<fg, fb, 0, s>>>(dpc, Bc);
+  end();
+  Bc = begin(DPE_CLASS_INIT);
+  k_random_init<<<fg, fb, 0, s>>>(dpc, Bc);
+  end();
   HIPC(hipGetLastError());
-  mark();   // 1: setup done
-  float t_strong = 0, t_weak = 0, t_ransac = 0;
   for (int it = 0; it < pc.P.max_iterations; ++it) {
-    const int e0 = ei; mark();
     for (int colour = 0; colour < 2; ++colour) {
       HIPC(hipMemcpyAsync(B.planes_snap, B.planes, L * sizeof(float4), hipMemcpyDeviceToDevice, s));
       HIPC(hipMemcpyAsync(B.costs_snap, B.costs, L * sizeof(float), hipMemcpyDeviceToDevice, s));
       HIPC(hipMemcpyAsync(B.sel_snap, B.sel, L * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
-      k_strong_sweep<<<hg, hb, sweep_lds, s>>>(dpc, B, it, colour);
+      Bc = begin(DPE_CLASS_STRONG);
+      k_strong_sweep<<<hg, hb, sweep_lds, s>>>(dpc, Bc, it, colour);
+      end();
     }
     HIPC(hipGetLastError());
-    mark();
-    k_ransac_fit<<<fg, fb, 0, s>>>(dpc, B, it);
-    mark();
-    for (int colour = 0; colour < 2; ++colour) k_weak_sweep<<<hg, hb, sweep_lds, s>>>(dpc, B, it, colour);
+    Bc = begin(DPE_CLASS_RANSAC);
+    k_ransac_fit<<<fg, fb, 0, s>>>(dpc, Bc, it);
+    end();
+    for (int colour = 0; colour < 2; ++colour) {
+      Bc = begin(DPE_CLASS_WEAK);
+      k_weak_sweep<<<hg, hb, sweep_lds, s>>>(dpc, Bc, it, colour);
+      end();
+    }
     HIPC(hipGetLastError());
-    mark();
-    (void)e0;
   }
-  k_depth_normal<<<fg, fb, 0, s>>>(dpc, B);
-  for (int colour = 0; colour < 2; ++colour) k_filter<<<hg, hb, 0, s>>>(dpc, B, colour);
-  mark();
-  k_depth_to_weak<<<fg, fb, d2w_lds, s>>>(dpc, B);
-  mark();
-  k_local_refine<<<fg, fb, 0, s>>>(dpc, B);
-  mark();
+  Bc = begin(DPE_CLASS_FILTER);
+  k_depth_normal<<<fg, fb, 0, s>>>(dpc, Bc);
+  for (int colour = 0; colour < 2; ++colour) k_filter<<<hg, hb, 0, s>>>(dpc, Bc, colour);
+  end();
+  Bc = begin(DPE_CLASS_DEPTH_TO_WEAK);
+  k_depth_to_weak<<<fg, fb, d2w_lds, s>>>(dpc, Bc);
+  end();
+  Bc = begin(DPE_CLASS_LOCAL_REFINE);
+  k_local_refine<<<fg, fb, 0, s>>>(dpc, Bc);
+  end();
   HIPC(hipGetLastError());
-  if (timing) {
-    HIPC(hipEventSynchronize(ev[ei - 1]));
-    float t;
-    auto el = [&](int a, int b) { float ms = 0; hipEventElapsedTime(&ms, ev[a], ev[b]); return ms; };
-    t = el(0, ei - 1); c->timings[0] = t;
-    c->timings[5] = el(0, 1);
-    int k = 2;
-    for (int it = 0; it < pc.P.max_iterations; ++it) {
-      t_strong += el(k, k + 1); t_ransac += el(k + 1, k + 2); t_weak += el(k + 2, k + 3);
-      k += 4;
+  if (timing && nev > 0) {
+    HIPC(hipEventSynchronize(c->ev[2 * nev - 1]));
+    for (int k = 0; k <= DPE_NUM_CLASSES; ++k) c->timings[k] = 0.0f;
+    float ms = 0;
+    hipEventElapsedTime(&ms, c->ev[2 * 64 - 2], c->ev[2 * nev - 1]);
+    c->timings[0] = ms;
+    for (int e = 0; e < nev; ++e) {
+      hipEventElapsedTime(&ms, c->ev[2 * e], c->ev[2 * e + 1]);
+      c->timings[1 + ev_class[e]] += ms;
     }
-    // k now points one past the last iteration's final mark
-    const int base = 2 + 4 * pc.P.max_iterations - 1;
-    c->timings[1] = t_strong; c->timings[2] = t_weak; c->timings[6] = t_ransac;
-    c->timings[7] = el(base, base + 1);
-    c->timings[3] = el(base + 1, base + 2);
-    c->timings[4] = el(base + 2, base + 3);
+  }
+  if (c->counting) {
+    HIPC(hipMemcpyAsync(c->counts, c->cnt.p, sizeof(c->counts), hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    for (int k = 0; k < DPE_NUM_CLASSES; ++k) c->counts[4 * k + 3] = (unsigned long long)c->launches[k];
   }
   return DPE_OK;
 }
@@ -422,7 +449,16 @@ extern "C" int dpe_pm_export_depth(DpeContext* c, float* dev_dst, void* stream_)
 
 extern "C" int dpe_pm_last_timings(DpeContext* c, float* out, int n) {
   if (!c || !out) return 0;
-  const int m = n < 8 ? n : 8;
+  const int m = n < DPE_NUM_CLASSES + 1 ? n : DPE_NUM_CLASSES + 1;
   for (int i = 0; i < m; ++i) out[i] = c->timings[i];
+  return m;
+}
+
+extern "C" void dpe_set_counting(DpeContext* c, int enable) { if (c) c->counting = enable != 0; }
+
+extern "C" int dpe_pm_last_counts(DpeContext* c, unsigned long long* out, int n) {
+  if (!c || !out) return 0;
+  const int m = n < DPE_NUM_CLASSES * 4 ? n : DPE_NUM_CLASSES * 4;
+  for (int i = 0; i < m; ++i) out[i] = c->counts[i];
   return m;
 }

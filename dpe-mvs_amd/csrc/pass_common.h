@@ -45,7 +45,14 @@ struct DevBufs {
   short2* nb; short2* nearest; short2* edge_neigh; short2* lab_bound;
   int* radius;
   const uint8_t* edge; const uint8_t* edge_low; const int* label;
+  // algorithmic work counters of the launch class (nullptr unless counting):
+  // [0] homographies (NCC set-ups), [1] bilinear taps, [2] geometric-consistency evaluations
+  unsigned long long* cnt;
 };
+
+DEV void count_work(const DevBufs& B, unsigned long long ncc, unsigned long long taps) {
+  if (B.cnt) { atomicAdd(B.cnt + 0, ncc); atomicAdd(B.cnt + 1, taps); }
+}
 
 // ------------------------------------------------------------------------------ bits
 DEV void setBit(uint32_t& v, unsigned n) { v |= (1u << n); }
@@ -241,6 +248,7 @@ DEV float patch_ncc_generic(const PassConst& pc, const DevBufs& B, const float4*
     }
     s_ref += r_ref; s_rr += r_rr; s_src += r_src; s_ss += r_ss; s_rs += r_rs; s_w += r_w;
   }
+  if (B.cnt) { const unsigned long long n = (unsigned long long)(2 * radius / increment + 1); count_work(B, 0, n * n); }
   return ncc_finalize(s_ref, s_rr, s_w, s_src, s_ss, s_rs);
 }
 
@@ -253,6 +261,7 @@ DEV bool center_outside(const PassConst& pc, int v, const Homog& H, int px, int 
 // ComputeBilateralNCCOld (DPE.cu:692-778), weights per tap.
 DEV float ncc_old_generic(const PassConst& pc, const DevBufs& B, int px, int py, int v, const float4& pl) {
   const Homog H = make_homography(pc, v, pl);
+  count_work(B, 1, 0);
   if (center_outside(pc, v, H, px, py)) return 2.0f;
   const float rc = ref_texel(B.ref, pc.W, pc.H, px, py);
   return patch_ncc_generic(pc, B, B.imgq[v], H, px, py, rc, pc.P.strong_radius, pc.P.strong_increment);
@@ -293,7 +302,8 @@ DEV void make_patch36(Patch36& P, const PassConst& pc, const DevBufs& B, int px,
 }
 DEV float ncc_old_patch36(const Patch36& P, const PassConst& pc, const DevBufs& B, int v, const float4& pl) {
   const Homog H = make_homography(pc, v, pl);
-  if (center_outside(pc, v, H, P.px, P.py)) return 2.0f;
+  if (center_outside(pc, v, H, P.px, P.py)) { count_work(B, 1, 0); return 2.0f; }
+  count_work(B, 1, 36);
   const float4* __restrict__ src = B.imgq[v];
   const int W = pc.W, Hh = pc.H;
   float s_src = 0, s_ss = 0, s_rs = 0;
@@ -334,6 +344,7 @@ DEV float ncc_new(const PassConst& pc, const DevBufs& B, int px, int py, int v, 
   const int W = pc.W, Hh = pc.H;
   const int center = px + py * W;
   const Homog H = make_homography(pc, v, pl);
+  count_work(B, 1, 0);
   if (center_outside(pc, v, H, px, py)) return 2.0f;
   float cost = 0.0f;
   if (B.weak[center] != DPE_WEAK) return cost;
@@ -374,6 +385,7 @@ DEV float ncc_new(const PassConst& pc, const DevBufs& B, int px, int py, int v, 
 
 // ComputeGeomConsistencyCost (DPE.cu:915-953)
 DEV float geom_cost(const PassConst& pc, const DevBufs& B, int px, int py, int v, const float4& pl) {
+  if (B.cnt) atomicAdd(B.cnt + 2, 1ull);
   const DpeCamera& rc = pc.cams[0];
   const DpeCamera& sc = pc.cams[v];
   const float depth = depth_from_plane(rc, pl, px, py);

@@ -167,13 +167,30 @@ void* dpe_pm_device_planes(DpeContext* ctx);
 /* Copies depth (planes.w) into a caller device buffer f32 [H][W] on `stream`. */
 int dpe_pm_export_depth(DpeContext* ctx, float* dev_dst, void* stream);
 
-/* Milliseconds of GPU time of the last dpe_pm_execute, per launch class (hipEvents):
- * out[0] = whole pass, out[1] = strong sweeps, out[2] = weak sweeps, out[3] = DepthToWeak,
- * out[4] = LocalRefine, out[5] = setup (edge/nearest/neighbours/init), out[6] = RANSAC fit,
- * out[7] = filter+depth/normal.  Returns the number of entries written (<= n).
- * Only valid when timing was enabled with dpe_set_timing(ctx, 1). */
-int dpe_pm_last_timings(DpeContext* ctx, float* out, int n);
+/* Kernel classes of one pass, for timing and work accounting. */
+enum {
+  DPE_CLASS_SETUP = 0,        /* GenEdgeInform, FindNearestStrongPoint, GenNeighbours, NeigbourUpdate */
+  DPE_CLASS_INIT = 1,         /* RandomInitialization */
+  DPE_CLASS_STRONG = 2,       /* Black/RedPixelUpdateStrong */
+  DPE_CLASS_RANSAC = 3,       /* RANSACToGetFitPlane */
+  DPE_CLASS_WEAK = 4,         /* Black/RedPixelUpdateWeak */
+  DPE_CLASS_FILTER = 5,       /* GetDepthandNormal + Black/RedPixelFilterStrong */
+  DPE_CLASS_DEPTH_TO_WEAK = 6,/* DepthToWeak */
+  DPE_CLASS_LOCAL_REFINE = 7, /* LocalRefine */
+  DPE_NUM_CLASSES = 8
+};
+
+/* Enables hipEvent timing of every launch of the following dpe_pm_execute calls. */
 void dpe_set_timing(DpeContext* ctx, int enable);
+/* ms[0] = whole pass (first to last event), ms[1 + c] = summed kernel time of class c.
+ * Returns the number of entries written (<= n, at most 1 + DPE_NUM_CLASSES). */
+int dpe_pm_last_timings(DpeContext* ctx, float* ms, int n);
+
+/* Enables algorithmic work counters (device atomics; a counting run is slower and is never the
+ * timed run).  out[4*c + k] for class c: k=0 homography set-ups (NCC evaluations), k=1 bilinear
+ * taps, k=2 geometric-consistency evaluations, k=3 launches.  Returns entries written. */
+void dpe_set_counting(DpeContext* ctx, int enable);
+int dpe_pm_last_counts(DpeContext* ctx, unsigned long long* out, int n);
 
 #ifdef __cplusplus
 }

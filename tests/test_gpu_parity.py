@@ -1,0 +1,121 @@
+"""GPU parity: the HIP path (through the C-ABI) is bit-exact against the CPU restatement.
+
+Tolerance: 0 — planes (depth + normal), costs, weak_info and selected_views must be
+bit-identical (the north star asks depth within 1e-3 relative and weak/edge maps bit-exact;
+the shared IEEE arithmetic makes every output exact).
+"""
+import numpy as np
+import pytest
+
+import oracle
+from DPE_MVS import _abi, synthetic
+from golden_io import bits_equal, load, names
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from DPE_MVS import native
+    c = native.PatchMatchContext(0)
+    yield c
+    c.close()
+
+
+def assert_same(g, o, what=""):
+    for k in ("planes", "weak", "sel", "costs"):
+        if not bits_equal(g[k], o[k]):
+            a, b = g[k], o[k]
+            neq = (a.view(np.uint32) != b.view(np.uint32)) if a.dtype == np.float32 else (a != b)
+            if neq.ndim == 3:
+                neq = neq.any(-1)
+            ys, xs = np.nonzero(neq)
+            pytest.fail(f"{what}: {k} differs at {len(ys)} pixels, first ({ys[0]}, {xs[0]})")
+
+
+@pytest.mark.parametrize("name", names())
+def test_gpu_matches_golden(ctx, name):
+    inp, st, exp = load(name)
+    assert_same(ctx.run(inp, st), exp, name)
+
+
+def _params(kind, iters=3):
+    p = _abi.default_params()
+    p.max_iterations = iters
+    if kind == "first":
+        p.state = _abi.FIRST_INIT; p.use_APD = False; p.use_edge = False
+    elif kind == "refine_init":
+        p.state = _abi.REFINE_INIT; p.rotate_time = 4; p.ransac_threshold = 0.0075; p.max_scale_size = 4
+        p.weak_peak_radius = 6
+    elif kind == "refine_iter":
+        p.state = _abi.REFINE_ITER; p.geom_consistency = True; p.rotate_time = 2; p.ransac_threshold = 0.00875
+        p.max_scale_size = 2; p.weak_peak_radius = 2
+    elif kind == "refine_iter_lowres":
+        p.state = _abi.REFINE_ITER; p.geom_consistency = True; p.rotate_time = 1; p.ransac_threshold = 0.01
+        p.high_res_img = False; p.use_label = True; p.weak_peak_radius = 4
+    return p
+
+
+CASES = [
+    # W, H, views, kind
+    (96, 72, 4, "first"),
+    (96, 72, 4, "refine_init"),
+    (128, 96, 6, "refine_iter"),
+    (77, 33, 3, "refine_iter"),          # odd H with (H/2) % 16 == 0: last row outside the red/black grid
+    (64, 48, 2, "first"),                # 1 source view
+    (72, 54, 5, "refine_iter_lowres"),
+]
+
+
+@pytest.mark.parametrize("W,H,N,kind", CASES)
+def test_gpu_matches_oracle(ctx, W, H, N, kind):
+    sc = synthetic.make_scene(W, H, N)
+    p = _params(kind)
+    geom = kind.startswith("refine_iter")
+    st = synthetic.first_init_state(sc) if kind == "first" else synthetic.gt_state(sc, seed=W + H)
+    inp = synthetic.pass_input(sc, p, depths=synthetic.src_depths(sc) if geom else None, seed=W * 7 + N)
+    assert_same(ctx.run(inp, st), oracle.run_pass(inp, st), f"{W}x{H}x{N} {kind}")
+
+
+def test_gpu_many_views(ctx):
+    # 32 images = the reference's MAX_IMAGES (31 source views, 32-bit view masks)
+    sc = synthetic.make_scene(48, 36, 32)
+    p = _params("refine_iter", iters=1)
+    st = synthetic.gt_state(sc)
+    inp = synthetic.pass_input(sc, p, depths=synthetic.src_depths(sc))
+    assert_same(ctx.run(inp, st), oracle.run_pass(inp, st), "32 views")
+
+
+def test_gpu_nondefault_patch(ctx):
+    # strong_radius / increment other than 5 / 2 take the generic (per-tap weight) NCC path
+    sc = synthetic.make_scene(64, 48, 3)
+    p = _params("first", iters=1)
+    p.strong_radius = 4; p.strong_increment = 1
+    inp = synthetic.pass_input(sc, p)
+    st = synthetic.first_init_state(sc)
+    assert_same(ctx.run(inp, st), oracle.run_pass(inp, st), "radius 4 / increment 1")
+
+
+def test_execute_idempotent_and_deterministic(ctx):
+    sc = synthetic.make_scene(160, 120, 5)
+    p = _params("refine_iter")
+    st = synthetic.gt_state(sc)
+    inp = synthetic.pass_input(sc, p, depths=synthetic.src_depths(sc))
+    ctx.stage(inp, st)
+    ctx.execute(); a = ctx.fetch()
+    ctx.execute(); b = ctx.fetch()
+    for k in a:
+        assert bits_equal(a[k], b[k]), k
+
+
+def test_error_paths(ctx):
+    from DPE_MVS import native
+    sc = synthetic.make_scene(32, 24, 2)
+    p = _params("refine_iter")
+    inp = synthetic.pass_input(sc, p, depths=None)          # geom without depth maps
+    with pytest.raises(native.DpeError):
+        ctx.run(inp, synthetic.gt_state(sc))
+    fresh = native.PatchMatchContext(0)
+    with pytest.raises(native.DpeError):
+        fresh.execute()                                      # execute before stage
+    fresh.close()
