@@ -16,8 +16,12 @@
 #include <vector>
 
 #include "pass_kernels.h"
+#include "pass_refine.h"
+#include "pass_sweep.h"
 
 using namespace dpe;
+
+static const int kDefaultXcdRows = 1;
 
 namespace {
 
@@ -64,6 +68,8 @@ struct DpeContext {
   // inputs
   DevArr<float> img_plain[DPE_MAX_IMAGES];  // plain f32 images (ref used directly)
   DevArr<float4> imgq[DPE_MAX_IMAGES];
+  DevArr<uint32_t> imgq8[DPE_MAX_IMAGES];
+  bool img8 = false;                 // all images are 8-bit grey levels -> u8 quad layout
   DevArr<float> depth[DPE_MAX_IMAGES];
   DevArr<uint8_t> edge, edge_low;
   DevArr<int> label;
@@ -78,6 +84,8 @@ struct DpeContext {
   DevArr<uint8_t> weak, weak_rel, vw;
   DevArr<short2> nb, nearest, edge_neigh, lab_bound;
   DevArr<int> radius;
+  DevArr<int> tab_right, tab_down;   // FindNearestStrongPoint tables
+  DevArr<int> lists, row_counts, list_totals;   // per-colour pixel lists for the sweeps
   DevBufs bufs;
 };
 
@@ -136,7 +144,7 @@ void dpe_destroy(DpeContext* c) {
   hipStreamSynchronize(c->stream);
   for (auto& e : c->ev) hipEventDestroy(e);
   c->dc.release();
-  for (int i = 0; i < DPE_MAX_IMAGES; ++i) { c->img_plain[i].release(); c->imgq[i].release(); c->depth[i].release(); }
+  for (int i = 0; i < DPE_MAX_IMAGES; ++i) { c->img_plain[i].release(); c->imgq[i].release(); c->imgq8[i].release(); c->depth[i].release(); }
   c->edge.release(); c->edge_low.release(); c->label.release();
   c->planes0.release(); c->weak0.release(); c->sel0.release();
   c->planes.release(); c->planes_snap.release(); c->fit_plane.release();
@@ -146,6 +154,8 @@ void dpe_destroy(DpeContext* c) {
   c->nb.release(); c->nearest.release(); c->edge_neigh.release(); c->lab_bound.release();
   c->radius.release();
   c->cnt.release();
+  c->tab_right.release(); c->tab_down.release();
+  c->lists.release(); c->row_counts.release(); c->list_totals.release();
   hipStreamDestroy(c->stream);
   delete c;
 }
@@ -240,13 +250,30 @@ extern "C" int dpe_pm_stage(DpeContext* c, const DpePassInput* in, const DpePass
   DevBufs& B = c->bufs;
   std::memset(&B, 0, sizeof(B));
   const dim3 qb(16, 16), qg((W + 2 + 15) / 16, (H + 2 + 15) / 16);
+  // u8 layout when every grey level is an integer in [0, 255] (images decoded from 8-bit files;
+  // a rescaled pyramid level is not): identical sample values, a quarter of the gather bytes
+  bool img8 = true;
+  for (int i = 0; i < N && img8; ++i) {
+    const float* im = in->images[i];
+    for (size_t k = 0; k < L; ++k) {
+      const float v = im[k];
+      if (!(v >= 0.0f && v <= 255.0f) || v != (float)(int)v) { img8 = false; break; }
+    }
+  }
+  c->img8 = img8;
   for (int i = 0; i < N; ++i) {
     HIPC(c->img_plain[i].ensure(L));
-    HIPC(c->imgq[i].ensure((size_t)(W + 2) * (H + 2)));
     HIPC(hipMemcpyAsync(c->img_plain[i].p, in->images[i], L * sizeof(float), hipMemcpyHostToDevice, c->stream));
-    k_build_quad<<<qg, qb, 0, c->stream>>>(c->img_plain[i].p, c->imgq[i].p, W, H);
+    if (img8) {
+      HIPC(c->imgq8[i].ensure((size_t)(W + 2) * (H + 2)));
+      k_build_quad8<<<qg, qb, 0, c->stream>>>(c->img_plain[i].p, c->imgq8[i].p, W, H);
+      B.imgq8[i] = c->imgq8[i].p;
+    } else {
+      HIPC(c->imgq[i].ensure((size_t)(W + 2) * (H + 2)));
+      k_build_quad<<<qg, qb, 0, c->stream>>>(c->img_plain[i].p, c->imgq[i].p, W, H);
+      B.imgq[i] = c->imgq[i].p;
+    }
     HIPC(hipGetLastError());
-    B.imgq[i] = c->imgq[i].p;
   }
   B.ref = c->img_plain[0].p;
   if (P.geom_consistency) {
@@ -281,6 +308,8 @@ extern "C" int dpe_pm_stage(DpeContext* c, const DpePassInput* in, const DpePass
   HIPC(c->weak.ensure(L)); HIPC(c->weak_rel.ensure(L)); HIPC(c->vw.ensure(L * DPE_MAX_IMAGES));
   HIPC(c->nb.ensure(L * 9)); HIPC(c->nearest.ensure(L)); HIPC(c->edge_neigh.ensure(L * 8)); HIPC(c->lab_bound.ensure(L * 8));
   HIPC(c->radius.ensure(L));
+  HIPC(c->tab_right.ensure(L)); HIPC(c->tab_down.ensure(L));
+  HIPC(c->lists.ensure(4 * (L / 2 + 64))); HIPC(c->row_counts.ensure(4 * (size_t)H + 4)); HIPC(c->list_totals.ensure(4));
   B.planes = c->planes.p; B.planes_snap = c->planes_snap.p; B.fit_plane = c->fit_plane.p;
   B.costs = c->costs.p; B.costs_snap = c->costs_snap.p; B.complex_ = c->complex_.p;
   B.sel = c->sel.p; B.sel_snap = c->sel_snap.p;
@@ -304,6 +333,10 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   const size_t L = (size_t)W * H;
   DevBufs B = c->bufs;
   B.cnt = nullptr;
+  {   // tuning knob: block rows per XCD chunk (see xcd_remap); DPE_XCD_ROWS=0 disables
+    const char* e = getenv("DPE_XCD_ROWS");
+    B.xcd_rows = e ? atoi(e) : kDefaultXcdRows;
+  }
   if (c->counting) {
     HIPC(c->cnt.ensure(DPE_NUM_CLASSES * 4));
     HIPC(hipMemsetAsync(c->cnt.p, 0, DPE_NUM_CLASSES * 4 * sizeof(unsigned long long), s));
@@ -341,18 +374,24 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   const dim3 fb(16, 16), fg((W + 15) / 16, (H + 15) / 16);
   const dim3 hb(32, 4), hg((((W + 1) / 2) + 31) / 32, (pc.half_rows + 3) / 4);
   const size_t sweep_lds = (size_t)10 * nv * 128 * sizeof(float) + (size_t)nv * 128;
-  const size_t d2w_lds = (size_t)61 * 256 * sizeof(float);
   DevBufs Bc;
 
   // RunPatchMatch launch sequence (DPE.cu:3150-3226)
   Bc = begin(DPE_CLASS_SETUP);
   k_gen_edge_inform<<<fg, fb, 0, s>>>(dpc, Bc);
-  k_find_nearest_strong<<<fg, fb, 0, s>>>(dpc, Bc);
+  k_strong_tables_rows<<<(H + 63) / 64, 64, 0, s>>>(dpc, Bc, c->tab_right.p);
+  k_strong_tables_cols<<<(W + 63) / 64, 64, 0, s>>>(dpc, Bc, c->tab_down.p);
+  k_find_nearest_strong<<<fg, fb, 0, s>>>(dpc, Bc, c->tab_right.p, c->tab_down.p);
   k_gen_neighbours<<<fg, fb, 0, s>>>(dpc, Bc);
   k_neighbour_update<<<fg, fb, 0, s>>>(dpc, Bc);
+  // per-colour pixel lists of the sweeps (weak_info is fixed from here until DepthToWeak)
+  const long list_stride = (long)(L / 2 + 64);
+  k_list_count<<<(pc.half_rows + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p);
+  k_list_scan<<<1, 64, 0, s>>>(dpc, c->row_counts.p, c->list_totals.p);
+  k_list_fill<<<(pc.half_rows + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p, c->lists.p, list_stride);
   end();
   Bc = begin(DPE_CLASS_INIT);
-  k_random_init<<<fg, fb, 0, s>>>(dpc, Bc);
+  if (c->img8) k_random_init<true><<<fg, fb, 0, s>>>(dpc, Bc); else k_random_init<false><<<fg, fb, 0, s>>>(dpc, Bc);
   end();
   HIPC(hipGetLastError());
   for (int it = 0; it < pc.P.max_iterations; ++it) {
@@ -361,7 +400,21 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
       HIPC(hipMemcpyAsync(B.costs_snap, B.costs, L * sizeof(float), hipMemcpyDeviceToDevice, s));
       HIPC(hipMemcpyAsync(B.sel_snap, B.sel, L * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
       Bc = begin(DPE_CLASS_STRONG);
-      k_strong_sweep<<<hg, hb, sweep_lds, s>>>(dpc, Bc, it, colour);
+      {
+        const int* lst = c->lists.p + (colour * 2 + 0) * list_stride;
+        const int* cnt = c->list_totals.p + colour * 2 + 0;
+        const bool edge = pc.P.use_edge;
+        const int P = edge ? 4 : 8, C = edge ? 16 : 8;
+        const size_t lds = (size_t)4 * strong_lds_per_wave(P, C, nv) * sizeof(float);
+        const unsigned grid = (unsigned)((L / 2 + 1 + 4 * P - 1) / (4 * P));
+        if (edge) {
+          if (c->img8) k_strong_coop<true, true><<<grid, 256, lds, s>>>(dpc, Bc, it, lst, cnt);
+          else k_strong_coop<false, true><<<grid, 256, lds, s>>>(dpc, Bc, it, lst, cnt);
+        } else {
+          if (c->img8) k_strong_coop<true, false><<<grid, 256, lds, s>>>(dpc, Bc, it, lst, cnt);
+          else k_strong_coop<false, false><<<grid, 256, lds, s>>>(dpc, Bc, it, lst, cnt);
+        }
+      }
       end();
     }
     HIPC(hipGetLastError());
@@ -370,7 +423,8 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
     end();
     for (int colour = 0; colour < 2; ++colour) {
       Bc = begin(DPE_CLASS_WEAK);
-      k_weak_sweep<<<hg, hb, sweep_lds, s>>>(dpc, Bc, it, colour);
+      if (c->img8) k_weak_sweep<true><<<hg, hb, sweep_lds, s>>>(dpc, Bc, it, colour);
+      else k_weak_sweep<false><<<hg, hb, sweep_lds, s>>>(dpc, Bc, it, colour);
       end();
     }
     HIPC(hipGetLastError());
@@ -380,10 +434,12 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   for (int colour = 0; colour < 2; ++colour) k_filter<<<hg, hb, 0, s>>>(dpc, Bc, colour);
   end();
   Bc = begin(DPE_CLASS_DEPTH_TO_WEAK);
-  k_depth_to_weak<<<fg, fb, d2w_lds, s>>>(dpc, Bc);
+  if (c->img8) k_depth_to_weak<true><<<(unsigned)((L + 3) / 4), 256, 0, s>>>(dpc, Bc);
+  else k_depth_to_weak<false><<<(unsigned)((L + 3) / 4), 256, 0, s>>>(dpc, Bc);
   end();
   Bc = begin(DPE_CLASS_LOCAL_REFINE);
-  k_local_refine<<<fg, fb, 0, s>>>(dpc, Bc);
+  if (c->img8) k_local_refine<true><<<(unsigned)((L + 19) / 20), 256, 0, s>>>(dpc, Bc);
+  else k_local_refine<false><<<(unsigned)((L + 19) / 20), 256, 0, s>>>(dpc, Bc);
   end();
   HIPC(hipGetLastError());
   if (timing && nev > 0) {

@@ -35,7 +35,8 @@ struct PassConst {
 };
 
 struct DevBufs {
-  const float4* imgq[DPE_MAX_IMAGES];
+  const float4* imgq[DPE_MAX_IMAGES];     // f32 quad-texel images (any grey levels)
+  const uint32_t* imgq8[DPE_MAX_IMAGES];  // u8 quad-texel images (8-bit grey levels: same values, 4 B/tap)
   const float* depth[DPE_MAX_IMAGES];
   const float* ref;
   float4* planes; float4* planes_snap; float4* fit_plane;
@@ -48,10 +49,25 @@ struct DevBufs {
   // algorithmic work counters of the launch class (nullptr unless counting):
   // [0] homographies (NCC set-ups), [1] bilinear taps, [2] geometric-consistency evaluations
   unsigned long long* cnt;
+  int xcd_rows;   // block rows per XCD chunk (0 = dispatcher order)
 };
 
 DEV void count_work(const DevBufs& B, unsigned long long ncc, unsigned long long taps) {
   if (B.cnt) { atomicAdd(B.cnt + 0, ncc); atomicAdd(B.cnt + 1, taps); }
+}
+
+// XCD-aware workgroup order.  The dispatcher deals workgroups round-robin to the 8 XCDs, each with
+// its own 4 MB L2 (MI355X_MICROARCH.md), so neighbouring tiles land on different L2s.  The remap
+// gives XCD k every 8th chunk of `chunk` consecutive logical workgroups (a band of block rows):
+// an XCD's in-flight tiles then share source-image footprints in its L2, while the interleave keeps
+// spatially clustered work (the WEAK regions) spread over all XCDs.  Bijective; speed only.
+DEV int xcd_remap(int b, int nb, int chunk) {
+  if (chunk <= 0) return b;
+  const int super = 8 * chunk;
+  const int S = (nb / super) * super;
+  if (b >= S) return b;
+  const int xcd = b & 7, pos = b >> 3;
+  return ((pos / chunk) * 8 + xcd) * chunk + (pos % chunk);
 }
 
 // ------------------------------------------------------------------------------ bits
@@ -198,6 +214,27 @@ DEV float sample_quad(const float4* __restrict__ q, int W, int H, float sx, floa
   const float r1 = __builtin_fmaf(ax, t.w - t.z, t.z);
   return __builtin_fmaf(ay, r1 - r0, r0);
 }
+// Same sampler on the u8 quad image: the four grey levels are exact small integers, so the floats
+// fed to the interpolation are identical to the f32 layout's.
+DEV float sample_quad8(const uint32_t* __restrict__ q, int W, int H, float sx, float sy) {
+  const float xb = __builtin_fminf(__builtin_fmaxf(sx, -1.0f), (float)W);
+  const float yb = __builtin_fminf(__builtin_fmaxf(sy, -1.0f), (float)H);
+  const int ux = (int)__builtin_fmaf(xb, 256.0f, 256.5f);
+  const int uy = (int)__builtin_fmaf(yb, 256.0f, 256.5f);
+  const float ax = (float)(ux & 255) * 0.00390625f;
+  const float ay = (float)(uy & 255) * 0.00390625f;
+  const uint32_t t = q[(uy >> 8) * (W + 2) + (ux >> 8)];
+  const float t00 = (float)(t & 255u), t10 = (float)((t >> 8) & 255u);
+  const float t01 = (float)((t >> 16) & 255u), t11 = (float)(t >> 24);
+  const float r0 = __builtin_fmaf(ax, t10 - t00, t00);
+  const float r1 = __builtin_fmaf(ax, t11 - t01, t01);
+  return __builtin_fmaf(ay, r1 - r0, r0);
+}
+template <bool U8> DEV float sample_src(const DevBufs& B, int v, int W, int H, float sx, float sy) {
+  if constexpr (U8) return sample_quad8(B.imgq8[v], W, H, sx, sy);
+  else return sample_quad(B.imgq[v], W, H, sx, sy);
+}
+
 DEV float depth_texel(const float* d, int W, int H, float x, float y) {   // DPE.cu:936
   return ref_texel(d, W, H, f2i(x), f2i(y));
 }
@@ -223,7 +260,8 @@ DEV float ncc_finalize(float s_ref, float s_rr, float s_w, float s_src, float s_
 
 // Generic bilateral NCC of one patch, weights computed per tap (NCC-New neighbour patches and
 // non-default radius/increment).  Same arithmetic order as the oracle's PatchNCC.
-DEV float patch_ncc_generic(const PassConst& pc, const DevBufs& B, const float4* __restrict__ src, const Homog& H,
+template <bool U8>
+DEV float patch_ncc_generic(const PassConst& pc, const DevBufs& B, int v, const Homog& H,
                             int cx, int cy, float rcp, int radius, int increment) {
   const int W = pc.W, Hh = pc.H;
   const float ss = pc.P.sigma_spatial, sc = pc.P.sigma_color;
@@ -235,7 +273,7 @@ DEV float patch_ncc_generic(const PassConst& pc, const DevBufs& B, const float4*
       const int y = cy + j;
       const float rp = ref_texel(B.ref, W, Hh, x, y);
       const float2 sp_ = project_h(H, (float)x, (float)y);
-      const float sp = sample_quad(src, W, Hh, sp_.x, sp_.y);
+      const float sp = sample_src<U8>(B, v, W, Hh, sp_.x, sp_.y);
       const float w = bilateral_weight(i, j, rp, rcp, ss, sc);
       const float wr = w * rp;
       r_ref = r_ref + wr;
@@ -259,12 +297,13 @@ DEV bool center_outside(const PassConst& pc, int v, const Homog& H, int px, int 
 }
 
 // ComputeBilateralNCCOld (DPE.cu:692-778), weights per tap.
+template <bool U8>
 DEV float ncc_old_generic(const PassConst& pc, const DevBufs& B, int px, int py, int v, const float4& pl) {
   const Homog H = make_homography(pc, v, pl);
   count_work(B, 1, 0);
   if (center_outside(pc, v, H, px, py)) return 2.0f;
   const float rc = ref_texel(B.ref, pc.W, pc.H, px, py);
-  return patch_ncc_generic(pc, B, B.imgq[v], H, px, py, rc, pc.P.strong_radius, pc.P.strong_increment);
+  return patch_ncc_generic<U8>(pc, B, v, H, px, py, rc, pc.P.strong_radius, pc.P.strong_increment);
 }
 
 // Reference patch of the Old NCC with the default radius 5 / increment 2 (36 taps), precomputed
@@ -300,11 +339,11 @@ DEV void make_patch36(Patch36& P, const PassConst& pc, const DevBufs& B, int px,
   }
   P.s_ref = s_ref; P.s_rr = s_rr; P.s_w = s_w;
 }
+template <bool U8>
 DEV float ncc_old_patch36(const Patch36& P, const PassConst& pc, const DevBufs& B, int v, const float4& pl) {
   const Homog H = make_homography(pc, v, pl);
   if (center_outside(pc, v, H, P.px, P.py)) { count_work(B, 1, 0); return 2.0f; }
   count_work(B, 1, 36);
-  const float4* __restrict__ src = B.imgq[v];
   const int W = pc.W, Hh = pc.H;
   float s_src = 0, s_ss = 0, s_rs = 0;
 #pragma unroll
@@ -321,7 +360,7 @@ DEV float ncc_old_patch36(const Patch36& P, const PassConst& pc, const DevBufs& 
       const float qy = __builtin_fmaf(H.h[4], y, by);
       const float qz = __builtin_fmaf(H.h[7], y, bz);
       const float iz = 1.0f / qz;
-      const float sp = sample_quad(src, W, Hh, qx * iz, qy * iz);
+      const float sp = sample_src<U8>(B, v, W, Hh, qx * iz, qy * iz);
       const float w = P.w[a * 6 + b], wr = P.wr[a * 6 + b];
       r_src = __builtin_fmaf(w, sp, r_src);
       const float ws = w * sp;
@@ -334,12 +373,14 @@ DEV float ncc_old_patch36(const Patch36& P, const PassConst& pc, const DevBufs& 
 }
 
 // Old NCC through the cached patch when the pass uses the default 5/2 patch, else generic.
+template <bool U8>
 DEV float ncc_old(const Patch36& P, bool fast, const PassConst& pc, const DevBufs& B, int v, const float4& pl) {
-  if (fast) return ncc_old_patch36(P, pc, B, v, pl);
-  return ncc_old_generic(pc, B, P.px, P.py, v, pl);
+  if (fast) return ncc_old_patch36<U8>(P, pc, B, v, pl);
+  return ncc_old_generic<U8>(pc, B, P.px, P.py, v, pl);
 }
 
 // ComputeBilateralNCCNew (DPE.cu:557-690)
+template <bool U8>
 DEV float ncc_new(const PassConst& pc, const DevBufs& B, int px, int py, int v, const float4& pl) {
   const int W = pc.W, Hh = pc.H;
   const int center = px + py * W;
@@ -370,7 +411,7 @@ DEV float ncc_new(const PassConst& pc, const DevBufs& B, int px, int py, int v, 
       radius = B.radius[center];
       increment = MAXo(2, d2i(2.0 * radius / 5.0));
     }
-    const float tc = patch_ncc_generic(pc, B, B.imgq[v], H, np.x, np.y, rc, radius, increment);
+    const float tc = patch_ncc_generic<U8>(pc, B, v, H, np.x, np.y, rc, radius, increment);
     if (k == 0) center_cost = tc;
     else { strong_cost += tc; strong_count++; }
   }

@@ -13,15 +13,17 @@
 namespace dpe {
 
 #define PIX2D_FULL()                                                   \
-  const int x = blockIdx.x * blockDim.x + threadIdx.x;                 \
-  const int y = blockIdx.y * blockDim.y + threadIdx.y;                 \
+  const int lb_ = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y, B.xcd_rows * gridDim.x); \
+  const int x = (lb_ % gridDim.x) * blockDim.x + threadIdx.x;          \
+  const int y = (lb_ / gridDim.x) * blockDim.y + threadIdx.y;          \
   if (x >= pc.W || y >= pc.H) return;                                  \
   const int center = x + y * pc.W;
 
 // half-sweep pixel of colour `colour` (0 = black: (x+y) even, 1 = red), DPE.cu:1864-1938
 #define PIX2D_HALF()                                                   \
-  const int y = blockIdx.y * blockDim.y + threadIdx.y;                 \
-  const int x = 2 * (blockIdx.x * blockDim.x + threadIdx.x) + ((y + colour) & 1); \
+  const int lb_ = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y, B.xcd_rows * gridDim.x); \
+  const int y = (lb_ / gridDim.x) * blockDim.y + threadIdx.y;          \
+  const int x = 2 * ((lb_ % gridDim.x) * blockDim.x + threadIdx.x) + ((y + colour) & 1); \
   if (x >= pc.W || y >= pc.H || y >= pc.half_rows) return;             \
   const int center = x + y * pc.W;
 
@@ -75,30 +77,6 @@ __global__ void k_gen_edge_inform(const PassConst* __restrict__ pcp, DevBufs B) 
       }
     }
   }
-}
-
-// ------------------------------------------------------------------------------ FindNearestStrongPoint
-__global__ void k_find_nearest_strong(const PassConst* __restrict__ pcp, DevBufs B) {   // DPE.cu:2855-2889
-  const PassConst& pc = *pcp;
-  PIX2D_FULL();
-  const int W = pc.W, H = pc.H;
-  short2 res = make_short2(-1, -1);
-  if (B.weak[center] == DPE_WEAK) {
-    bool found = false;
-    for (int r = 0; r <= 100 && !found; ++r)
-      for (int dx = -r; dx <= r && !found; ++dx) {
-        const int nx = x + dx;
-        if (nx < 0 || nx >= W) continue;
-        const bool edge_col = (dx == -r || dx == r);
-        // ring order: every y for the two edge columns, else only the top and bottom cells
-        for (int dy = -r; dy <= r; dy += (edge_col ? 1 : (r > 0 ? 2 * r : 1))) {
-          const int ny = y + dy;
-          if (ny < 0 || ny >= H) continue;
-          if (B.weak[nx + ny * W] == DPE_STRONG) { res = make_short2((short)nx, (short)ny); found = true; break; }
-        }
-      }
-  }
-  B.nearest[center] = res;
 }
 
 // ------------------------------------------------------------------------------ GenNeighbours
@@ -364,6 +342,7 @@ __global__ void k_neighbour_update(const PassConst* __restrict__ pcp, DevBufs B)
 }
 
 // ------------------------------------------------------------------------------ RandomInitialization
+template <bool U8>
 __global__ void __launch_bounds__(256) k_random_init(const PassConst* __restrict__ pcp, DevBufs B) {   // DPE.cu:1035-1063
   const PassConst& pc = *pcp;
   PIX2D_FULL();
@@ -382,7 +361,7 @@ __global__ void __launch_bounds__(256) k_random_init(const PassConst* __restrict
     float sorted[DPE_MAX_IMAGES];
     int cost_count = 0, num_valid = 0;
     for (int i = 1; i < N; ++i) {
-      const float c = ncc_old(P, fast, pc, B, i, ph);
+      const float c = ncc_old<U8>(P, fast, pc, B, i, ph);
       // insertion into the sorted prefix == sort_small of the full vector afterwards
       int j = cost_count;
       for (; j >= 1 && c < sorted[j - 1]; j--) sorted[j] = sorted[j - 1];
@@ -398,7 +377,7 @@ __global__ void __launch_bounds__(256) k_random_init(const PassConst* __restrict
       for (int i = 0; i < top_k; ++i) s += sorted[i];
       const float thr = sorted[top_k - 1];
       // second pass recomputes the (deterministic) per-view costs instead of keeping a copy
-      for (int i = 1; i < N; ++i) if (ncc_old(P, fast, pc, B, i, ph) <= thr) setBit(sel, i - 1);
+      for (int i = 1; i < N; ++i) if (ncc_old<U8>(P, fast, pc, B, i, ph) <= thr) setBit(sel, i - 1);
       cost = s / top_k;
     }
     B.sel[center] = sel;
@@ -413,7 +392,7 @@ __global__ void __launch_bounds__(256) k_random_init(const PassConst* __restrict
     int cc = 0; float cost = 0.0f;
     for (int i = 1; i < N; ++i) {
       if (isSet(sel, i - 1)) {
-        const float c = ncc_old(P, fast, pc, B, i, ph);
+        const float c = ncc_old<U8>(P, fast, pc, B, i, ph);
         if (c < 2.0f) { cc++; cost += c; }
         else unSetBit(sel, i - 1);
       }
@@ -472,6 +451,7 @@ DEV void view_selection(const LdsView& L, int iter, PriorF prior, Rng& rs, uint3
 // ------------------------------------------------------------------------------ strong sweep
 // CheckerboardPropagationStrong (DPE.cu:1214-1666) + PlaneHypothesisRefinementStrong (:1065-1118).
 // Neighbour reads come from the snapshot taken before the half-sweep (same-colour semantics).
+template <bool U8>
 __global__ void __launch_bounds__(128) k_strong_sweep(const PassConst* __restrict__ pcp, DevBufs B, int iter, int colour) {
   extern __shared__ float lds[];
   const PassConst& pc = *pcp;
@@ -496,7 +476,7 @@ __global__ void __launch_bounds__(128) k_strong_sweep(const PassConst* __restric
   for (int d = 0; d < 8; ++d) positions[d] = 0;
 
   auto costvec = [&](const float4& pl, int slot) {
-    for (int v = 1; v < N; ++v) L.cost(slot, v - 1) = ncc_old(P, fast, pc, B, v, pl);
+    for (int v = 1; v < N; ++v) L.cost(slot, v - 1) = ncc_old<U8>(P, fast, pc, B, v, pl);
   };
 
   if (pc.P.use_edge) {
@@ -663,7 +643,7 @@ __global__ void __launch_bounds__(128) k_strong_sweep(const PassConst* __restric
 
   const float4 cur = planes[center];
   float cost_now = 0.0f;
-  for (int i = 0; i < nv; ++i) { const int w = L.vw(i); if (w > 0) cost_now += w * ncc_old(P, fast, pc, B, i + 1, cur); }
+  for (int i = 0; i < nv; ++i) { const int w = L.vw(i); if (w > 0) cost_now += w * ncc_old<U8>(P, fast, pc, B, i + 1, cur); }
   cost_now /= wnorm;
   const float cost_written = cost_now;
   B.costs[center] = cost_now;
@@ -698,7 +678,7 @@ __global__ void __launch_bounds__(128) k_strong_sweep(const PassConst* __restric
       else { dh = depth_perturbed; tp = pl0; }
       tp.w = dist2origin(c0, x, y, dh, tp);
       float tc = 0.0f;
-      for (int j = 0; j < nv; ++j) { const int w = L.vw(j); if (w > 0) tc += w * ncc_old(P, fast, pc, B, j + 1, tp); }
+      for (int j = 0; j < nv; ++j) { const int w = L.vw(j); if (w > 0) tc += w * ncc_old<U8>(P, fast, pc, B, j + 1, tp); }
       tc /= wnorm;
       const float db = depth_from_plane(c0, tp, x, y);
       if (db >= dmin && db <= dmax && tc < cost_now) { depth_now = db; pnow = tp; cost_now = tc; }
@@ -865,6 +845,7 @@ __global__ void __launch_bounds__(256) k_ransac_fit(const PassConst* __restrict_
 
 // ------------------------------------------------------------------------------ weak sweep
 // CheckerboardPropagationWeak (DPE.cu:1668-1862) + PlaneHypothesisRefinementWeak (:1120-1212).
+template <bool U8>
 __global__ void __launch_bounds__(128) k_weak_sweep(const PassConst* __restrict__ pcp, DevBufs B, int iter, int colour) {
   extern __shared__ float lds[];
   const PassConst& pc = *pcp;
@@ -890,7 +871,7 @@ __global__ void __launch_bounds__(128) k_weak_sweep(const PassConst* __restrict_
     positions[i] = np.x + np.y * W;
     flags |= 1u << i;
     const float4 pl = B.planes[positions[i]];
-    for (int v = 1; v < N; ++v) L.cost(i, v - 1) = ncc_new(pc, B, x, y, v, pl);
+    for (int v = 1; v < N; ++v) L.cost(i, v - 1) = ncc_new<U8>(pc, B, x, y, v, pl);
   }
   uint32_t nsv[8];
 #pragma unroll
@@ -942,7 +923,7 @@ __global__ void __launch_bounds__(128) k_weak_sweep(const PassConst* __restrict_
     for (int j = 0; j < nv; ++j) {
       const int w = L.vw(j);
       if (w > 0) {
-        const float c = ncc_new(pc, B, x, y, j + 1, tp);
+        const float c = ncc_new<U8>(pc, B, x, y, j + 1, tp);
         if (geom) tc += w * (c + gf * geom_cost(pc, B, x, y, j + 1, tp));
         else tc += w * c;
       }
@@ -1010,7 +991,7 @@ __global__ void __launch_bounds__(128) k_weak_sweep(const PassConst* __restrict_
     Patch36 P;
     if (fast) make_patch36(P, pc, B, x, y); else { P.px = x; P.py = y; }
     float c2 = 0.0f;
-    for (int i = 0; i < nv; ++i) { const int w = L.vw(i); if (w > 0) c2 += w * ncc_old(P, fast, pc, B, i + 1, fin); }
+    for (int i = 0; i < nv; ++i) { const int w = L.vw(i); if (w > 0) c2 += w * ncc_old<U8>(P, fast, pc, B, i + 1, fin); }
     B.costs[center] = c2 / wnorm;
   }
 }
@@ -1056,136 +1037,18 @@ __global__ void k_filter(const PassConst* __restrict__ pcp, DevBufs B, int colou
   B.planes[center].w = (n % 2 == 0) ? (filter[m - 1] + filter[m]) / 2 : filter[m];
 }
 
-// ------------------------------------------------------------------------------ DepthToWeak / LocalRefine
-struct CostBase { float cost_now, base_line, weight_normal; int valid; };
-
-DEV CostBase cost_and_baseline(const PassConst& pc, const DevBufs& B, const Patch36& P, bool fast, int x, int y,
-                               uint32_t sel, const uint8_t* vw, const float4& op, float od) {
-  CostBase r = {0.0f, 0.0f, 0.0f, 0};
-  const DpeCamera& c0 = pc.cams[0];
-  for (int si = 1; si < pc.N; ++si) {
-    const int vi = si - 1;
-    if (isSet(sel, vi)) {
-      float4 tp = op;
-      tp.w = dist2origin(c0, x, y, od, tp);
-      float tc = ncc_old(P, fast, pc, B, si, tp);
-      if (pc.P.geom_consistency) tc += pc.P.geom_factor * geom_cost(pc, B, x, y, si, tp);
-      r.cost_now += (tc * vw[vi]);
-      r.weight_normal += vw[vi];
-      const DpeCamera& cs = pc.cams[si];
-      const float d0 = c0.c[0] - cs.c[0], d1 = c0.c[1] - cs.c[1], d2 = c0.c[2] - cs.c[2];
-      const float tv = d0 * d0 + d1 * d1 + d2 * d2;
-      r.base_line += __builtin_sqrtf(tv);
-      r.valid++;
-    }
-  }
-  return r;
-}
-
-__global__ void __launch_bounds__(256) k_depth_to_weak(const PassConst* __restrict__ pcp, DevBufs B) {   // DPE.cu:2593-2747
-  extern __shared__ float lds[];
-  const PassConst& pc = *pcp;
-  PIX2D_FULL();
-  const int W = pc.W, H = pc.H;
-  const int min_margin = 6;
-  if (x < min_margin || y < min_margin || x >= W - min_margin || y >= H - min_margin) { B.weak[center] = DPE_UNKNOWN; return; }
-  const DpeCamera& c0 = pc.cams[0];
-  const uint8_t* vw = B.vw + (size_t)DPE_MAX_IMAGES * center;
-  const float4 op = transform_normal_ref(c0, B.planes[center]);
-  const float od = op.w;
-  if (od == 0) { B.weak[center] = DPE_UNKNOWN; return; }
-  const uint32_t sel = B.sel[center];
-  const bool fast = pc.P.strong_radius == 5 && pc.P.strong_increment == 2;
-  Patch36 P;
-  if (fast) make_patch36(P, pc, B, x, y); else { P.px = x; P.py = y; }
-  CostBase cn = cost_and_baseline(pc, B, P, fast, x, y, sel, vw, op, od);
-  if (cn.valid == 0) { B.weak[center] = DPE_UNKNOWN; return; }
-  cn.cost_now /= cn.weight_normal;
-  cn.base_line /= cn.valid;
-  const float disp = c0.K[0] * cn.base_line / od;
-  const int bs = blockDim.x * blockDim.y, tid = threadIdx.y * blockDim.x + threadIdx.x;
-  float* pcs = lds;   // p_costs[61] as [61][bs]
-  const int radius = 30;
-  for (int pd = -radius; pd <= radius; ++pd) {
-    const float p_depth = c0.K[0] * cn.base_line / (disp + (float)pd);
-    float val;
-    if (p_depth < pc.P.depth_min || p_depth > pc.P.depth_max) val = 2.0f;
-    else {
-      float4 tp = op;
-      tp.w = dist2origin(c0, x, y, p_depth, tp);
-      float p_cost = 0.0f;
-      for (int si = 1; si < pc.N; ++si) {
-        const int vi = si - 1;
-        if (isSet(sel, vi)) {
-          float tcst = 0.0f;
-          tcst += ncc_old(P, fast, pc, B, si, tp);
-          if (pc.P.geom_consistency) tcst += pc.P.geom_factor * geom_cost(pc, B, x, y, si, tp);
-          p_cost += (tcst * vw[vi]);
-        }
-      }
-      p_cost /= cn.weight_normal;
-      val = MINo(2.0f, p_cost);
-    }
-    pcs[(pd + radius) * bs + tid] = val;
-  }
-  auto pcv = [&](int i) { return pcs[i * bs + tid]; };
-  int peak_count = 0, min_peak = 0;
-  float min_cost = 2.0f;
-  uint64_t is_peak = 0;
-  for (int i = 2; i < 59; ++i) {
-    const float c = pcv(i);
-    if (pcv(i - 1) > c && pcv(i + 1) > c) {
-      is_peak |= 1ull << i; peak_count++;
-      if (c < min_cost) { min_peak = i; min_cost = c; }
-    }
-  }
-  if (abs(min_peak - radius) > pc.P.weak_peak_radius || pcv(min_peak) > 0.5f) { B.weak[center] = DPE_WEAK; return; }
-  if (peak_count == 1) { B.weak[center] = pcv(min_peak) <= 0.15f ? DPE_STRONG : DPE_WEAK; return; }
-  float var = 0.0f;
-  for (int i = 2; i < 59; ++i) if (((is_peak >> i) & 1ull) && i != min_peak) { const float d = pcv(i) - min_cost; var += d * d; }
-  var = __builtin_sqrtf(var);
-  var /= (peak_count - 1);
-  B.weak[center] = var > 0.2f ? DPE_STRONG : DPE_WEAK;
-}
-
-__global__ void __launch_bounds__(256) k_local_refine(const PassConst* __restrict__ pcp, DevBufs B) {   // DPE.cu:2749-2835
-  const PassConst& pc = *pcp;
-  PIX2D_FULL();
-  const DpeCamera& c0 = pc.cams[0];
-  const uint8_t* vw = B.vw + (size_t)DPE_MAX_IMAGES * center;
-  const float4 op = transform_normal_ref(c0, B.planes[center]);
-  const float od = op.w;
-  if (od == 0) return;
-  const uint32_t sel = B.sel[center];
-  const bool fast = pc.P.strong_radius == 5 && pc.P.strong_increment == 2;
-  Patch36 P;
-  if (fast) make_patch36(P, pc, B, x, y); else { P.px = x; P.py = y; }
-  CostBase cn = cost_and_baseline(pc, B, P, fast, x, y, sel, vw, op, od);
-  if (cn.weight_normal == 0 || cn.valid == 0) return;
-  cn.cost_now /= cn.weight_normal;
-  cn.base_line /= cn.valid;
-  const float disp = c0.K[0] * cn.base_line / od;
-  float min_cost = 2.0f, best_depth = od;
-  for (int pd = -5; pd <= 5; ++pd) {
-    const float p_depth = c0.K[0] * cn.base_line / (disp + (float)pd);
-    if (p_depth < pc.P.depth_min || p_depth > pc.P.depth_max) continue;
-    float4 tp = op;
-    tp.w = dist2origin(c0, x, y, p_depth, tp);
-    float tc = 0.0f;
-    for (int si = 1; si < pc.N; ++si) {
-      const int vi = si - 1;
-      if (isSet(sel, vi)) {
-        tc += (ncc_old(P, fast, pc, B, si, tp) * vw[vi]);
-        if (pc.P.geom_consistency) tc += (pc.P.geom_factor * geom_cost(pc, B, x, y, si, tp) * vw[vi]);
-      }
-    }
-    tc /= cn.weight_normal;
-    if (tc < min_cost) { min_cost = tc; best_depth = p_depth; }
-  }
-  if ((double)(cn.cost_now - min_cost) > 0.1) B.planes[center].w = best_depth;
-}
-
 // ------------------------------------------------------------------------------ staging kernels
+// u8 padded quad-texel image (images that are 8-bit grey levels)
+__global__ void k_build_quad8(const float* __restrict__ img, uint32_t* __restrict__ q, int W, int H) {
+  const int X = blockIdx.x * blockDim.x + threadIdx.x;
+  const int Y = blockIdx.y * blockDim.y + threadIdx.y;
+  if (X > W + 1 || Y > H + 1) return;
+  auto cl = [](int v, int n) { return v < 0 ? 0 : (v > n - 1 ? n - 1 : v); };
+  const int x0 = cl(X - 1, W), x1 = cl(X, W), y0 = cl(Y - 1, H), y1 = cl(Y, H);
+  const uint32_t a = (uint32_t)img[y0 * W + x0], b = (uint32_t)img[y0 * W + x1];
+  const uint32_t c = (uint32_t)img[y1 * W + x0], d = (uint32_t)img[y1 * W + x1];
+  q[Y * (W + 2) + X] = a | (b << 8) | (c << 16) | (d << 24);
+}
 // padded quad-texel image (see pass_common.h)
 __global__ void k_build_quad(const float* __restrict__ img, float4* __restrict__ q, int W, int H) {
   const int X = blockIdx.x * blockDim.x + threadIdx.x;

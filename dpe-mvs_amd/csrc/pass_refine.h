@@ -1,0 +1,347 @@
+// pass_refine.h — wave-cooperative kernels: DepthToWeak, LocalRefine, FindNearestStrongPoint.
+//
+// DepthToWeak (DPE.cu:2593-2747) evaluates 61 disparity hypotheses per pixel and LocalRefine
+// (:2749-2835) 11; the reference loops over them in one thread.  Here one wave owns one pixel
+// (DepthToWeak: lane = hypothesis) or five pixels (LocalRefine: 12 lanes per pixel = 11
+// hypotheses + the current depth), so the per-pixel state (view mask, weights, baseline) is
+// wave-uniform and the 36-tap reference patch is built once per pixel, cooperatively, in LDS.
+// Reductions whose floating-point order matters (the peak variance, the arg-min) are done
+// serially by one lane in the reference's index order, so results stay bit-exact.
+#pragma once
+#include "pass_common.h"
+
+namespace dpe {
+
+// wave-local LDS hand-off (all lanes of one wave; no workgroup barrier)
+DEV void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// 36-tap reference patch in LDS: w[36], wr[36], rp[36] (grey level) for pixel (px, py).
+// Lane `t` of the group computes taps t, t+stride, ...
+DEV void patch_lds_build(float* pw, const PassConst& pc, const DevBufs& B, int px, int py, int t, int stride) {
+  const float rc = ref_texel(B.ref, pc.W, pc.H, px, py);
+  for (int k = t; k < 36; k += stride) {
+    const int i = -5 + 2 * (k / 6), j = -5 + 2 * (k % 6);
+    const float rp = ref_texel(B.ref, pc.W, pc.H, px + i, py + j);
+    const float w = bilateral_weight(i, j, rp, rc, pc.P.sigma_spatial, pc.P.sigma_color);
+    pw[k] = w;
+    pw[36 + k] = w * rp;
+    pw[72 + k] = rp;
+  }
+}
+// reference sums in the row order of make_patch36 (bit-identical)
+DEV void patch_lds_sums(const float* pw, float& s_ref, float& s_rr, float& s_w) {
+  float a_ref = 0, a_rr = 0, a_w = 0;
+#pragma unroll
+  for (int a = 0; a < 6; ++a) {
+    float r_ref = 0, r_rr = 0, r_w = 0;
+#pragma unroll
+    for (int b = 0; b < 6; ++b) {
+      const float w = pw[a * 6 + b], wr = pw[36 + a * 6 + b], rp = pw[72 + a * 6 + b];
+      r_ref = r_ref + wr;
+      r_rr = __builtin_fmaf(wr, rp, r_rr);
+      r_w = r_w + w;
+    }
+    a_ref += r_ref; a_rr += r_rr; a_w += r_w;
+  }
+  s_ref = a_ref; s_rr = a_rr; s_w = a_w;
+}
+// Old NCC with the patch read from LDS (same arithmetic as ncc_old_patch36)
+template <bool U8>
+DEV float ncc_old_lds(const float* pw, float s_ref, float s_rr, float s_w, int px, int py, const PassConst& pc,
+                      const DevBufs& B, int v, const float4& pl) {
+  const Homog H = make_homography(pc, v, pl);
+  if (center_outside(pc, v, H, px, py)) { count_work(B, 1, 0); return 2.0f; }
+  count_work(B, 1, 36);
+  const int W = pc.W, Hh = pc.H;
+  float s_src = 0, s_ss = 0, s_rs = 0;
+#pragma unroll
+  for (int a = 0; a < 6; ++a) {
+    const float x = (float)(px - 5 + 2 * a);
+    const float bx = __builtin_fmaf(H.h[0], x, H.h[2]);
+    const float by = __builtin_fmaf(H.h[3], x, H.h[5]);
+    const float bz = __builtin_fmaf(H.h[6], x, H.h[8]);
+    float r_src = 0, r_ss = 0, r_rs = 0;
+#pragma unroll
+    for (int b = 0; b < 6; ++b) {
+      const float y = (float)(py - 5 + 2 * b);
+      const float qx = __builtin_fmaf(H.h[1], y, bx);
+      const float qy = __builtin_fmaf(H.h[4], y, by);
+      const float qz = __builtin_fmaf(H.h[7], y, bz);
+      const float iz = 1.0f / qz;
+      const float sp = sample_src<U8>(B, v, W, Hh, qx * iz, qy * iz);
+      const float w = pw[a * 6 + b], wr = pw[36 + a * 6 + b];
+      r_src = __builtin_fmaf(w, sp, r_src);
+      const float ws = w * sp;
+      r_ss = __builtin_fmaf(ws, sp, r_ss);
+      r_rs = __builtin_fmaf(wr, sp, r_rs);
+    }
+    s_src += r_src; s_ss += r_ss; s_rs += r_rs;
+  }
+  return ncc_finalize(s_ref, s_rr, s_w, s_src, s_ss, s_rs);
+}
+
+template <bool U8>
+DEV float ncc_old_any(bool fast, const float* pw, float s_ref, float s_rr, float s_w, int px, int py,
+                      const PassConst& pc, const DevBufs& B, int v, const float4& pl) {
+  if (fast) return ncc_old_lds<U8>(pw, s_ref, s_rr, s_w, px, py, pc, B, v, pl);
+  return ncc_old_generic<U8>(pc, B, px, py, v, pl);
+}
+
+// Baseline part of DPE.cu:2629-2648 (without the cost, which DepthToWeak never uses).
+DEV void baseline_and_weights(const PassConst& pc, uint32_t sel, const uint8_t* vw, float& base_line, float& weight_normal,
+                              int& valid) {
+  const DpeCamera& c0 = pc.cams[0];
+  base_line = 0.0f; weight_normal = 0.0f; valid = 0;
+  for (int si = 1; si < pc.N; ++si) {
+    const int vi = si - 1;
+    if (isSet(sel, vi)) {
+      weight_normal += vw[vi];
+      const DpeCamera& cs = pc.cams[si];
+      const float d0 = c0.c[0] - cs.c[0], d1 = c0.c[1] - cs.c[1], d2 = c0.c[2] - cs.c[2];
+      const float tv = d0 * d0 + d1 * d1 + d2 * d2;
+      base_line += __builtin_sqrtf(tv);
+      valid++;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------ DepthToWeak
+// grid: one wave per pixel, 4 waves per 256-thread workgroup.
+template <bool U8>
+__global__ void __launch_bounds__(256) k_depth_to_weak(const PassConst* __restrict__ pcp, DevBufs B) {   // DPE.cu:2593-2747
+  __shared__ float s_patch[4][108];
+  __shared__ float s_pc[4][64];
+  const PassConst& pc = *pcp;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int W = pc.W, H = pc.H;
+  const long pix = (long)xcd_remap(blockIdx.x, gridDim.x, B.xcd_rows * 16 * ((pc.W + 3) / 4)) * 4 + wave;
+  if (pix >= (long)W * H) return;                 // wave-uniform
+  const int x = (int)(pix % W), y = (int)(pix / W);
+  const int center = (int)pix;
+  const int min_margin = 6;
+  if (x < min_margin || y < min_margin || x >= W - min_margin || y >= H - min_margin) {
+    if (lane == 0) B.weak[center] = DPE_UNKNOWN;
+    return;
+  }
+  const DpeCamera& c0 = pc.cams[0];
+  const float4 op = transform_normal_ref(c0, B.planes[center]);
+  const float od = op.w;
+  if (od == 0) { if (lane == 0) B.weak[center] = DPE_UNKNOWN; return; }
+  const uint32_t sel = B.sel[center];
+  const uint8_t* vw = B.vw + (size_t)DPE_MAX_IMAGES * center;
+  float base_line, weight_normal; int valid;
+  baseline_and_weights(pc, sel, vw, base_line, weight_normal, valid);
+  if (valid == 0) { if (lane == 0) B.weak[center] = DPE_UNKNOWN; return; }
+  base_line /= valid;
+  const float disp = c0.K[0] * base_line / od;
+  const bool fast = pc.P.strong_radius == 5 && pc.P.strong_increment == 2;
+  float* pw = s_patch[wave];
+  if (fast) patch_lds_build(pw, pc, B, x, y, lane, 64);
+  wave_sync();
+  float s_ref = 0, s_rr = 0, s_w = 0;
+  if (fast) patch_lds_sums(pw, s_ref, s_rr, s_w);
+  const int radius = 30;
+  if (lane < 2 * radius + 1) {
+    const int pd = lane - radius;
+    const float p_depth = c0.K[0] * base_line / (disp + (float)pd);
+    float val;
+    if (p_depth < pc.P.depth_min || p_depth > pc.P.depth_max) val = 2.0f;
+    else {
+      float4 tp = op;
+      tp.w = dist2origin(c0, x, y, p_depth, tp);
+      float p_cost = 0.0f;
+      for (int si = 1; si < pc.N; ++si) {
+        const int vi = si - 1;
+        if (isSet(sel, vi)) {
+          float tcst = 0.0f;
+          tcst += ncc_old_any<U8>(fast, pw, s_ref, s_rr, s_w, x, y, pc, B, si, tp);
+          if (pc.P.geom_consistency) tcst += pc.P.geom_factor * geom_cost(pc, B, x, y, si, tp);
+          p_cost += (tcst * vw[vi]);
+        }
+      }
+      p_cost /= weight_normal;
+      val = MINo(2.0f, p_cost);
+    }
+    s_pc[wave][lane] = val;
+  }
+  wave_sync();
+  if (lane != 0) return;
+  const float* pcs = s_pc[wave];
+  int peak_count = 0, min_peak = 0;
+  float min_cost = 2.0f;
+  uint64_t is_peak = 0;
+  for (int i = 2; i < 59; ++i) {
+    const float c = pcs[i];
+    if (pcs[i - 1] > c && pcs[i + 1] > c) {
+      is_peak |= 1ull << i; peak_count++;
+      if (c < min_cost) { min_peak = i; min_cost = c; }
+    }
+  }
+  uint8_t cls;
+  if (abs(min_peak - radius) > pc.P.weak_peak_radius || pcs[min_peak] > 0.5f) cls = DPE_WEAK;
+  else if (peak_count == 1) cls = pcs[min_peak] <= 0.15f ? DPE_STRONG : DPE_WEAK;
+  else {
+    float var = 0.0f;
+    for (int i = 2; i < 59; ++i) if (((is_peak >> i) & 1ull) && i != min_peak) { const float d = pcs[i] - min_cost; var += d * d; }
+    var = __builtin_sqrtf(var);
+    var /= (peak_count - 1);
+    cls = var > 0.2f ? DPE_STRONG : DPE_WEAK;
+  }
+  B.weak[center] = cls;
+}
+
+// ------------------------------------------------------------------------------ LocalRefine
+// grid: five pixels per wave (12 lanes each: lanes 0..10 = hypotheses -5..5, lane 11 = cost at
+// the current depth), 4 waves per 256-thread workgroup.
+template <bool U8>
+__global__ void __launch_bounds__(256) k_local_refine(const PassConst* __restrict__ pcp, DevBufs B) {   // DPE.cu:2749-2835
+  __shared__ float s_patch[4][5][108];
+  __shared__ float s_tc[4][5][12];
+  const PassConst& pc = *pcp;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int grp = lane / 12, g = lane % 12;
+  const int W = pc.W;
+  const long L = (long)W * pc.H;
+  const long pix = ((long)xcd_remap(blockIdx.x, gridDim.x, B.xcd_rows * 16 * ((pc.W + 19) / 20)) * 4 + wave) * 5 + grp;
+  const bool active = grp < 5 && pix < L;
+  const int x = active ? (int)(pix % W) : 0, y = active ? (int)(pix / W) : 0;
+  const int center = (int)(active ? pix : 0);
+  const DpeCamera& c0 = pc.cams[0];
+  bool go = active;
+  float4 op = make_float4(0, 0, 0, 0);
+  float od = 0, base_line = 0, weight_normal = 0, disp = 0;
+  int valid = 0;
+  uint32_t sel = 0;
+  const uint8_t* vw = B.vw + (size_t)DPE_MAX_IMAGES * center;
+  if (go) {
+    op = transform_normal_ref(c0, B.planes[center]);
+    od = op.w;
+    if (od == 0) go = false;
+  }
+  if (go) {
+    sel = B.sel[center];
+    baseline_and_weights(pc, sel, vw, base_line, weight_normal, valid);
+    if (weight_normal == 0 || valid == 0) go = false;
+  }
+  const bool fast = pc.P.strong_radius == 5 && pc.P.strong_increment == 2;
+  float* pw = s_patch[wave][grp < 5 ? grp : 0];
+  if (go && fast) patch_lds_build(pw, pc, B, x, y, g, 12);
+  wave_sync();
+  float s_ref = 0, s_rr = 0, s_w = 0;
+  if (go && fast) patch_lds_sums(pw, s_ref, s_rr, s_w);
+  const uint32_t vmask = (pc.N - 1) >= 32 ? 0xFFFFFFFFu : ((1u << (pc.N - 1)) - 1u);
+  if (go) {
+    base_line /= valid;
+    disp = c0.K[0] * base_line / od;
+    float tc = 0.0f;
+    if (g < 11) {
+      const int pd = g - 5;
+      const float p_depth = c0.K[0] * base_line / (disp + (float)pd);
+      if (p_depth < pc.P.depth_min || p_depth > pc.P.depth_max) tc = __builtin_nanf("");   // skipped hypothesis
+      else {
+        float4 tp = op;
+        tp.w = dist2origin(c0, x, y, p_depth, tp);
+        // the pixel's own selected views in ascending order (same summation order as the
+        // reference's si loop; lanes of different pixels do not serialise on each other's views)
+        for (uint32_t bits = sel & vmask; bits; bits &= bits - 1) {
+          const int vi = __builtin_ctz(bits), si = vi + 1;
+          tc += (ncc_old_any<U8>(fast, pw, s_ref, s_rr, s_w, x, y, pc, B, si, tp) * vw[vi]);
+          if (pc.P.geom_consistency) tc += (pc.P.geom_factor * geom_cost(pc, B, x, y, si, tp) * vw[vi]);
+        }
+        tc /= weight_normal;
+      }
+    } else {
+      // cost at the current depth (DPE.cu:2776-2795, its own accumulation formula)
+      float4 tp = op;
+      tp.w = dist2origin(c0, x, y, od, tp);
+      for (uint32_t bits = sel & vmask; bits; bits &= bits - 1) {
+        const int vi = __builtin_ctz(bits), si = vi + 1;
+        float t = ncc_old_any<U8>(fast, pw, s_ref, s_rr, s_w, x, y, pc, B, si, tp);
+        if (pc.P.geom_consistency) t += pc.P.geom_factor * geom_cost(pc, B, x, y, si, tp);
+        tc += (t * vw[vi]);
+      }
+      tc /= weight_normal;
+    }
+    s_tc[wave][grp][g] = tc;
+  }
+  wave_sync();
+  if (!go || g != 0) return;
+  const float* t = s_tc[wave][grp];
+  float min_cost = 2.0f, best_depth = od;
+  for (int pd = -5; pd <= 5; ++pd) {
+    const float p_depth = c0.K[0] * base_line / (disp + (float)pd);
+    if (p_depth < pc.P.depth_min || p_depth > pc.P.depth_max) continue;
+    const float tcv = t[pd + 5];
+    if (tcv < min_cost) { min_cost = tcv; best_depth = p_depth; }
+  }
+  if ((double)(t[11] - min_cost) > 0.1) B.planes[center].w = best_depth;
+}
+
+// ------------------------------------------------------------------------------ FindNearestStrongPoint
+// Ring search r = 0..100 (DPE.cu:2855-2889) in O(1) per ring with two tables:
+//   next_right[y*W + x] = smallest x' >= x with weak(x', y) == STRONG (W if none)
+//   next_down [y*W + x] = smallest y' >= y with weak(x, y') == STRONG (H if none)
+// Ring order of the reference: column dx = -r (all dy ascending), then columns -r < dx < r
+// (dy = -r before dy = +r), then column dx = +r -> first hit = same pixel.
+__global__ void k_strong_tables_rows(const PassConst* __restrict__ pcp, DevBufs B, int* __restrict__ next_right) {
+  const PassConst& pc = *pcp;
+  const int y = blockIdx.x * blockDim.x + threadIdx.x;
+  if (y >= pc.H) return;
+  int nxt = pc.W;
+  for (int x = pc.W - 1; x >= 0; --x) {
+    if (B.weak[y * pc.W + x] == DPE_STRONG) nxt = x;
+    next_right[y * pc.W + x] = nxt;
+  }
+}
+__global__ void k_strong_tables_cols(const PassConst* __restrict__ pcp, DevBufs B, int* __restrict__ next_down) {
+  const PassConst& pc = *pcp;
+  const int x = blockIdx.x * blockDim.x + threadIdx.x;
+  if (x >= pc.W) return;
+  int nxt = pc.H;
+  for (int y = pc.H - 1; y >= 0; --y) {
+    if (B.weak[y * pc.W + x] == DPE_STRONG) nxt = y;
+    next_down[y * pc.W + x] = nxt;
+  }
+}
+__global__ void k_find_nearest_strong(const PassConst* __restrict__ pcp, DevBufs B, const int* __restrict__ next_right,
+                                      const int* __restrict__ next_down) {
+  const PassConst& pc = *pcp;
+  const int x = blockIdx.x * blockDim.x + threadIdx.x;
+  const int y = blockIdx.y * blockDim.y + threadIdx.y;
+  if (x >= pc.W || y >= pc.H) return;
+  const int W = pc.W, H = pc.H;
+  const int center = x + y * W;
+  short2 res = make_short2(-1, -1);
+  if (B.weak[center] == DPE_WEAK) {
+    for (int r = 1; r <= 100; ++r) {   // r = 0 is the pixel itself, which is WEAK
+      const int y0 = MAXo(y - r, 0), y1 = MINo(y + r, H - 1);
+      // column dx = -r
+      const int xl = x - r;
+      if (xl >= 0) {
+        const int yy = next_down[y0 * W + xl];
+        if (yy <= y1) { res = make_short2((short)xl, (short)yy); break; }
+      }
+      // columns -r < dx < r on rows y - r and y + r
+      const int xa = MAXo(x - r + 1, 0), xb = MINo(x + r - 1, W - 1);
+      int best = W, besty = 0;
+      if (xa <= xb) {
+        if (y - r >= 0) { const int xx = next_right[(y - r) * W + xa]; if (xx <= xb) { best = xx; besty = y - r; } }
+        if (y + r < H) { const int xx = next_right[(y + r) * W + xa]; if (xx <= xb && xx < best) { best = xx; besty = y + r; } }
+      }
+      if (best < W) { res = make_short2((short)best, (short)besty); break; }
+      // column dx = +r
+      const int xr = x + r;
+      if (xr < W) {
+        const int yy = next_down[y0 * W + xr];
+        if (yy <= y1) { res = make_short2((short)xr, (short)yy); break; }
+      }
+    }
+  }
+  B.nearest[center] = res;
+}
+
+}  // namespace dpe

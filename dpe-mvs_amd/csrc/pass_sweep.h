@@ -1,0 +1,427 @@
+// pass_sweep.h — cooperative red/black sweeps (CheckerboardPropagationStrong/Weak, DPE.cu:1214-1862).
+//
+// The reference runs one thread per pixel with cost_array[8][32] in local memory (DPE.cu:1236, 1690).
+// Here a wave owns P pixels and gives each pixel C lanes:
+//   strong sweep, edge mode      P = 4,  C = 16 (8 adaptive + 8 fixed 11-step candidates)
+//   strong sweep, ACMH mode      P = 8,  C = 8  (near/far candidates)
+//   weak sweep                   P = 8,  C = 8  (the 8 deformable neighbours)
+// Candidate scans and the candidate x view NCC cost vectors run in parallel lanes; cost vectors
+// live in LDS ([pixel][candidate][view], a few KB per wave, so occupancy is register-limited);
+// the reference patch (weights, weight*grey) is built once per pixel in LDS.  Every step whose
+// floating-point order or RNG order matters (CDF, the 15 view samples, cost sums over views,
+// hypothesis acceptance) runs on the pixel's first lane in the reference's order, so results are
+// bit-identical to the serial restatement.  Pixels come from per-colour compacted lists.
+#pragma once
+#include "pass_common.h"
+#include "pass_refine.h"
+
+namespace dpe {
+
+// ------------------------------------------------------------------------------ pixel lists
+// list[k] (k = colour*2 + weak?1:0): pixels of that colour and class inside the red/black grid,
+// in row-major order.  One wave per row; ballot-based compaction keeps the order deterministic.
+__global__ void k_list_count(const PassConst* __restrict__ pcp, DevBufs B, int* __restrict__ row_counts) {
+  const PassConst& pc = *pcp;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int y = blockIdx.x * 4 + wave;
+  if (y >= pc.half_rows) return;
+  int cnt[4] = {0, 0, 0, 0};
+  for (int x0 = 0; x0 < pc.W; x0 += 64) {
+    const int x = x0 + lane;
+    int k = -1;
+    if (x < pc.W) k = (((x + y) & 1) << 1) | (B.weak[y * pc.W + x] == DPE_WEAK ? 1 : 0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) cnt[j] += __popcll(__ballot(k == j));
+  }
+  if (lane == 0)
+    for (int j = 0; j < 4; ++j) row_counts[j * pc.half_rows + y] = cnt[j];
+}
+// exclusive scan of the row counts of each list (one workgroup, serial over rows per list)
+__global__ void k_list_scan(const PassConst* __restrict__ pcp, int* __restrict__ row_counts, int* __restrict__ totals) {
+  const PassConst& pc = *pcp;
+  const int j = threadIdx.x;
+  if (j >= 4) return;
+  int acc = 0;
+  for (int y = 0; y < pc.half_rows; ++y) {
+    const int c = row_counts[j * pc.half_rows + y];
+    row_counts[j * pc.half_rows + y] = acc;
+    acc += c;
+  }
+  totals[j] = acc;
+}
+__global__ void k_list_fill(const PassConst* __restrict__ pcp, DevBufs B, const int* __restrict__ row_offsets,
+                            int* __restrict__ lists, long list_stride) {
+  const PassConst& pc = *pcp;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int y = blockIdx.x * 4 + wave;
+  if (y >= pc.half_rows) return;
+  int off[4];
+  for (int j = 0; j < 4; ++j) off[j] = row_offsets[j * pc.half_rows + y];
+  const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (int x0 = 0; x0 < pc.W; x0 += 64) {
+    const int x = x0 + lane;
+    int k = -1;
+    if (x < pc.W) k = (((x + y) & 1) << 1) | (B.weak[y * pc.W + x] == DPE_WEAK ? 1 : 0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const unsigned long long m = __ballot(k == j);
+      if (k == j) lists[j * list_stride + off[j] + __popcll(m & below)] = y * pc.W + x;
+      off[j] += __popcll(m);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------ view selection
+// sampling probability of view i before the prior (DPE.cu:1568-1589), costs by candidate j.
+template <class CostF>
+DEV float view_prob_raw(CostF cost, int i, float cost_threshold) {
+  float count = 0; int count_false = 0; float tmpw = 0;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const float c = cost(j, i);
+    if (c < cost_threshold) { tmpw += d_expf(c * c / (-0.18f)); count++; }
+    if (c > 1.2f) count_false++;
+  }
+  float sp = 0.0f;
+  if (count > 2 && count_false < 3) sp = tmpw / count;
+  else if (count_false < 3) sp = d_expf(cost_threshold * cost_threshold / (-0.32f));
+  return sp;
+}
+
+// Serial part of the joint view selection on one lane (DPE.cu:1592-1615): CDF over `sp`, 15 samples.
+DEV void view_sample(const float* sp, int nv, Rng& rs, uint8_t* vw, uint32_t& tsv, float& wnorm) {
+  for (int i = 0; i < DPE_MAX_IMAGES; ++i) vw[i] = 0;
+  float psum = 0.0f;
+  for (int i = 0; i < nv; ++i) psum += sp[i];
+  const float inv = 1.0f / psum;
+  float cdf[DPE_MAX_IMAGES];
+  float cum = 0.0f;
+  for (int i = 0; i < nv; ++i) { const float q = sp[i] * inv; cum += q; cdf[i] = cum; }
+  for (int s = 0; s < 15; ++s) {
+    const float rp = rng_uniform(rs) - 1.1920929e-07f;
+    for (int id = 0; id < nv; ++id)
+      if (cdf[id] > rp) { vw[id] += 1; break; }
+  }
+  uint32_t t = 0; float wn = 0;
+  for (int i = 0; i < nv; ++i) if (vw[i] > 0) { setBit(t, i); wn += vw[i]; }
+  tsv = t; wnorm = wn;
+}
+
+// ------------------------------------------------------------------------------ candidate scans
+// Edge-adaptive (kind 0) and fixed 11-step (kind 1) scans of direction d (DPE.cu:1250-1292, 1297-1322).
+DEV int edge_candidate(const PassConst& pc, const DevBufs& B, const float* __restrict__ costs, int x, int y, int center,
+                       int iter, int d, int kind, bool on_edge) {
+  const int W = pc.W, H = pc.H;
+  const int dx = kDir[d][0], dy = kDir[d][1];
+  const int s0 = MAXo(1, 5 - 2 * iter);
+  const int min_step_len = 2;
+  int step_num = 11, step_len = min_step_len;
+  if (kind == 0) {
+    const float max_edge_dist = MAXo(H, W) / 30.0f;
+    const short2 ep = B.edge_neigh[(size_t)center * 8 + d];
+    const double ex = (double)(ep.x - x), ey = (double)(ep.y - y);
+    float dist = (float)__builtin_sqrt(ex * ex + ey * ey);
+    if (d >= 4) dist = (float)((double)dist / 1.4142135623730951);
+    if (on_edge) dist = 11 * min_step_len;
+    else if (ep.x == -1 || ep.y == -1 || dist > max_edge_dist) {
+      dist = max_edge_dist;
+      if (d >= 4) dist = (float)((double)dist / 1.4142135623730951);
+    }
+    step_num = MINo(MAXo(11, f2i(1.0f * dist / min_step_len)), 22);
+    step_len = MAXo(f2i(1.0f * dist / step_num), min_step_len);
+    if (d < 4 && step_len % 2 == 1) step_len -= 1;
+  }
+  int fx = 0, fy = 0;
+  if (d > 4) { if (d % 2) fx = dx; else fy = dy; }
+  int mpos = -1; float mc = 3.40282347e+38f;
+  for (int step = 0; step < step_num; ++step) {
+    const int tx = x + s0 * dx + step * step_len * dx + fx, ty = y + s0 * dy + step * step_len * dy + fy;
+    if (!(tx >= 0 && ty >= 0 && tx < W && ty < H)) continue;
+    const int ptc = tx + ty * W;
+    const float c = costs[ptc];
+    if (mc > c) { mpos = ptc; mc = c; }
+  }
+  return mc < 3.40282347e+38f ? mpos : -1;
+}
+
+// ACMH near/far candidate of slot s (DPE.cu:1346-1544): 0 up_near, 1 up_far, 2 down_near,
+// 3 down_far, 4 left_near, 5 left_far, 6 right_near, 7 right_far.  -1 if the slot is absent.
+DEV int acmh_candidate(const PassConst& pc, const float* __restrict__ costs, int x, int y, int center, int s) {
+  const int W = pc.W, H = pc.H;
+  float costMin; int cmp;
+  switch (s) {
+    case 1: {
+      if (!(y > 2)) return -1;
+      const int up_far = center - 3 * W; costMin = costs[up_far]; cmp = up_far;
+      for (int i = 1; i < 11; ++i) if (y > 2 + 2 * i) { const int pt = up_far - 2 * i * W; if (costs[pt] < costMin) { costMin = costs[pt]; cmp = pt; } }
+      return cmp;
+    }
+    case 3: {
+      if (!(y < H - 3)) return -1;
+      const int down_far = center + 3 * W; costMin = costs[down_far]; cmp = down_far;
+      for (int i = 1; i < 11; ++i) if (y < H - 3 - 2 * i) { const int pt = down_far + 2 * i * W; if (costs[pt] < costMin) { costMin = costs[pt]; cmp = pt; } }
+      return cmp;
+    }
+    case 5: {
+      if (!(x > 2)) return -1;
+      const int left_far = center - 3; costMin = costs[left_far]; cmp = left_far;
+      for (int i = 1; i < 11; ++i) if (x > 2 + 2 * i) { const int pt = left_far - 2 * i; if (costs[pt] < costMin) { costMin = costs[pt]; cmp = pt; } }
+      return cmp;
+    }
+    case 7: {
+      if (!(x < W - 3)) return -1;
+      const int right_far = center + 3; costMin = costs[right_far]; cmp = right_far;
+      for (int i = 1; i < 11; ++i) if (x < W - 3 - 2 * i) { const int pt = right_far + 2 * i; if (costs[pt] < costMin) { costMin = costs[pt]; cmp = pt; } }
+      return cmp;
+    }
+    case 0: {
+      if (!(y > 0)) return -1;
+      const int up_near = center - W; costMin = costs[up_near]; cmp = up_near;
+      for (int i = 0; i < 3; ++i) {
+        if (y > 1 + i && x > i) { const int pt = up_near - (1 + i) * W - (1 + i); if (costs[pt] < costMin) { costMin = costs[pt]; cmp = pt; } }
+        if (y > 1 + i && x < W - 1 - i) { const int pt = up_near - (1 + i) * W + (1 + i); if (costs[pt] < costMin) { costMin = costs[pt]; cmp = pt; } }
+      }
+      return cmp;
+    }
+    case 2: {
+      if (!(y < H - 1)) return -1;
+      const int down_near = center + W; costMin = costs[down_near]; cmp = down_near;
+      for (int i = 0; i < 3; ++i) {
+        if (y < H - 2 - i && x > i) { const int pt = down_near + (1 + i) * W - (1 + i); if (costs[pt] < costMin) { costMin = costs[pt]; cmp = pt; } }
+        if (y < H - 2 - i && x < W - 1 - i) { const int pt = down_near + (1 + i) * W + (1 + i); if (costs[pt] < costMin) { costMin = costs[pt]; cmp = pt; } }
+      }
+      return cmp;
+    }
+    case 4: {
+      if (!(x > 0)) return -1;
+      const int left_near = center - 1; costMin = costs[left_near]; cmp = left_near;
+      for (int i = 0; i < 3; ++i) {
+        if (x > 1 + i && y > i) { const int pt = left_near - (1 + i) - (1 + i) * W; if (costs[pt] < costMin) { costMin = costs[pt]; cmp = pt; } }
+        if (x > 1 + i && y < H - 1 - i) { const int pt = left_near - (1 + i) + (1 + i) * W; if (costs[pt] < costMin) { costMin = costs[pt]; cmp = pt; } }
+      }
+      return cmp;
+    }
+    default: {   // 6
+      if (!(x < W - 1)) return -1;
+      const int right_near = center + 1; costMin = costs[right_near]; cmp = right_near;
+      for (int i = 0; i < 3; ++i) {
+        if (x < W - 2 - i && y > i) { const int pt = right_near + (1 + i) - (1 + i) * W; if (costs[pt] < costMin) { costMin = costs[pt]; cmp = pt; } }
+        if (x < W - 2 - i && y < H - 1 - i) { const int pt = right_near + (1 + i) + (1 + i) * W; if (costs[pt] < costMin) { costMin = costs[pt]; cmp = pt; } }
+      }
+      return cmp;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------ strong sweep
+// LDS floats per wave for P pixels, C lanes each, nv source views (multiple of 4: float4 alignment)
+__host__ __device__ inline int strong_lds_per_wave(int P, int C, int nv) {
+  return (P * (160 + C + C * nv + 8 * nv) + 3) & ~3;
+}
+
+template <bool U8, bool EDGE>
+__global__ void __launch_bounds__(256) k_strong_coop(const PassConst* __restrict__ pcp, DevBufs B, int iter,
+                                                     const int* __restrict__ list, const int* __restrict__ nlist_p) {
+  extern __shared__ float4 lds4[];
+  float* lds = (float*)lds4;
+  const int nlist = *nlist_p;
+  constexpr int C = EDGE ? 16 : 8;
+  constexpr int P = 64 / C;
+  const PassConst& pc = *pcp;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int ps = lane / C, c = lane % C;
+  const int W = pc.W, nv = pc.N - 1;
+  const DpeCamera& c0 = pc.cams[0];
+  const int gi = (xcd_remap(blockIdx.x, gridDim.x, B.xcd_rows * 16) * 4 + wave) * P + ps;
+  if ((xcd_remap(blockIdx.x, gridDim.x, B.xcd_rows * 16) * 4 + wave) * P >= nlist) return;   // wave-uniform tail
+  const bool active = gi < nlist;
+  const int center = active ? list[gi] : 0;
+  const int x = center % W, y = center / W;
+  // ---- LDS carve (per wave)
+  float* wl = lds + (size_t)wave * strong_lds_per_wave(P, C, nv);
+  float4* hyp = (float4*)wl + ps * 5;                    // [P][5] float4
+  float* pw = wl + P * 20 + ps * 108;                    // [P][108] patch
+  float* cost = wl + P * 128 + ps * C * nv;              // [P][C][nv]
+  float* sp = wl + P * (128 + C * nv) + ps * nv;         // [P][nv]
+  float* cur = sp + P * nv;                              // [P][nv]   current-plane NCC per selected view
+  float* ref = wl + P * (128 + C * nv + 2 * nv) + ps * 5 * nv;   // [P][5][nv] refinement NCCs
+  float* fc = wl + P * (128 + C * nv + 7 * nv) + ps * 8;  // [P][8]  final costs
+  uint8_t* vwl = (uint8_t*)(wl + P * (136 + C * nv + 7 * nv)) + ps * 32;   // [P][32] view weights
+  int* ib = (int*)(wl + P * (144 + C * nv + 7 * nv)) + ps * (C + 16 + nv);
+  int* posl = ib;                                        // [C] candidate positions (-1 = none)
+  int* fin = ib + C;                                     // [8] final slot of direction d (-1 = zero vector)
+  int* misc = ib + C + 8;                                // [8] 0: nsel, 1: tsv
+  int* sel_list = ib + C + 16;                           // [nv]
+
+  const float* __restrict__ costs_s = B.costs_snap;
+  const float4* __restrict__ planes_s = B.planes_snap;
+  const bool fast = pc.P.strong_radius == 5 && pc.P.strong_increment == 2;
+  bool on_edge = false;
+  // ---- phase 1: reference patch + candidate scans
+  if (active) {
+    if (fast) patch_lds_build(pw, pc, B, x, y, c, C);
+    int pos;
+    if constexpr (EDGE) {
+      on_edge = B.edge[center] != 0;
+      const int d = c & 7, kind = c >> 3;
+      pos = (kind == 1 && on_edge) ? -1 : edge_candidate(pc, B, costs_s, x, y, center, iter, d, kind, on_edge);
+    } else {
+      pos = acmh_candidate(pc, costs_s, x, y, center, c);
+    }
+    posl[c] = pos;
+  }
+  wave_sync();
+  float s_ref = 0, s_rr = 0, s_w = 0;
+  if (active && fast) patch_lds_sums(pw, s_ref, s_rr, s_w);
+  // ---- phase 2: candidate cost vectors (lane = candidate)
+  if (active) {
+    const int pos = posl[c];
+    if (pos >= 0) {
+      const float4 pl = planes_s[pos];
+      for (int v = 1; v <= nv; ++v) cost[c * nv + v - 1] = ncc_old_any<U8>(fast, pw, s_ref, s_rr, s_w, x, y, pc, B, v, pl);
+    }
+  }
+  wave_sync();
+  // ---- phase 3: arbitration of the two candidates of each direction (edge mode, DPE.cu:1323-1342)
+  if (active && c < 8) {
+    if constexpr (EDGE) {
+      const int d = c;
+      const bool hasA = posl[d] >= 0, hasB = !on_edge && posl[8 + d] >= 0;
+      int f = hasA ? d : -1;
+      if (hasB) {
+        const float good_threshold = 0.8f * d_expf((float)(iter * iter) / (-90.0f));
+        int g0 = 0, g1 = 0, b0 = 0, b1 = 0;
+        for (int j = 0; j < nv; ++j) {
+          // slot A as the reference sees it: its vector, or the zero-initialised row
+          const float v0 = hasA ? cost[d * nv + j] : ((d == 0 && j == 0) ? 2.0f : 0.0f);
+          if (v0 < good_threshold) g0++;
+          if (v0 > 1.2f) b0++;
+          const float v1 = cost[(8 + d) * nv + j];
+          if (v1 < good_threshold) g1++;
+          if (v1 > 1.2f) b1++;
+        }
+        if (!hasA || g1 > g0 || (g1 == g0 && b1 < b0)) f = 8 + d;
+      }
+      fin[d] = f;
+    } else {
+      fin[c] = posl[c] >= 0 ? c : -1;
+    }
+  }
+  wave_sync();
+  // cost of (direction j, view i) as the reference's cost_array holds it
+  auto cst = [&](int j, int i) -> float {
+    const int f = fin[j];
+    return f >= 0 ? cost[f * nv + i] : ((j == 0 && i == 0) ? 2.0f : 0.0f);
+  };
+  const float cost_threshold = (float)(0.8 * (double)d_expf((float)(iter * iter) / (-90.0f)));
+  // ---- phase 4: per-view sampling probabilities with the 4-neighbour priors (DPE.cu:1552-1590)
+  if (active) {
+    const long Lp = (long)W * pc.H;
+    uint32_t nsv[4];
+    bool nfl[4];
+    const long npos[4] = {(long)center - W, (long)center + W, (long)center - 1, (long)center + 1};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      nfl[i] = fin[2 * i] >= 0;
+      nsv[i] = (nfl[i] && npos[i] >= 0 && npos[i] < Lp) ? B.sel_snap[npos[i]] : 0u;
+    }
+    for (int v = c; v < nv; v += C) {
+      float prior = 0.0f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) if (nfl[i]) prior += isSet(nsv[i], v) == 1 ? 0.9f : 0.1f;
+      sp[v] = view_prob_raw(cst, v, cost_threshold) * prior;
+    }
+  }
+  wave_sync();
+  // ---- serial: samples + view weights (pixel lane 0)
+  Rng rs;
+  uint32_t tsv = 0; float wnorm = 0.0f;
+  if (active && c == 0) {
+    rng_init(rs, (uint32_t)center, pc.seed32, STREAM_ITER_BASE + 4 * iter + 0, pc.salt);
+    view_sample(sp, nv, rs, vwl, tsv, wnorm);
+    int ns = 0;
+    for (int i = 0; i < nv; ++i) if (vwl[i] > 0) sel_list[ns++] = i;
+    misc[0] = ns;
+    uint8_t* vwg = B.vw + (size_t)center * DPE_MAX_IMAGES;
+    for (int j = 0; j < DPE_MAX_IMAGES; ++j) vwg[j] = vwl[j];
+  }
+  wave_sync();
+  const int nsel = active ? misc[0] : 0;
+  // ---- phase 5: final costs of the 8 directions + current-plane NCCs over the selected views
+  if (active) {
+    if (c < 8) {
+      float wn = 0.0f;
+      for (int i = 0; i < nv; ++i) wn += vwl[i];   // == weight_norm (same order: sum of vw > 0)
+      float f = 0.0f;
+      for (int j = 0; j < nv; ++j) { const int w = vwl[j]; if (w > 0) f += w * cst(c, j); }
+      fc[c] = f / wn;
+    }
+    const float4 curp = planes_s[center];
+    for (int k = c; k < nsel; k += C) cur[k] = ncc_old_any<U8>(fast, pw, s_ref, s_rr, s_w, x, y, pc, B, sel_list[k] + 1, curp);
+  }
+  wave_sync();
+  // ---- serial: propagation acceptance + refinement hypotheses (DPE.cu:1617-1654, 1065-1095)
+  float cost_now = 0.0f, cost_written = 0.0f, depth_now = 0.0f;
+  float4 pnow = make_float4(0, 0, 0, 0);
+  if (active && c == 0) {
+    int mi = 0; float mcost = fc[0];
+    for (int i = 1; i < 8; ++i) if (fc[i] <= mcost) { mcost = fc[i]; mi = i; }
+    const float4 curp = planes_s[center];
+    for (int k = 0; k < nsel; ++k) cost_now += vwl[sel_list[k]] * cur[k];
+    cost_now /= wnorm;
+    cost_written = cost_now;
+    B.costs[center] = cost_now;
+    depth_now = depth_from_plane(c0, curp, x, y);
+    pnow = curp;
+    const int f = fin[mi];
+    if (f >= 0) {
+      const float4 cand = planes_s[posl[f]];
+      const float db = depth_from_plane(c0, cand, x, y);
+      if (db >= pc.P.depth_min && db <= pc.P.depth_max && fc[mi] < cost_now) {
+        depth_now = db; pnow = cand; cost_now = fc[mi]; B.sel[center] = tsv;
+      }
+    }
+    const float dmin = pc.P.depth_min, dmax = pc.P.depth_max;
+    const float depth_rand = rng_uniform(rs) * (dmax - dmin) + dmin;
+    const float4 prand = random_normal(c0, x, y, rs, depth_now);
+    const float dminp = (1 - 0.02f) * depth_now, dmaxp = (1 + 0.02f) * depth_now;
+    const float depth_perturbed = rng_uniform(rs) * (dmaxp - dminp) + dminp;
+    const float4 ppert = perturbed_normal(c0, x, y, pnow, rs, (float)(0.02f * 3.14159265358979323846));
+    float4 h0 = pnow, h1 = prand, h2 = prand, h3 = ppert, h4 = pnow;
+    h0.w = dist2origin(c0, x, y, depth_rand, h0);
+    h1.w = dist2origin(c0, x, y, depth_now, h1);
+    h2.w = dist2origin(c0, x, y, depth_rand, h2);
+    h3.w = dist2origin(c0, x, y, depth_now, h3);
+    h4.w = dist2origin(c0, x, y, depth_perturbed, h4);
+    hyp[0] = h0; hyp[1] = h1; hyp[2] = h2; hyp[3] = h3; hyp[4] = h4;
+  }
+  wave_sync();
+  // ---- phase 6: refinement NCCs, jobs (hypothesis, selected view)
+  if (active) {
+    for (int j = c; j < 5 * nsel; j += C) {
+      const int h = j / nsel, k = j % nsel;
+      ref[h * nv + k] = ncc_old_any<U8>(fast, pw, s_ref, s_rr, s_w, x, y, pc, B, sel_list[k] + 1, hyp[h]);
+    }
+  }
+  wave_sync();
+  // ---- serial: sequential acceptance + write-back (DPE.cu:1097-1117, 1656-1665)
+  if (active && c == 0) {
+    const float dmin = pc.P.depth_min, dmax = pc.P.depth_max;
+    for (int h = 0; h < 5; ++h) {
+      const float4 tp = hyp[h];
+      float tc = 0.0f;
+      for (int k = 0; k < nsel; ++k) tc += vwl[sel_list[k]] * ref[h * nv + k];
+      tc /= wnorm;
+      const float db = depth_from_plane(c0, tp, x, y);
+      if (db >= dmin && db <= dmax && tc < cost_now) { depth_now = db; pnow = tp; cost_now = tc; }
+    }
+    if (pc.P.state == DPE_REFINE_INIT) {
+      if ((double)cost_now < (double)cost_written - 0.1) { B.costs[center] = cost_now; B.planes[center] = pnow; }
+    } else {
+      B.costs[center] = cost_now;
+      B.planes[center] = pnow;
+    }
+  }
+}
+
+}  // namespace dpe

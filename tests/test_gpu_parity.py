@@ -119,3 +119,13 @@ def test_error_paths(ctx):
     with pytest.raises(native.DpeError):
         fresh.execute()                                      # execute before stage
     fresh.close()
+
+
+def test_gpu_non_integer_images(ctx):
+    # rescaled pyramid levels are not 8-bit integers: exercises the f32 quad-texel layout
+    sc = synthetic.make_scene(96, 72, 4)
+    sc["images"] = [(im * np.float32(0.73) + np.float32(0.31)).astype(np.float32) for im in sc["images"]]
+    p = _params("refine_iter")
+    st = synthetic.gt_state(sc)
+    inp = synthetic.pass_input(sc, p, depths=synthetic.src_depths(sc))
+    assert_same(ctx.run(inp, st), oracle.run_pass(inp, st), "f32 images")
