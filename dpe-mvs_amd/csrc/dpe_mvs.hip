@@ -22,6 +22,7 @@
 using namespace dpe;
 
 static const int kDefaultXcdRows = 1;
+static constexpr int kWeakLanes = 16;   // lanes per weak pixel in k_weak_coop
 
 namespace {
 
@@ -373,7 +374,7 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
 
   const dim3 fb(16, 16), fg((W + 15) / 16, (H + 15) / 16);
   const dim3 hb(32, 4), hg((((W + 1) / 2) + 31) / 32, (pc.half_rows + 3) / 4);
-  const size_t sweep_lds = (size_t)10 * nv * 128 * sizeof(float) + (size_t)nv * 128;
+
   DevBufs Bc;
 
   // RunPatchMatch launch sequence (DPE.cu:3150-3226)
@@ -423,8 +424,16 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
     end();
     for (int colour = 0; colour < 2; ++colour) {
       Bc = begin(DPE_CLASS_WEAK);
-      if (c->img8) k_weak_sweep<true><<<hg, hb, sweep_lds, s>>>(dpc, Bc, it, colour);
-      else k_weak_sweep<false><<<hg, hb, sweep_lds, s>>>(dpc, Bc, it, colour);
+      {
+        const int* lst = c->lists.p + (colour * 2 + 1) * list_stride;
+        const int* cnt = c->list_totals.p + colour * 2 + 1;
+        constexpr int C = kWeakLanes, P = 64 / C;
+        const size_t per_wave = (size_t)P * weak_lds_per_pixel(nv) * sizeof(float);
+        const int wpb = per_wave * 4 <= 64 * 1024 ? 4 : (per_wave * 2 <= 64 * 1024 ? 2 : 1);
+        const unsigned grid = (unsigned)((L / 2 + 1 + wpb * P - 1) / (wpb * P));
+        if (c->img8) k_weak_coop<true, C><<<grid, 64 * wpb, per_wave * wpb, s>>>(dpc, Bc, it, lst, cnt);
+        else k_weak_coop<false, C><<<grid, 64 * wpb, per_wave * wpb, s>>>(dpc, Bc, it, lst, cnt);
+      }
       end();
     }
     HIPC(hipGetLastError());

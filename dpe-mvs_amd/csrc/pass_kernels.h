@@ -402,296 +402,6 @@ __global__ void __launch_bounds__(256) k_random_init(const PassConst* __restrict
   }
 }
 
-// ------------------------------------------------------------------------------ view selection
-// Multi-hypothesis joint view selection (DPE.cu:1547-1615 / 1710-1779).  `ca` = LDS cost slots
-// (slot-major, [slot][view][thread]), `cdf` = LDS [view][thread], `vwl` = LDS u8 [view][thread].
-struct LdsView {
-  float* ca; float* cdf; uint8_t* vwl; int bs; int tid; int nv;
-  DEV float& cost(int slot, int v) const { return ca[(slot * nv + v) * bs + tid]; }
-  DEV float& prob(int v) const { return cdf[v * bs + tid]; }
-  DEV uint8_t& vw(int v) const { return vwl[v * bs + tid]; }
-};
-
-template <class PriorF>
-DEV void view_selection(const LdsView& L, int iter, PriorF prior, Rng& rs, uint32_t& tsv, float& wnorm) {
-  const int nv = L.nv;
-  for (int i = 0; i < nv; ++i) L.vw(i) = 0;
-  const float cost_threshold = (float)(0.8 * (double)d_expf((float)(iter * iter) / (-90.0f)));
-  float psum = 0.0f;
-  for (int i = 0; i < nv; i++) {
-    float count = 0; int count_false = 0; float tmpw = 0;
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-      const float c = L.cost(j, i);
-      if (c < cost_threshold) { tmpw += d_expf(c * c / (-0.18f)); count++; }
-      if (c > 1.2f) count_false++;
-    }
-    float sp = 0.0f;
-    if (count > 2 && count_false < 3) sp = tmpw / count;
-    else if (count_false < 3) sp = d_expf(cost_threshold * cost_threshold / (-0.32f));
-    sp = sp * prior(i);
-    L.prob(i) = sp;
-    psum += sp;
-  }
-  // TransformPDFToCDF (DPE.cu:293-307)
-  const float inv = 1.0f / psum;
-  float cum = 0.0f;
-  for (int i = 0; i < nv; ++i) { const float q = L.prob(i) * inv; cum += q; L.prob(i) = cum; }
-  for (int s = 0; s < 15; ++s) {
-    const float rp = rng_uniform(rs) - 1.1920929e-07f;
-    for (int id = 0; id < nv; ++id) {
-      if (L.prob(id) > rp) { L.vw(id) = L.vw(id) + 1; break; }
-    }
-  }
-  uint32_t t = 0; float wn = 0;
-  for (int i = 0; i < nv; ++i) { const int w = L.vw(i); if (w > 0) { setBit(t, i); wn += w; } }
-  tsv = t; wnorm = wn;
-}
-
-// ------------------------------------------------------------------------------ strong sweep
-// CheckerboardPropagationStrong (DPE.cu:1214-1666) + PlaneHypothesisRefinementStrong (:1065-1118).
-// Neighbour reads come from the snapshot taken before the half-sweep (same-colour semantics).
-template <bool U8>
-__global__ void __launch_bounds__(128) k_strong_sweep(const PassConst* __restrict__ pcp, DevBufs B, int iter, int colour) {
-  extern __shared__ float lds[];
-  const PassConst& pc = *pcp;
-  PIX2D_HALF();
-  if (B.weak[center] == DPE_WEAK) return;
-  const int W = pc.W, H = pc.H, N = pc.N, nv = N - 1;
-  const DpeCamera& c0 = pc.cams[0];
-  const int bs = blockDim.x * blockDim.y, tid = threadIdx.y * blockDim.x + threadIdx.x;
-  LdsView L{lds, lds + 9 * nv * bs, (uint8_t*)(lds + 10 * nv * bs), bs, tid, nv};
-  Rng rs; rng_init(rs, (uint32_t)center, pc.seed32, STREAM_ITER_BASE + 4 * iter + 0, pc.salt);
-  const bool fast = pc.P.strong_radius == 5 && pc.P.strong_increment == 2;
-  Patch36 P;
-  if (fast) make_patch36(P, pc, B, x, y); else { P.px = x; P.py = y; }
-  const float* __restrict__ costs = B.costs_snap;
-  const float4* __restrict__ planes = B.planes_snap;
-
-  for (int d = 0; d < 8; ++d) for (int v = 0; v < nv; ++v) L.cost(d, v) = 0.0f;
-  L.cost(0, 0) = 2.0f;   // cost_array[8][32] = {2.0f} (DPE.cu:1236)
-  uint32_t flags = 0;
-  int positions[8];
-#pragma unroll
-  for (int d = 0; d < 8; ++d) positions[d] = 0;
-
-  auto costvec = [&](const float4& pl, int slot) {
-    for (int v = 1; v < N; ++v) L.cost(slot, v - 1) = ncc_old<U8>(P, fast, pc, B, v, pl);
-  };
-
-  if (pc.P.use_edge) {
-    const short2* en = B.edge_neigh + (size_t)center * 8;
-    const float max_edge_dist = MAXo(H, W) / 30.0f;
-    const int min_step_len = 2;
-    const bool on_edge = B.edge[center] != 0;
-#pragma unroll
-    for (int d = 0; d < 8; ++d) {
-      const int dx = kDir[d][0], dy = kDir[d][1];
-      const int s0 = MAXo(1, 5 - 2 * iter);
-      const short2 ep = en[d];
-      const double ex = (double)(ep.x - x), ey = (double)(ep.y - y);
-      float dist = (float)__builtin_sqrt(ex * ex + ey * ey);
-      if (d >= 4) dist = (float)((double)dist / 1.4142135623730951);
-      if (on_edge) dist = 11 * min_step_len;
-      else if (ep.x == -1 || ep.y == -1 || dist > max_edge_dist) {
-        dist = max_edge_dist;
-        if (d >= 4) dist = (float)((double)dist / 1.4142135623730951);
-      }
-      const int step_num = MINo(MAXo(11, f2i(1.0f * dist / min_step_len)), 22);
-      int step_len = MAXo(f2i(1.0f * dist / step_num), min_step_len);
-      if (d < 4 && step_len % 2 == 1) step_len -= 1;
-      int fx = 0, fy = 0;
-      if (d > 4) { if (d % 2) fx = dx; else fy = dy; }
-      int mpos = 0; float mc = 3.40282347e+38f;
-      for (int step = 0; step < step_num; ++step) {
-        const int tx = x + s0 * dx + step * step_len * dx + fx, ty = y + s0 * dy + step * step_len * dy + fy;
-        if (!(tx >= 0 && ty >= 0 && tx < W && ty < H)) continue;
-        const int ptc = tx + ty * W;
-        const float c = costs[ptc];
-        if (mc > c) { mpos = ptc; mc = c; }
-      }
-      if (mc < 3.40282347e+38f) { flags |= 1u << d; positions[d] = mpos; costvec(planes[mpos], d); }
-    }
-    if (!on_edge) {
-      const float good_threshold = 0.8f * d_expf((float)(iter * iter) / (-90.0f));
-      const float bad_threshold = 1.2f;
-#pragma unroll
-      for (int d = 0; d < 8; ++d) {
-        const int dx = kDir[d][0], dy = kDir[d][1];
-        const int s0 = MAXo(1, 5 - 2 * iter);
-        const bool had = (flags >> d) & 1u;
-        int fx = 0, fy = 0;
-        if (d > 4) { if (d % 2) fx = dx; else fy = dy; }
-        int mpos = 0; float mc = 3.40282347e+38f;
-        for (int step = 0; step < 11; ++step) {
-          const int tx = x + s0 * dx + step * min_step_len * dx + fx, ty = y + s0 * dy + step * min_step_len * dy + fy;
-          if (!(tx >= 0 && ty >= 0 && tx < W && ty < H)) continue;
-          const int ptc = tx + ty * W;
-          const float c = costs[ptc];
-          if (mc > c) { mpos = ptc; mc = c; }
-        }
-        if (mc < 3.40282347e+38f) {
-          flags |= 1u << d;
-          costvec(planes[mpos], 8);
-          int g0 = 0, g1 = 0, b0 = 0, b1 = 0;
-          for (int j = 0; j < nv; j++) {
-            const float v0 = L.cost(d, j);
-            if (v0 < good_threshold) g0++;
-            if (v0 > bad_threshold) b0++;
-          }
-          for (int j = 0; j < nv; j++) {
-            const float v1 = L.cost(8, j);
-            if (v1 < good_threshold) g1++;
-            if (v1 > bad_threshold) b1++;
-          }
-          if (!had || g1 > g0 || (g1 == g0 && b1 < b0)) {
-            positions[d] = mpos;
-            for (int j = 0; j < nv; j++) L.cost(d, j) = L.cost(8, j);
-          }
-        }
-      }
-    }
-  } else {
-    // ACMH-style near/far candidates (DPE.cu:1346-1544); slot order 0 up_near, 1 up_far,
-    // 2 down_near, 3 down_far, 4 left_near, 5 left_far, 6 right_near, 7 right_far
-    float costMin; int cmp;
-    int left_near = center - 1, left_far = center - 3, right_near = center + 1, right_far = center + 3;
-    int up_near = center - W, up_far = center - 3 * W, down_near = center + W, down_far = center + 3 * W;
-    if (y > 2) {
-      flags |= 1u << 1; costMin = costs[up_far]; cmp = up_far;
-      for (int i = 1; i < 11; ++i) if (y > 2 + 2 * i) { const int pt = up_far - 2 * i * W; if (costs[pt] < costMin) { costMin = costs[pt]; cmp = pt; } }
-      up_far = cmp; costvec(planes[up_far], 1);
-    }
-    if (y < H - 3) {
-      flags |= 1u << 3; costMin = costs[down_far]; cmp = down_far;
-      for (int i = 1; i < 11; ++i) if (y < H - 3 - 2 * i) { const int pt = down_far + 2 * i * W; if (costs[pt] < costMin) { costMin = costs[pt]; cmp = pt; } }
-      down_far = cmp; costvec(planes[down_far], 3);
-    }
-    if (x > 2) {
-      flags |= 1u << 5; costMin = costs[left_far]; cmp = left_far;
-      for (int i = 1; i < 11; ++i) if (x > 2 + 2 * i) { const int pt = left_far - 2 * i; if (costs[pt] < costMin) { costMin = costs[pt]; cmp = pt; } }
-      left_far = cmp; costvec(planes[left_far], 5);
-    }
-    if (x < W - 3) {
-      flags |= 1u << 7; costMin = costs[right_far]; cmp = right_far;
-      for (int i = 1; i < 11; ++i) if (x < W - 3 - 2 * i) { const int pt = right_far + 2 * i; if (costs[pt] < costMin) { costMin = costs[pt]; cmp = pt; } }
-      right_far = cmp; costvec(planes[right_far], 7);
-    }
-    if (y > 0) {
-      flags |= 1u << 0; costMin = costs[up_near]; cmp = up_near;
-      for (int i = 0; i < 3; ++i) {
-        if (y > 1 + i && x > i) { const int pt = up_near - (1 + i) * W - (1 + i); if (costs[pt] < costMin) { costMin = costs[pt]; cmp = pt; } }
-        if (y > 1 + i && x < W - 1 - i) { const int pt = up_near - (1 + i) * W + (1 + i); if (costs[pt] < costMin) { costMin = costs[pt]; cmp = pt; } }
-      }
-      up_near = cmp; costvec(planes[up_near], 0);
-    }
-    if (y < H - 1) {
-      flags |= 1u << 2; costMin = costs[down_near]; cmp = down_near;
-      for (int i = 0; i < 3; ++i) {
-        if (y < H - 2 - i && x > i) { const int pt = down_near + (1 + i) * W - (1 + i); if (costs[pt] < costMin) { costMin = costs[pt]; cmp = pt; } }
-        if (y < H - 2 - i && x < W - 1 - i) { const int pt = down_near + (1 + i) * W + (1 + i); if (costs[pt] < costMin) { costMin = costs[pt]; cmp = pt; } }
-      }
-      down_near = cmp; costvec(planes[down_near], 2);
-    }
-    if (x > 0) {
-      flags |= 1u << 4; costMin = costs[left_near]; cmp = left_near;
-      for (int i = 0; i < 3; ++i) {
-        if (x > 1 + i && y > i) { const int pt = left_near - (1 + i) - (1 + i) * W; if (costs[pt] < costMin) { costMin = costs[pt]; cmp = pt; } }
-        if (x > 1 + i && y < H - 1 - i) { const int pt = left_near - (1 + i) + (1 + i) * W; if (costs[pt] < costMin) { costMin = costs[pt]; cmp = pt; } }
-      }
-      left_near = cmp; costvec(planes[left_near], 4);
-    }
-    if (x < W - 1) {
-      flags |= 1u << 6; costMin = costs[right_near]; cmp = right_near;
-      for (int i = 0; i < 3; ++i) {
-        if (x < W - 2 - i && y > i) { const int pt = right_near + (1 + i) - (1 + i) * W; if (costs[pt] < costMin) { costMin = costs[pt]; cmp = pt; } }
-        if (x < W - 2 - i && y < H - 1 - i) { const int pt = right_near + (1 + i) + (1 + i) * W; if (costs[pt] < costMin) { costMin = costs[pt]; cmp = pt; } }
-      }
-      right_near = cmp; costvec(planes[right_near], 6);
-    }
-    positions[0] = up_near; positions[1] = up_far; positions[2] = down_near; positions[3] = down_far;
-    positions[4] = left_near; positions[5] = left_far; positions[6] = right_near; positions[7] = right_far;
-  }
-
-  // priors from the 4-neighbourhood (DPE.cu:1552-1566), snapshot reads, out-of-array -> 0
-  const long Lp = (long)W * H;
-  uint32_t nsv[4];
-  const long npos[4] = {(long)center - W, (long)center + W, (long)center - 1, (long)center + 1};
-#pragma unroll
-  for (int i = 0; i < 4; ++i) nsv[i] = ((flags >> (2 * i)) & 1u) && npos[i] >= 0 && npos[i] < Lp ? B.sel_snap[npos[i]] : 0u;
-  auto prior = [&](int j) {
-    float p = 0.0f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) if ((flags >> (2 * i)) & 1u) p += isSet(nsv[i], j) == 1 ? 0.9f : 0.1f;
-    return p;
-  };
-  uint32_t tsv; float wnorm;
-  view_selection(L, iter, prior, rs, tsv, wnorm);
-  uint8_t* vwg = B.vw + (size_t)center * DPE_MAX_IMAGES;
-  for (int j = 0; j < DPE_MAX_IMAGES; ++j) vwg[j] = j < nv ? L.vw(j) : 0;
-
-  float final_costs[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    float f = 0.0f;
-    for (int j = 0; j < nv; ++j) { const int w = L.vw(j); if (w > 0) f += w * L.cost(i, j); }
-    final_costs[i] = f / wnorm;
-  }
-  int mi = 0; float mcost = final_costs[0];
-#pragma unroll
-  for (int i = 1; i < 8; ++i) if (final_costs[i] <= mcost) { mcost = final_costs[i]; mi = i; }   // FindMinCostIndex
-
-  const float4 cur = planes[center];
-  float cost_now = 0.0f;
-  for (int i = 0; i < nv; ++i) { const int w = L.vw(i); if (w > 0) cost_now += w * ncc_old<U8>(P, fast, pc, B, i + 1, cur); }
-  cost_now /= wnorm;
-  const float cost_written = cost_now;
-  B.costs[center] = cost_now;
-  float depth_now = depth_from_plane(c0, cur, x, y);
-  float4 pnow = cur;
-  int mpos = 0; float mfc = 0.0f;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) if (i == mi) { mpos = positions[i]; mfc = final_costs[i]; }
-  if ((flags >> mi) & 1u) {
-    const float4 cand = planes[mpos];
-    const float db = depth_from_plane(c0, cand, x, y);
-    if (db >= pc.P.depth_min && db <= pc.P.depth_max && mfc < cost_now) {
-      depth_now = db; pnow = cand; cost_now = mfc; B.sel[center] = tsv;
-    }
-  }
-  // PlaneHypothesisRefinementStrong (DPE.cu:1065-1118)
-  {
-    const float dmin = pc.P.depth_min, dmax = pc.P.depth_max;
-    const float depth_rand = rng_uniform(rs) * (dmax - dmin) + dmin;
-    const float4 prand = random_normal(c0, x, y, rs, depth_now);
-    const float dminp = (1 - 0.02f) * depth_now, dmaxp = (1 + 0.02f) * depth_now;
-    const float depth_perturbed = rng_uniform(rs) * (dmaxp - dminp) + dminp;
-    const float4 ppert = perturbed_normal(c0, x, y, pnow, rs, (float)(0.02f * 3.14159265358979323846));
-    const float dep0 = depth_now;
-    const float4 pl0 = pnow;
-    for (int h = 0; h < 5; ++h) {
-      float dh; float4 tp;
-      if (h == 0) { dh = depth_rand; tp = pl0; }
-      else if (h == 1) { dh = dep0; tp = prand; }
-      else if (h == 2) { dh = depth_rand; tp = prand; }
-      else if (h == 3) { dh = dep0; tp = ppert; }
-      else { dh = depth_perturbed; tp = pl0; }
-      tp.w = dist2origin(c0, x, y, dh, tp);
-      float tc = 0.0f;
-      for (int j = 0; j < nv; ++j) { const int w = L.vw(j); if (w > 0) tc += w * ncc_old<U8>(P, fast, pc, B, j + 1, tp); }
-      tc /= wnorm;
-      const float db = depth_from_plane(c0, tp, x, y);
-      if (db >= dmin && db <= dmax && tc < cost_now) { depth_now = db; pnow = tp; cost_now = tc; }
-    }
-  }
-  if (pc.P.state == DPE_REFINE_INIT) {
-    if ((double)cost_now < (double)cost_written - 0.1) { B.costs[center] = cost_now; B.planes[center] = pnow; }
-  } else {
-    B.costs[center] = cost_now;
-    B.planes[center] = pnow;
-  }
-}
-
 // ------------------------------------------------------------------------------ RANSACToGetFitPlane
 __global__ void __launch_bounds__(256) k_ransac_fit(const PassConst* __restrict__ pcp, DevBufs B, int iter) {   // DPE.cu:2891-3124
   const PassConst& pc = *pcp;
@@ -840,159 +550,6 @@ __global__ void __launch_bounds__(256) k_ransac_fit(const PassConst* __restrict_
   } else {
     B.fit_plane[center] = make_float4(0, 0, 0, 0);
     if (pc.P.use_radius) B.radius[center] = pc.P.strong_radius;
-  }
-}
-
-// ------------------------------------------------------------------------------ weak sweep
-// CheckerboardPropagationWeak (DPE.cu:1668-1862) + PlaneHypothesisRefinementWeak (:1120-1212).
-template <bool U8>
-__global__ void __launch_bounds__(128) k_weak_sweep(const PassConst* __restrict__ pcp, DevBufs B, int iter, int colour) {
-  extern __shared__ float lds[];
-  const PassConst& pc = *pcp;
-  PIX2D_HALF();
-  if (B.weak[center] != DPE_WEAK) return;
-  const int W = pc.W, N = pc.N, nv = N - 1;
-  const DpeCamera& c0 = pc.cams[0];
-  const int bs = blockDim.x * blockDim.y, tid = threadIdx.y * blockDim.x + threadIdx.x;
-  LdsView L{lds, lds + 9 * nv * bs, (uint8_t*)(lds + 10 * nv * bs), bs, tid, nv};
-  Rng rs; rng_init(rs, (uint32_t)center, pc.seed32, STREAM_ITER_BASE + 4 * iter + 2, pc.salt);
-  const bool geom = pc.P.geom_consistency;
-  const float gf = pc.P.geom_factor;
-  for (int d = 0; d < 8; ++d) for (int v = 0; v < nv; ++v) L.cost(d, v) = 0.0f;
-  L.cost(0, 0) = 2.0f;
-  const short2* nb = B.nb + (size_t)center * 9;
-  uint32_t flags = 0;
-  int positions[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    positions[i] = 0;
-    const short2 np = nb[i + 1];
-    if (np.x == -1 || np.y == -1 || B.weak[np.x + np.y * W] != DPE_STRONG) continue;
-    positions[i] = np.x + np.y * W;
-    flags |= 1u << i;
-    const float4 pl = B.planes[positions[i]];
-    for (int v = 1; v < N; ++v) L.cost(i, v - 1) = ncc_new<U8>(pc, B, x, y, v, pl);
-  }
-  uint32_t nsv[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const short2 np = nb[i + 1];
-    nsv[i] = (np.x == -1 || np.y == -1) ? 0u : B.sel[np.x + np.y * W];
-  }
-  auto prior = [&](int j) {
-    float p = 0.0f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const short2 np = nb[i + 1];
-      if (np.x == -1 || np.y == -1) continue;
-      p += isSet(nsv[i], j) == 1 ? 0.9f : 0.1f;
-    }
-    return p;
-  };
-  uint32_t tsv; float wnorm;
-  view_selection(L, iter, prior, rs, tsv, wnorm);
-  uint8_t* vwg = B.vw + (size_t)center * DPE_MAX_IMAGES;
-  for (int j = 0; j < DPE_MAX_IMAGES; ++j) vwg[j] = j < nv ? L.vw(j) : 0;
-
-  float final_costs[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    float f = 0.0f;
-    const bool fl = (flags >> i) & 1u;
-    const float4 cpl = B.planes[positions[i]];
-    for (int j = 0; j < nv; ++j) {
-      const int w = L.vw(j);
-      if (w > 0) {
-        if (geom) {
-          if (fl) f += w * (L.cost(i, j) + gf * geom_cost(pc, B, x, y, j + 1, cpl));
-          else f += w * (L.cost(i, j) + gf * 3.0f);
-        } else {
-          f += w * L.cost(i, j);
-        }
-      }
-    }
-    final_costs[i] = f / wnorm;
-  }
-  int mi = 0; float mcost = final_costs[0];
-#pragma unroll
-  for (int i = 1; i < 8; ++i) if (final_costs[i] <= mcost) { mcost = final_costs[i]; mi = i; }
-
-  const float4 cur = B.planes[center];
-  auto hyp_cost = [&](const float4& tp) {
-    float tc = 0.0f;
-    for (int j = 0; j < nv; ++j) {
-      const int w = L.vw(j);
-      if (w > 0) {
-        const float c = ncc_new<U8>(pc, B, x, y, j + 1, tp);
-        if (geom) tc += w * (c + gf * geom_cost(pc, B, x, y, j + 1, tp));
-        else tc += w * c;
-      }
-    }
-    return tc;
-  };
-  float cost_now = hyp_cost(cur) / wnorm;
-  const float cost_written = cost_now;
-  B.costs[center] = cost_now;
-  float depth_now = depth_from_plane(c0, cur, x, y);
-  float4 pnow = cur;
-  int mpos = 0; float mfc = 0.0f;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) if (i == mi) { mpos = positions[i]; mfc = final_costs[i]; }
-  if ((flags >> mi) & 1u) {
-    const float4 cand = B.planes[mpos];
-    const float db = depth_from_plane(c0, cand, x, y);
-    if (db >= pc.P.depth_min && db <= pc.P.depth_max && mfc < cost_now) {
-      depth_now = db; pnow = cand; cost_now = mfc; B.sel[center] = tsv;
-    }
-  }
-  // PlaneHypothesisRefinementWeak (DPE.cu:1120-1212)
-  {
-    const float dmin = pc.P.depth_min, dmax = pc.P.depth_max;
-    bool skip = false;
-    const float4 fp = B.fit_plane[center];
-    if (fp.x == 0 && fp.y == 0 && fp.z == 0) skip = true;
-    else {
-      const float tc = hyp_cost(fp) / wnorm;
-      const float db = depth_from_plane(c0, fp, x, y);
-      if (db >= dmin && db <= dmax && tc < cost_now) { depth_now = db; pnow = fp; cost_now = tc; }
-    }
-    if (!skip) {
-      const float depth_rand = rng_uniform(rs) * (dmax - dmin) + dmin;
-      const float4 prand = random_normal(c0, x, y, rs, depth_now);
-      const float dminp = (1 - 0.02f) * depth_now, dmaxp = (1 + 0.02f) * depth_now;
-      const float depth_perturbed = rng_uniform(rs) * (dmaxp - dminp) + dminp;
-      const float4 ppert = perturbed_normal(c0, x, y, pnow, rs, (float)(0.02f * 3.14159265358979323846));
-      const float dep0 = depth_now;
-      const float4 pl0 = pnow;
-      for (int h = 0; h < 5; ++h) {
-        float dh; float4 tp;
-        if (h == 0) { dh = depth_rand; tp = pl0; }
-        else if (h == 1) { dh = dep0; tp = prand; }
-        else if (h == 2) { dh = depth_rand; tp = prand; }
-        else if (h == 3) { dh = dep0; tp = ppert; }
-        else { dh = depth_perturbed; tp = pl0; }
-        tp.w = dist2origin(c0, x, y, dh, tp);
-        const float tc = hyp_cost(tp) / wnorm;
-        const float db = depth_from_plane(c0, tp, x, y);
-        if (db >= dmin && db <= dmax && tc < cost_now) { depth_now = db; pnow = tp; cost_now = tc; }
-      }
-    }
-  }
-  float4 fin = cur;
-  if (pc.P.state == DPE_REFINE_INIT) {
-    if ((double)cost_now < (double)cost_written - 0.1) { fin = pnow; B.planes[center] = pnow; }
-  } else {
-    fin = pnow;
-    B.planes[center] = pnow;
-  }
-  // final cost with the Old NCC (DPE.cu:1845-1861)
-  {
-    const bool fast = pc.P.strong_radius == 5 && pc.P.strong_increment == 2;
-    Patch36 P;
-    if (fast) make_patch36(P, pc, B, x, y); else { P.px = x; P.py = y; }
-    float c2 = 0.0f;
-    for (int i = 0; i < nv; ++i) { const int w = L.vw(i); if (w > 0) c2 += w * ncc_old<U8>(P, fast, pc, B, i + 1, fin); }
-    B.costs[center] = c2 / wnorm;
   }
 }
 

@@ -424,4 +424,363 @@ __global__ void __launch_bounds__(256) k_strong_coop(const PassConst* __restrict
   }
 }
 
+// ------------------------------------------------------------------------------ weak sweep
+// The NCC-New cost of a weak pixel (DPE.cu:557-690) is 9 bilateral patches (its own, radius from
+// the RANSAC radius map, and one around each deformable strong neighbour).  All tap weights are
+// plane- and view-independent, so they are tabulated once per pixel in LDS together with the
+// reference sums of each patch; an NCC job is then projection + bilinear fetch + 3 FMAs per tap.
+struct WeakTab {
+  const float* tcw; const float* tcwr;    // centre patch  w[n_c^2], w*grey[n_c^2]
+  const float* tnw; const float* tnwr;    // neighbour k=1..8: [(k-1)*9 + t]
+  const float* sums;                      // [9][3]: s_ref, s_rr, s_w of each tabulated patch
+  const short2* nbl;                      // [9] neighbour pixels (nb[0] = the pixel itself)
+  const uint32_t* nsv;                    // [9] selected_views of the neighbours
+  int rad_c, inc_c, n_c, rad_n, inc_n, n_n;
+  bool tab_c, tab_n;
+  float rc;                               // grey level of the pixel
+};
+
+// patch NCC with tabulated weights; the same tap order and arithmetic as patch_ncc_generic
+template <bool U8>
+DEV float patch_ncc_tab(const PassConst& pc, const DevBufs& B, int v, const Homog& H, int cx, int cy, int rad, int inc,
+                        int n, const float* __restrict__ tw, const float* __restrict__ twr, const float* sm) {
+  const int W = pc.W, Hh = pc.H;
+  float s_src = 0, s_ss = 0, s_rs = 0;
+  for (int a = 0; a < n; ++a) {
+    const float xf = (float)(cx - rad + a * inc);
+    const float bx = __builtin_fmaf(H.h[0], xf, H.h[2]);
+    const float by = __builtin_fmaf(H.h[3], xf, H.h[5]);
+    const float bz = __builtin_fmaf(H.h[6], xf, H.h[8]);
+    float r_src = 0, r_ss = 0, r_rs = 0;
+    for (int b = 0; b < n; ++b) {
+      const float yf = (float)(cy - rad + b * inc);
+      const float qx = __builtin_fmaf(H.h[1], yf, bx);
+      const float qy = __builtin_fmaf(H.h[4], yf, by);
+      const float qz = __builtin_fmaf(H.h[7], yf, bz);
+      const float iz = 1.0f / qz;
+      const float sp = sample_src<U8>(B, v, W, Hh, qx * iz, qy * iz);
+      const float w = tw[a * n + b], wr = twr[a * n + b];
+      r_src = __builtin_fmaf(w, sp, r_src);
+      const float ws = w * sp;
+      r_ss = __builtin_fmaf(ws, sp, r_ss);
+      r_rs = __builtin_fmaf(wr, sp, r_rs);
+    }
+    s_src += r_src; s_ss += r_ss; s_rs += r_rs;
+  }
+  count_work(B, 0, (unsigned long long)(n * n));
+  return ncc_finalize(sm[0], sm[1], sm[2], s_src, s_ss, s_rs);
+}
+
+// ComputeBilateralNCCNew (DPE.cu:557-690) of the tabulated weak pixel (px, py)
+template <bool U8>
+DEV float ncc_new_tab(const PassConst& pc, const DevBufs& B, const WeakTab& T, int px, int py, int v, const float4& pl) {
+  const int W = pc.W, Hh = pc.H;
+  const Homog H = make_homography(pc, v, pl);
+  count_work(B, 1, 0);
+  if (center_outside(pc, v, H, px, py)) return 2.0f;
+  float center_cost = 0.0f, strong_cost = 0.0f;
+  int strong_count = 0;
+  for (int k = 0; k < DPE_NEIGHBOUR_NUM; ++k) {
+    const short2 np = T.nbl[k];
+    if (np.x == -1 || np.y == -1) continue;
+    const float2 nsp = project_h(H, (float)np.x, (float)np.y);
+    if (nsp.x < 0 || nsp.y < 0 || nsp.x >= (float)W || nsp.y >= (float)Hh) {
+      if (k != 0) {
+        if (isSet(T.nsv[k], v - 1)) { strong_cost += 2.0f; strong_count++; }
+        continue;
+      }
+      return 2.0f;
+    }
+    float tc;
+    if (k == 0) {
+      tc = T.tab_c ? patch_ncc_tab<U8>(pc, B, v, H, np.x, np.y, T.rad_c, T.inc_c, T.n_c, T.tcw, T.tcwr, T.sums)
+                   : patch_ncc_generic<U8>(pc, B, v, H, np.x, np.y, T.rc, T.rad_c, T.inc_c);
+      center_cost = tc;
+    } else {
+      tc = T.tab_n ? patch_ncc_tab<U8>(pc, B, v, H, np.x, np.y, T.rad_n, T.inc_n, T.n_n, T.tnw + (k - 1) * 9,
+                                       T.tnwr + (k - 1) * 9, T.sums + 3 * k)
+                   : patch_ncc_generic<U8>(pc, B, v, H, np.x, np.y, T.rc, T.rad_n, T.inc_n);
+      strong_cost += tc; strong_count++;
+    }
+  }
+  if (strong_count == 0) return center_cost;
+  strong_cost /= (float)strong_count;
+  strong_cost = MINo(strong_cost, 2.0f);
+  return (float)(0.25 * (double)center_cost + 0.75 * (double)strong_cost);
+}
+
+// LDS floats per weak pixel (fixed part 480, see the carve in k_weak_coop); multiple of 4
+__host__ __device__ inline int weak_lds_per_pixel(int nv) { return (480 + 17 * nv + 3) & ~3; }
+
+// CheckerboardPropagationWeak (DPE.cu:1668-1862) + PlaneHypothesisRefinementWeak (:1120-1212).
+// C lanes per pixel, 64/C pixels per wave, blockDim.x/64 waves per workgroup.
+template <bool U8, int C>
+__global__ void __launch_bounds__(256) k_weak_coop(const PassConst* __restrict__ pcp, DevBufs B, int iter,
+                                                   const int* __restrict__ list, const int* __restrict__ nlist_p) {
+  extern __shared__ float4 lds4[];
+  constexpr int P = 64 / C;
+  const PassConst& pc = *pcp;
+  const int nlist = *nlist_p;
+  const int wpb = blockDim.x >> 6;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int ps = lane / C, c = lane % C;
+  const int W = pc.W, Hh = pc.H, nv = pc.N - 1;
+  const DpeCamera& c0 = pc.cams[0];
+  const int wbase = (xcd_remap(blockIdx.x, gridDim.x, B.xcd_rows * 16) * wpb + wave) * P;
+  if (wbase >= nlist) return;                            // wave-uniform tail
+  const int gi = wbase + ps;
+  const bool active = gi < nlist;
+  const int center = active ? list[gi] : 0;
+  const int x = center % W, y = center / W;
+  // ---- LDS carve (per pixel, floats)
+  const int S = weak_lds_per_pixel(nv);
+  float* pb = (float*)lds4 + (size_t)(wave * P + ps) * S;
+  float* pw = pb;                                        // [108] Old-NCC patch (patch_lds_build)
+  float* tcw = pb + 108; float* tcwr = pb + 144;         // centre patch table
+  float* tnw = pb + 180; float* tnwr = pb + 252;         // neighbour patch tables [8][9]
+  float* sums = pb + 324;                                // [9][3]
+  float* osum = pb + 352;                                // [3] Old-NCC patch sums
+  float4* cpl = (float4*)(pb + 356);                     // [8] candidate planes
+  float4* hyp = (float4*)(pb + 388);                     // [7] refinement hypotheses / final plane
+  float* fc = pb + 416;                                  // [8] final candidate costs
+  int* misc = (int*)(pb + 424);                          // 0 nsel, 1 ncand, 2 skip, 3 tsv, 4 wnorm, 8..15 flags
+  short2* nbl = (short2*)(pb + 440);                     // [9]
+  uint32_t* nsv = (uint32_t*)(pb + 452);                 // [9]
+  int* cand = (int*)(pb + 464);                          // [8] flagged candidate rows
+  uint8_t* vwl = (uint8_t*)(pb + 472);                   // [32] view weights
+  float* cost = pb + 480;                                // [8][nv]
+  float* sp = cost + 8 * nv;                             // [nv]
+  int* sel_list = (int*)(sp + nv);                       // [nv]
+  float* hv = (float*)(sel_list + nv);                   // [7][nv] hypothesis x selected-view values
+
+  const bool geom = pc.P.geom_consistency;
+  const float gf = pc.P.geom_factor;
+  const bool fast_old = pc.P.strong_radius == 5 && pc.P.strong_increment == 2;
+  WeakTab T;
+  T.rad_c = pc.P.strong_radius; T.inc_c = pc.P.strong_increment;
+  if (pc.P.use_radius && active) { T.rad_c = B.radius[center]; T.inc_c = MAXo(2, d2i(2.0 * T.rad_c / 5.0)); }
+  T.rad_n = pc.P.weak_radius; T.inc_n = pc.P.weak_increment;
+  T.n_c = T.rad_c >= 0 ? (2 * T.rad_c) / T.inc_c + 1 : 0;
+  T.n_n = T.rad_n >= 0 ? (2 * T.rad_n) / T.inc_n + 1 : 0;
+  T.tab_c = T.n_c >= 1 && T.n_c <= 6;
+  T.tab_n = T.n_n >= 1 && T.n_n <= 3;
+  T.rc = active ? ref_texel(B.ref, W, Hh, x, y) : 0.0f;
+  T.tcw = tcw; T.tcwr = tcwr; T.tnw = tnw; T.tnwr = tnwr; T.sums = sums; T.nbl = nbl; T.nsv = nsv;
+  const short2* nbg = B.nb + (size_t)center * 9;
+
+  // ---- phase 1: neighbours, weight tables, Old-NCC patch, candidate rows
+  if (active) {
+    if (fast_old) patch_lds_build(pw, pc, B, x, y, c, C);
+    for (int k = c; k < 9; k += C) {
+      const short2 np = nbg[k];
+      nbl[k] = np;
+      nsv[k] = (np.x == -1 || np.y == -1) ? 0u : B.sel[np.x + np.y * W];
+    }
+    const int ntc = T.tab_c ? T.n_c * T.n_c : 0, ntn = T.tab_n ? T.n_n * T.n_n : 0;
+    const float ss = pc.P.sigma_spatial, sc = pc.P.sigma_color;
+    for (int t = c; t < ntc + 8 * ntn; t += C) {
+      int k, tt, n, rad, inc;
+      if (t < ntc) { k = 0; tt = t; n = T.n_c; rad = T.rad_c; inc = T.inc_c; }
+      else { k = 1 + (t - ntc) / ntn; tt = (t - ntc) % ntn; n = T.n_n; rad = T.rad_n; inc = T.inc_n; }
+      const short2 np = nbg[k];
+      if (np.x == -1 || np.y == -1) continue;
+      const int i = -rad + (tt / n) * inc, j = -rad + (tt % n) * inc;
+      const float rp = ref_texel(B.ref, W, Hh, np.x + i, np.y + j);
+      const float w = bilateral_weight(i, j, rp, T.rc, ss, sc);
+      if (k == 0) { tcw[tt] = w; tcwr[tt] = w * rp; }
+      else { tnw[(k - 1) * 9 + tt] = w; tnwr[(k - 1) * 9 + tt] = w * rp; }
+    }
+    for (int i = c; i < 8; i += C) {
+      const short2 np = nbg[i + 1];
+      const bool fl = !(np.x == -1 || np.y == -1) && B.weak[np.x + np.y * W] == DPE_STRONG;
+      misc[8 + i] = fl ? 1 : 0;
+      if (fl) cpl[i] = B.planes[np.x + np.y * W];
+      else for (int v = 0; v < nv; ++v) cost[i * nv + v] = (i == 0 && v == 0) ? 2.0f : 0.0f;
+    }
+  }
+  wave_sync();
+  // ---- phase 1b: reference sums of every tabulated patch (tap order of patch_ncc_generic)
+  if (active) {
+    for (int k = c; k < 9; k += C) {
+      const short2 np = nbl[k];
+      if (np.x == -1 || np.y == -1 || !(k == 0 ? T.tab_c : T.tab_n)) continue;
+      const int n = k == 0 ? T.n_c : T.n_n, rad = k == 0 ? T.rad_c : T.rad_n, inc = k == 0 ? T.inc_c : T.inc_n;
+      const float* tw = k == 0 ? tcw : tnw + (k - 1) * 9;
+      const float* twr = k == 0 ? tcwr : tnwr + (k - 1) * 9;
+      float a_ref = 0, a_rr = 0, a_w = 0;
+      for (int a = 0; a < n; ++a) {
+        float r_ref = 0, r_rr = 0, r_w = 0;
+        for (int b = 0; b < n; ++b) {
+          const float rp = ref_texel(B.ref, W, Hh, np.x - rad + a * inc, np.y - rad + b * inc);
+          const float w = tw[a * n + b], wr = twr[a * n + b];
+          r_ref = r_ref + wr;
+          r_rr = __builtin_fmaf(wr, rp, r_rr);
+          r_w = r_w + w;
+        }
+        a_ref += r_ref; a_rr += r_rr; a_w += r_w;
+      }
+      sums[3 * k] = a_ref; sums[3 * k + 1] = a_rr; sums[3 * k + 2] = a_w;
+    }
+    if (c == C - 1) {
+      if (fast_old) patch_lds_sums(pw, osum[0], osum[1], osum[2]);
+      int nc = 0;
+      for (int i = 0; i < 8; ++i) if (misc[8 + i]) cand[nc++] = i;
+      misc[1] = nc;
+    }
+  }
+  wave_sync();
+  // ---- phase 2: candidate cost vectors, jobs (flagged neighbour, view)
+  if (active) {
+    const int ncand = misc[1];
+    for (int j = c; j < ncand * nv; j += C) {
+      const int i = cand[j / nv], v = j % nv + 1;
+      cost[i * nv + v - 1] = ncc_new_tab<U8>(pc, B, T, x, y, v, cpl[i]);
+    }
+  }
+  wave_sync();
+  // ---- phase 3: per-view probabilities with the deformable-neighbour priors (DPE.cu:1768-1790)
+  const float cost_threshold = (float)(0.8 * (double)d_expf((float)(iter * iter) / (-90.0f)));
+  if (active) {
+    auto cst = [&](int j, int i) -> float { return cost[j * nv + i]; };
+    for (int v = c; v < nv; v += C) {
+      float prior = 0.0f;
+      for (int i = 0; i < 8; ++i) {
+        const short2 np = nbl[i + 1];
+        if (np.x == -1 || np.y == -1) continue;
+        prior += isSet(nsv[i + 1], v) == 1 ? 0.9f : 0.1f;
+      }
+      sp[v] = view_prob_raw(cst, v, cost_threshold) * prior;
+    }
+  }
+  wave_sync();
+  Rng rs;
+  uint32_t tsv = 0; float wnorm = 0.0f;
+  if (active && c == 0) {
+    rng_init(rs, (uint32_t)center, pc.seed32, STREAM_ITER_BASE + 4 * iter + 2, pc.salt);
+    view_sample(sp, nv, rs, vwl, tsv, wnorm);
+    int ns = 0;
+    for (int i = 0; i < nv; ++i) if (vwl[i] > 0) sel_list[ns++] = i;
+    misc[0] = ns;
+    misc[4] = __float_as_int(wnorm);
+    uint8_t* vwg = B.vw + (size_t)center * DPE_MAX_IMAGES;
+    for (int j = 0; j < DPE_MAX_IMAGES; ++j) vwg[j] = vwl[j];
+  }
+  wave_sync();
+  const int nsel = active ? misc[0] : 0;
+  const float wn = active ? __int_as_float(misc[4]) : 1.0f;
+  const float4 cur = active ? B.planes[center] : make_float4(0, 0, 0, 1);
+  const float4 fp = active ? B.fit_plane[center] : make_float4(0, 0, 0, 0);
+  const bool has_fit = !(fp.x == 0 && fp.y == 0 && fp.z == 0);
+  auto hyp_val = [&](int v, const float4& pl) -> float {   // one term of hyp_cost (DPE.cu:1140-1150)
+    const float cn = ncc_new_tab<U8>(pc, B, T, x, y, v, pl);
+    return geom ? cn + gf * geom_cost(pc, B, x, y, v, pl) : cn;
+  };
+  // ---- phase 4: current plane and fit plane over the selected views; final candidate costs
+  if (active) {
+    const int nj = (has_fit ? 2 : 1) * nsel;
+    for (int j = c; j < nj; j += C) {
+      const int h = j / nsel, k = j % nsel;
+      hv[h * nv + k] = hyp_val(sel_list[k] + 1, h ? fp : cur);
+    }
+    for (int i = c; i < 8; i += C) {
+      const bool fl = misc[8 + i] != 0;
+      float f = 0.0f;
+      for (int j = 0; j < nv; ++j) {
+        const int w = vwl[j];
+        if (w > 0) {
+          if (geom) {
+            if (fl) f += w * (cost[i * nv + j] + gf * geom_cost(pc, B, x, y, j + 1, cpl[i]));
+            else f += w * (cost[i * nv + j] + gf * 3.0f);
+          } else {
+            f += w * cost[i * nv + j];
+          }
+        }
+      }
+      fc[i] = f / wn;
+    }
+  }
+  wave_sync();
+  // ---- serial: propagation acceptance, fit plane, refinement hypotheses (DPE.cu:1792-1843, 1120-1170)
+  float cost_now = 0.0f, cost_written = 0.0f, depth_now = 0.0f;
+  float4 pnow = cur;
+  const float dmin = pc.P.depth_min, dmax = pc.P.depth_max;
+  if (active && c == 0) {
+    int mi = 0; float mcost = fc[0];
+    for (int i = 1; i < 8; ++i) if (fc[i] <= mcost) { mcost = fc[i]; mi = i; }
+    for (int k = 0; k < nsel; ++k) cost_now += vwl[sel_list[k]] * hv[k];
+    cost_now /= wnorm;
+    cost_written = cost_now;
+    depth_now = depth_from_plane(c0, cur, x, y);
+    if (misc[8 + mi]) {
+      const float4 cand_pl = cpl[mi];
+      const float db = depth_from_plane(c0, cand_pl, x, y);
+      if (db >= dmin && db <= dmax && fc[mi] < cost_now) {
+        depth_now = db; pnow = cand_pl; cost_now = fc[mi]; B.sel[center] = tsv;
+      }
+    }
+    if (has_fit) {
+      float tc = 0.0f;
+      for (int k = 0; k < nsel; ++k) tc += vwl[sel_list[k]] * hv[nv + k];
+      tc /= wnorm;
+      const float db = depth_from_plane(c0, fp, x, y);
+      if (db >= dmin && db <= dmax && tc < cost_now) { depth_now = db; pnow = fp; cost_now = tc; }
+      const float depth_rand = rng_uniform(rs) * (dmax - dmin) + dmin;
+      const float4 prand = random_normal(c0, x, y, rs, depth_now);
+      const float dminp = (1 - 0.02f) * depth_now, dmaxp = (1 + 0.02f) * depth_now;
+      const float depth_perturbed = rng_uniform(rs) * (dmaxp - dminp) + dminp;
+      const float4 ppert = perturbed_normal(c0, x, y, pnow, rs, (float)(0.02f * 3.14159265358979323846));
+      float4 h0 = pnow, h1 = prand, h2 = prand, h3 = ppert, h4 = pnow;
+      h0.w = dist2origin(c0, x, y, depth_rand, h0);
+      h1.w = dist2origin(c0, x, y, depth_now, h1);
+      h2.w = dist2origin(c0, x, y, depth_rand, h2);
+      h3.w = dist2origin(c0, x, y, depth_now, h3);
+      h4.w = dist2origin(c0, x, y, depth_perturbed, h4);
+      hyp[0] = h0; hyp[1] = h1; hyp[2] = h2; hyp[3] = h3; hyp[4] = h4;
+    }
+  }
+  wave_sync();
+  // ---- phase 5: refinement NCCs, jobs (hypothesis, selected view)
+  if (active && has_fit) {
+    for (int j = c; j < 5 * nsel; j += C) {
+      const int h = j / nsel, k = j % nsel;
+      hv[(2 + h) * nv + k] = hyp_val(sel_list[k] + 1, hyp[h]);
+    }
+  }
+  wave_sync();
+  // ---- serial: sequential acceptance + write-back (DPE.cu:1190-1207, 1831-1843)
+  if (active && c == 0) {
+    if (has_fit) {
+      for (int h = 0; h < 5; ++h) {
+        const float4 tp = hyp[h];
+        float tc = 0.0f;
+        for (int k = 0; k < nsel; ++k) tc += vwl[sel_list[k]] * hv[(2 + h) * nv + k];
+        tc /= wnorm;
+        const float db = depth_from_plane(c0, tp, x, y);
+        if (db >= dmin && db <= dmax && tc < cost_now) { depth_now = db; pnow = tp; cost_now = tc; }
+      }
+    }
+    float4 fin = cur;
+    if (pc.P.state == DPE_REFINE_INIT) {
+      if ((double)cost_now < (double)cost_written - 0.1) { fin = pnow; B.planes[center] = pnow; }
+    } else {
+      fin = pnow;
+      B.planes[center] = pnow;
+    }
+    hyp[5] = fin;
+  }
+  wave_sync();
+  // ---- phase 6: the stored cost is the Old NCC of the final plane (DPE.cu:1845-1861)
+  if (active) {
+    const float4 fin = hyp[5];
+    for (int k = c; k < nsel; k += C)
+      hv[k] = ncc_old_any<U8>(fast_old, pw, osum[0], osum[1], osum[2], x, y, pc, B, sel_list[k] + 1, fin);
+  }
+  wave_sync();
+  if (active && c == 0) {
+    float c2 = 0.0f;
+    for (int k = 0; k < nsel; ++k) c2 += vwl[sel_list[k]] * hv[k];
+    B.costs[center] = c2 / wnorm;
+  }
+}
+
 }  // namespace dpe
