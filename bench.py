@@ -36,6 +36,11 @@ HBM_PEAK_GBS = 8000.0           # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 FLOP_PER_TAP = 32               # algorithmic model: 36-tap NCC = 36*32 + 120
 FLOP_PER_HOMOGRAPHY = 120
 FLOP_PER_GEOM = 60
+# per-dispatch HBM bytes from the committed PMC passes (tools/pmc.sh + tools/prof_summary.py)
+PMC_JSON = os.path.join(ROOT, "profiles", "r01_pmc.json")
+CLASS_KERNEL = {"strong": "k_strong_coop", "weak": "k_weak_coop", "depth_to_weak": "k_depth_to_weak",
+                "local_refine": "k_local_refine", "init": "k_random_init", "ransac": "k_ransac_fit",
+                "setup": "k_gen_neighbours"}
 
 
 def workload_params(abi, N):
@@ -56,6 +61,15 @@ def workload_params(abi, N):
 
 def algorithmic_flops(cnt: dict) -> float:
     return FLOP_PER_HOMOGRAPHY * cnt["ncc"] + FLOP_PER_TAP * cnt["taps"] + FLOP_PER_GEOM * cnt["geom"]
+
+
+def pmc_traffic(cls: str):
+    """HBM bytes per launch of the class's kernel from the committed PMC summary, or None."""
+    if not os.path.exists(PMC_JSON):
+        return None
+    tr = json.load(open(PMC_JSON)).get("traffic", {})
+    vals = [v["hbm_bytes_per_dispatch"] for k, v in tr.items() if k.split("<")[0] == CLASS_KERNEL.get(cls)]
+    return sum(vals) / len(vals) if vals else None
 
 
 def cpu_baseline(abi, synthetic, seconds_hint: float = 20.0) -> dict:
@@ -197,7 +211,8 @@ def main():
             "peak": FP32_PEAK_TFLOPS,
             "unit": "TFLOP/s",
             "frac": round(achieved_tflops / FP32_PEAK_TFLOPS, 4),
-            "traffic": None,
+            "traffic": pmc_traffic(dom),
+            "traffic_source": os.path.relpath(PMC_JSON, ROOT) + " (FETCH_SIZE x2 x1024 + WRITE_SIZE x1024, per launch)",
             "note": "FP32-ALU bound (no MFMA-shaped work; the f32 MFMA peak equals the f32 VALU peak). "
                     "achieved = algorithmic FLOP per launch (120/homography + 32/bilinear tap + 60/geom term, "
                     "counted on device) / avg launch time (hipEvents)",

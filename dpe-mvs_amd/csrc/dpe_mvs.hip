@@ -9,6 +9,7 @@
 //   * cuRAND states (48 B/px + curand_init) are replaced by counter-based Philox;
 //   * errors are return codes (no exit()).
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -310,7 +311,7 @@ extern "C" int dpe_pm_stage(DpeContext* c, const DpePassInput* in, const DpePass
   HIPC(c->nb.ensure(L * 9)); HIPC(c->nearest.ensure(L)); HIPC(c->edge_neigh.ensure(L * 8)); HIPC(c->lab_bound.ensure(L * 8));
   HIPC(c->radius.ensure(L));
   HIPC(c->tab_right.ensure(L)); HIPC(c->tab_down.ensure(L));
-  HIPC(c->lists.ensure(4 * (L / 2 + 64))); HIPC(c->row_counts.ensure(4 * (size_t)H + 4)); HIPC(c->list_totals.ensure(4));
+  HIPC(c->lists.ensure(4 * (L / 2 + 64) + L + 64)); HIPC(c->row_counts.ensure(4 * (size_t)H + 4)); HIPC(c->list_totals.ensure(8));
   B.planes = c->planes.p; B.planes_snap = c->planes_snap.p; B.fit_plane = c->fit_plane.p;
   B.costs = c->costs.p; B.costs_snap = c->costs_snap.p; B.complex_ = c->complex_.p;
   B.sel = c->sel.p; B.sel_snap = c->sel_snap.p;
@@ -383,13 +384,18 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   k_strong_tables_rows<<<(H + 63) / 64, 64, 0, s>>>(dpc, Bc, c->tab_right.p);
   k_strong_tables_cols<<<(W + 63) / 64, 64, 0, s>>>(dpc, Bc, c->tab_down.p);
   k_find_nearest_strong<<<fg, fb, 0, s>>>(dpc, Bc, c->tab_right.p, c->tab_down.p);
-  k_gen_neighbours<<<fg, fb, 0, s>>>(dpc, Bc);
+  // list of all WEAK pixels (list slot 4), then GenNeighbours one wave per WEAK pixel
+  const long list_stride = (long)(L / 2 + 64);
+  int* weak_list = c->lists.p + 4 * list_stride;
+  k_list_count<1><<<(H + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p);
+  k_list_scan<1><<<1, 64, 0, s>>>(dpc, c->row_counts.p, c->list_totals.p + 4);
+  k_list_fill<1><<<(H + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p, weak_list, (long)L);
+  k_gen_neighbours<<<(unsigned)((L + 255) / 256), 256, 0, s>>>(dpc, Bc, weak_list, c->list_totals.p + 4);
   k_neighbour_update<<<fg, fb, 0, s>>>(dpc, Bc);
   // per-colour pixel lists of the sweeps (weak_info is fixed from here until DepthToWeak)
-  const long list_stride = (long)(L / 2 + 64);
-  k_list_count<<<(pc.half_rows + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p);
-  k_list_scan<<<1, 64, 0, s>>>(dpc, c->row_counts.p, c->list_totals.p);
-  k_list_fill<<<(pc.half_rows + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p, c->lists.p, list_stride);
+  k_list_count<0><<<(pc.half_rows + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p);
+  k_list_scan<0><<<1, 256, 0, s>>>(dpc, c->row_counts.p, c->list_totals.p);
+  k_list_fill<0><<<(pc.half_rows + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p, c->lists.p, list_stride);
   end();
   Bc = begin(DPE_CLASS_INIT);
   if (c->img8) k_random_init<true><<<fg, fb, 0, s>>>(dpc, Bc); else k_random_init<false><<<fg, fb, 0, s>>>(dpc, Bc);

@@ -80,11 +80,15 @@ __global__ void k_gen_edge_inform(const PassConst* __restrict__ pcp, DevBufs B) 
 }
 
 // ------------------------------------------------------------------------------ GenNeighbours
-__global__ void __launch_bounds__(256) k_gen_neighbours(const PassConst* __restrict__ pcp, DevBufs B) {   // DPE.cu:2103-2463
+// One thread per WEAK pixel of `list` (the reference's full-grid launch with most threads idle).
+__global__ void __launch_bounds__(256) k_gen_neighbours(const PassConst* __restrict__ pcp, DevBufs B,
+                                                        const int* __restrict__ list, const int* __restrict__ nlist_p) {   // DPE.cu:2103-2463
   const PassConst& pc = *pcp;
-  PIX2D_FULL();
+  const int gi = xcd_remap(blockIdx.x, gridDim.x, B.xcd_rows * 16) * blockDim.x + threadIdx.x;
+  if (gi >= *nlist_p) return;
   const int W = pc.W, H = pc.H;
-  if (B.weak[center] != DPE_WEAK) return;
+  const int center = list[gi];
+  const int x = center % W, y = center / W;
   const int min_margin = 6;
   const float depth_diff = pc.P.depth_max - pc.P.depth_min;
   const DpeCamera& camera = pc.cams[0];

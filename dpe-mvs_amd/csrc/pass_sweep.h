@@ -18,52 +18,72 @@
 namespace dpe {
 
 // ------------------------------------------------------------------------------ pixel lists
-// list[k] (k = colour*2 + weak?1:0): pixels of that colour and class inside the red/black grid,
-// in row-major order.  One wave per row; ballot-based compaction keeps the order deterministic.
+// MODE 0: list[k] (k = colour*2 + weak?1:0) = pixels of that colour and class inside the red/black
+//         grid (rows < half_rows), for the sweeps (built after NeigbourUpdate).
+// MODE 1: one list of all WEAK pixels (rows < H), for GenNeighbours (built before it).
+// Row-major order; one wave per row; ballot compaction keeps the order deterministic.
+template <int MODE> DEV int list_rows(const PassConst& pc) { return MODE ? pc.H : pc.half_rows; }
+template <int MODE> DEV int list_key(const PassConst& pc, const DevBufs& B, int x, int y) {
+  const bool wk = B.weak[y * pc.W + x] == DPE_WEAK;
+  if constexpr (MODE == 1) return wk ? 0 : -1;
+  else return (((x + y) & 1) << 1) | (wk ? 1 : 0);
+}
+template <int MODE>
 __global__ void k_list_count(const PassConst* __restrict__ pcp, DevBufs B, int* __restrict__ row_counts) {
+  constexpr int NL = MODE ? 1 : 4;
   const PassConst& pc = *pcp;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int y = blockIdx.x * 4 + wave;
-  if (y >= pc.half_rows) return;
-  int cnt[4] = {0, 0, 0, 0};
+  const int y = blockIdx.x * 4 + wave, rows = list_rows<MODE>(pc);
+  if (y >= rows) return;
+  int cnt[NL];
+  for (int j = 0; j < NL; ++j) cnt[j] = 0;
   for (int x0 = 0; x0 < pc.W; x0 += 64) {
     const int x = x0 + lane;
-    int k = -1;
-    if (x < pc.W) k = (((x + y) & 1) << 1) | (B.weak[y * pc.W + x] == DPE_WEAK ? 1 : 0);
+    const int k = x < pc.W ? list_key<MODE>(pc, B, x, y) : -1;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) cnt[j] += __popcll(__ballot(k == j));
+    for (int j = 0; j < NL; ++j) cnt[j] += __popcll(__ballot(k == j));
   }
   if (lane == 0)
-    for (int j = 0; j < 4; ++j) row_counts[j * pc.half_rows + y] = cnt[j];
+    for (int j = 0; j < NL; ++j) row_counts[j * rows + y] = cnt[j];
 }
-// exclusive scan of the row counts of each list (one workgroup, serial over rows per list)
+// exclusive scan of the row counts of each list: one wave per list, 64 rows per step
+template <int MODE>
 __global__ void k_list_scan(const PassConst* __restrict__ pcp, int* __restrict__ row_counts, int* __restrict__ totals) {
   const PassConst& pc = *pcp;
-  const int j = threadIdx.x;
-  if (j >= 4) return;
+  const int j = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int rows = list_rows<MODE>(pc);
+  if (j >= (MODE ? 1 : 4)) return;
   int acc = 0;
-  for (int y = 0; y < pc.half_rows; ++y) {
-    const int c = row_counts[j * pc.half_rows + y];
-    row_counts[j * pc.half_rows + y] = acc;
-    acc += c;
+  for (int y0 = 0; y0 < rows; y0 += 64) {
+    const int y = y0 + lane;
+    const int c = y < rows ? row_counts[j * rows + y] : 0;
+    int incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int t = __shfl_up(incl, o);
+      if (lane >= o) incl += t;
+    }
+    if (y < rows) row_counts[j * rows + y] = acc + incl - c;
+    acc += __shfl(incl, 63);
   }
-  totals[j] = acc;
+  if (lane == 0) totals[j] = acc;
 }
+template <int MODE>
 __global__ void k_list_fill(const PassConst* __restrict__ pcp, DevBufs B, const int* __restrict__ row_offsets,
                             int* __restrict__ lists, long list_stride) {
+  constexpr int NL = MODE ? 1 : 4;
   const PassConst& pc = *pcp;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int y = blockIdx.x * 4 + wave;
-  if (y >= pc.half_rows) return;
-  int off[4];
-  for (int j = 0; j < 4; ++j) off[j] = row_offsets[j * pc.half_rows + y];
+  const int y = blockIdx.x * 4 + wave, rows = list_rows<MODE>(pc);
+  if (y >= rows) return;
+  int off[NL];
+  for (int j = 0; j < NL; ++j) off[j] = row_offsets[j * rows + y];
   const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   for (int x0 = 0; x0 < pc.W; x0 += 64) {
     const int x = x0 + lane;
-    int k = -1;
-    if (x < pc.W) k = (((x + y) & 1) << 1) | (B.weak[y * pc.W + x] == DPE_WEAK ? 1 : 0);
+    const int k = x < pc.W ? list_key<MODE>(pc, B, x, y) : -1;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < NL; ++j) {
       const unsigned long long m = __ballot(k == j);
       if (k == j) lists[j * list_stride + off[j] + __popcll(m & below)] = y * pc.W + x;
       off[j] += __popcll(m);
