@@ -5,10 +5,13 @@
 //
 // What it restates: csrc/DPE-MVS/DPE.cu (the whole `DPE::RunPatchMatch` pass, :3126-3249, and
 // every kernel / device function it reaches), line by line, in scalar C++.  Each function cites
-// the reference lines it follows.  The reference itself cannot be built here (needs nvcc, CUDA
-// textures, cuRAND, OpenCV — SURVEY.md §8c) and has no tests or golden vectors:
-// parity is pinned by this restatement, by per-function known-answer tests and by invariants
-// (see DESIGN.md "Oracle").
+// the reference lines it follows.
+//
+// PARITY UNPINNED: the reference cannot be built here (needs nvcc, CUDA textures, cuRAND, OpenCV —
+// SURVEY.md §8c) and holds no tests, golden vectors or fixtures for this path, so
+// no reference output pins this restatement.  What pins it: the published Philox4x32-10 KATs
+// (Random123), per-function known-answer / invariant tests (tests/test_oracle_kat.py) and the
+// self-generated golden fixtures that freeze it (tests/golden/).  See DESIGN.md §4.
 //
 // Deliberate, documented restatement choices:
 //  1. Arithmetic primitives are those of oracle_math.h (the reference is --use_fast_math).
