@@ -246,3 +246,52 @@ def first_init_state(scene: dict) -> dict:
     H, W = scene["H"], scene["W"]
     return dict(planes=np.zeros((H, W, 4), np.float32), weak=np.full((H, W), _abi.STRONG, np.uint8),
                 sel=np.zeros((H, W), np.uint32))
+
+
+def _labels_edges_at(sid: np.ndarray, w: int, h: int):
+    """Edges ({0,255} u8) and labels (region id + 1, 0 on edges, i32) of a surface-id map sampled
+    (nearest) at w x h -- the stand-in for EdgeSegment's edges_<s>.dmb / labels_<s>.dmb."""
+    H, W = sid.shape
+    ry = np.minimum(((np.arange(h) + 0.5) * H / h).astype(np.int64), H - 1)
+    rx = np.minimum(((np.arange(w) + 0.5) * W / w).astype(np.int64), W - 1)
+    s = sid[np.ix_(ry, rx)]
+    e = _edges_from_ids(s)
+    return (e * 255).astype(np.uint8), np.where(e, 0, s + 1).astype(np.int32)
+
+
+def write_dense_folder(folder: str, W: int, H: int, n_views: int, seed: int = SCENE_SEED, jpeg_quality: int = 95,
+                       max_src: int = 8) -> dict:
+    """Writes a complete DPE-MVS dense_folder for a synthetic scene: images/%08d.jpg (8-bit grey),
+    cams/%08d_cam.txt (4-number depth line), pair.txt, and per reference image the EdgeSegment
+    outputs DPE/%08d/edges_<s>.dmb and labels_<s>.dmb for every pyramid scale of the schedule."""
+    import os
+    from PIL import Image
+    from . import pipeline
+    sc = make_scene(W, H, n_views, seed=seed)
+    os.makedirs(os.path.join(folder, "images"), exist_ok=True)
+    os.makedirs(os.path.join(folder, "cams"), exist_ok=True)
+    for i, v in enumerate(sc["views"]):
+        Image.fromarray(v["image"].astype(np.uint8), mode="L").save(
+            os.path.join(folder, "images", f"{i:08d}.jpg"), format="JPEG", quality=jpeg_quality)
+        pipeline.write_camera(os.path.join(folder, "cams", f"{i:08d}_cam.txt"), v["K"], v["R"], v["t"],
+                              sc["dmin"], sc["dmax"])
+    with open(os.path.join(folder, "pair.txt"), "w") as f:
+        f.write(f"{n_views}\n")
+        for i in range(n_views):
+            others = sorted((j for j in range(n_views) if j != i), key=lambda j: (abs(j - i), j))[:max_src]
+            f.write(f"{i}\n{len(others)} " + " ".join(f"{j} {100.0 - 5 * abs(i - j):.1f}" for j in others) + "\n")
+    max_size, rounds = max(W, H), 1
+    while max_size > 800:
+        max_size //= 2
+        rounds += 1
+    rounds = max(rounds, 2)
+    for i, v in enumerate(sc["views"]):
+        rf = os.path.join(folder, pipeline.OUT_NAME, f"{i:08d}")
+        os.makedirs(rf, exist_ok=True)
+        for s in range(rounds):
+            f = 1.0 / (1 << s)
+            w, h = pipeline._std_round(np.float32(W) * np.float32(f)), pipeline._std_round(np.float32(H) * np.float32(f))
+            e, lab = _labels_edges_at(v["sid"], w, h)
+            pipeline.write_bin_mat(os.path.join(rf, f"edges_{s}.dmb"), e)
+            pipeline.write_bin_mat(os.path.join(rf, f"labels_{s}.dmb"), lab)
+    return sc
