@@ -13,7 +13,7 @@ import numpy as np
 from . import _abi
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libdpe_mvs.so")
+LIB_PATH = os.environ.get("DPE_MVS_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "libdpe_mvs.so")
 
 EXPORTED = [
     "dpe_params_default", "dpe_create", "dpe_destroy", "dpe_last_error", "dpe_pm_stage",

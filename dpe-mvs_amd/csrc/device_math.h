@@ -88,6 +88,19 @@ DEV double d_exp_d(double x) {
   return p * pow2i_d((int)k);
 }
 
+// Correctly rounded 1/z (== IEEE 1.0f / z, bit for bit) in 3 VALU ops instead of the ~10-op
+// div_scale/div_fmas/div_fixup sequence: v_rcp_f32 + one FMA Newton step.  Verified exhaustively on
+// gfx950 for every float whose biased exponent is in [1, 252], both signs (tools/rcp_check.hip,
+// tests/test_gpu_rcp.py).  Callers must guarantee that range (see rcp_range_ok); outside it (zero,
+// denormals, |z| >= 2^126, inf, NaN) only the IEEE division is exact.
+DEV float d_rcp_fast(float z) {
+  const float r = __builtin_amdgcn_rcpf(z);
+  return __builtin_fmaf(__builtin_fmaf(-z, r, 1.0f), r, r);
+}
+template <bool FAST> DEV float rcp_sel(float z) {
+  if constexpr (FAST) return d_rcp_fast(z);
+  else return 1.0f / z;
+}
 DEV float d_rsqrtf(float x) { return 1.0f / __builtin_sqrtf(x); }
 
 // float -> int with cvt.rzi.s32 semantics (saturating, NaN -> 0): written explicitly so the

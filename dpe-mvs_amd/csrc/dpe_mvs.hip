@@ -70,7 +70,7 @@ struct DpeContext {
   // inputs
   DevArr<float> img_plain[DPE_MAX_IMAGES];  // plain f32 images (ref used directly)
   DevArr<float4> imgq[DPE_MAX_IMAGES];
-  DevArr<uint32_t> imgq8[DPE_MAX_IMAGES];
+  DevArr<uint32_t> imgq8_all;        // all u8 quad images, one allocation (32-bit tap offsets)
   bool img8 = false;                 // all images are 8-bit grey levels -> u8 quad layout
   DevArr<float> depth[DPE_MAX_IMAGES];
   DevArr<uint8_t> edge, edge_low;
@@ -146,7 +146,8 @@ void dpe_destroy(DpeContext* c) {
   hipStreamSynchronize(c->stream);
   for (auto& e : c->ev) hipEventDestroy(e);
   c->dc.release();
-  for (int i = 0; i < DPE_MAX_IMAGES; ++i) { c->img_plain[i].release(); c->imgq[i].release(); c->imgq8[i].release(); c->depth[i].release(); }
+  for (int i = 0; i < DPE_MAX_IMAGES; ++i) { c->img_plain[i].release(); c->imgq[i].release(); c->depth[i].release(); }
+  c->imgq8_all.release();
   c->edge.release(); c->edge_low.release(); c->label.release();
   c->planes0.release(); c->weak0.release(); c->sel0.release();
   c->planes.release(); c->planes_snap.release(); c->fit_plane.release();
@@ -267,9 +268,13 @@ extern "C" int dpe_pm_stage(DpeContext* c, const DpePassInput* in, const DpePass
     HIPC(c->img_plain[i].ensure(L));
     HIPC(hipMemcpyAsync(c->img_plain[i].p, in->images[i], L * sizeof(float), hipMemcpyHostToDevice, c->stream));
     if (img8) {
-      HIPC(c->imgq8[i].ensure((size_t)(W + 2) * (H + 2)));
-      k_build_quad8<<<qg, qb, 0, c->stream>>>(c->img_plain[i].p, c->imgq8[i].p, W, H);
-      B.imgq8[i] = c->imgq8[i].p;
+      const size_t plane = (size_t)(W + 2) * (H + 2);
+      HIPC(c->imgq8_all.ensure(plane * N));
+      uint32_t* q8 = c->imgq8_all.p + plane * i;
+      k_build_quad8<<<qg, qb, 0, c->stream>>>(c->img_plain[i].p, q8, W, H);
+      B.imgq8[i] = q8;
+      B.img8 = (const uint8_t*)c->imgq8_all.p;
+      B.img8_view = (uint32_t)(plane * 4);
     } else {
       HIPC(c->imgq[i].ensure((size_t)(W + 2) * (H + 2)));
       k_build_quad<<<qg, qb, 0, c->stream>>>(c->img_plain[i].p, c->imgq[i].p, W, H);

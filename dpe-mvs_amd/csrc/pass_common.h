@@ -37,6 +37,8 @@ struct PassConst {
 struct DevBufs {
   const float4* imgq[DPE_MAX_IMAGES];     // f32 quad-texel images (any grey levels)
   const uint32_t* imgq8[DPE_MAX_IMAGES];  // u8 quad-texel images (8-bit grey levels: same values, 4 B/tap)
+  const uint8_t* img8;                    // == imgq8[0]: all u8 quad images in one allocation,
+  uint32_t img8_view;                     //   view v at byte offset v * img8_view (< 4 GiB: 32-bit offsets)
   const float* depth[DPE_MAX_IMAGES];
   const float* ref;
   float4* planes; float4* planes_snap; float4* fit_plane;
@@ -195,6 +197,26 @@ DEV float2 project_h(const Homog& H, float x, float y) {   // ComputeCorrespondi
   return make_float2(px * iz, py * iz);
 }
 
+// True when every tap (x, y) of the rectangle [x0, x1] x [y0, y1] computes its projective
+// denominator qz = fma(h7, y, fma(h6, x, h8)) with a biased exponent in [1, 252], so the 3-op
+// d_rcp_fast(qz) is bit-identical to 1.0f / qz.  qz is affine in (x, y): its exact values over the
+// rectangle lie between the four corner values (evaluated here with the taps' own formula), and
+// a tap's computed value is within 2^-22 * max(|bz|, |qz|) of the exact one.  Same sign at the
+// corners, a minimum magnitude well above that error and above 2^-100, and magnitudes below 2^100
+// give the range with a wide margin.  NaN/inf anywhere -> false.
+DEV bool rcp_range_ok(const Homog& H, float x0, float x1, float y0, float y1) {
+  const float b0 = __builtin_fmaf(H.h[6], x0, H.h[8]), b1 = __builtin_fmaf(H.h[6], x1, H.h[8]);
+  const float q00 = __builtin_fmaf(H.h[7], y0, b0), q01 = __builtin_fmaf(H.h[7], y1, b0);
+  const float q10 = __builtin_fmaf(H.h[7], y0, b1), q11 = __builtin_fmaf(H.h[7], y1, b1);
+  const float mn = __builtin_fminf(__builtin_fminf(q00, q01), __builtin_fminf(q10, q11));
+  const float mx = __builtin_fmaxf(__builtin_fmaxf(q00, q01), __builtin_fmaxf(q10, q11));
+  const float amax = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(b0), __builtin_fabsf(b1)),
+                                     __builtin_fmaxf(__builtin_fabsf(mn), __builtin_fabsf(mx)));
+  const float lo = mn > 0.0f ? mn : -mx;
+  return (mn > 0.0f || mx < 0.0f) && lo > amax * 9.5367431640625e-07f && lo > 7.888609052210118e-31f &&
+         amax < 1.2676506002282294e+30f;
+}
+
 // ------------------------------------------------------------------------------ sampling
 DEV float ref_texel(const float* ref, int W, int H, int x, int y) {
   x = x < 0 ? 0 : (x > W - 1 ? W - 1 : x);
@@ -230,6 +252,45 @@ DEV float sample_quad8(const uint32_t* __restrict__ q, int W, int H, float sx, f
   const float r1 = __builtin_fmaf(ax, t11 - t01, t01);
   return __builtin_fmaf(ay, r1 - r0, r0);
 }
+// Minimum waves per SIMD the tap-heavy kernels are compiled for (register cap 512 / waves).
+#ifndef DPE_TAP_WAVES
+#define DPE_TAP_WAVES 4
+#endif
+// 1: unroll the 6 rows of the 36-tap patch loop (more ILP, more registers)
+#ifndef DPE_UNROLL_ROWS
+#define DPE_UNROLL_ROWS 1
+#endif
+// 1: the u8 fast tap uses packed FP32 / med3 / one-base 32-bit offsets (tap_u8_fast)
+#ifndef DPE_PACKED_TAP
+#define DPE_PACKED_TAP 1
+#endif
+
+typedef float f2v __attribute__((ext_vector_type(2)));
+DEV f2v f2s(float a) { return (f2v){a, a}; }
+DEV f2v fma2(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
+
+// One bilinear tap of the u8 quad image whose byte offset is `vofs`, at the projection of the tap
+// (row terms bxy = (h0 x + h2, h3 x + h5), bz = h6 x + h8; column yf).  Bit-identical to
+// sample_quad8(project) when the tap's qz is in d_rcp_fast's exact range (rcp_range_ok), with
+// packed FP32 ops, one med3 per clamp and a 32-bit offset from one uniform base.
+DEV float tap_u8_fast(const DevBufs& B, uint32_t vofs, uint32_t stride, f2v lim, const float* h, f2v bxy, float bz,
+                      float yf) {
+  const f2v q = fma2((f2v){h[1], h[4]}, f2s(yf), bxy);
+  const float iz = d_rcp_fast(__builtin_fmaf(h[7], yf, bz));
+  const f2v sxy = q * f2s(iz);
+  const float xb = __builtin_amdgcn_fmed3f(sxy.x, -1.0f, lim.x);
+  const float yb = __builtin_amdgcn_fmed3f(sxy.y, -1.0f, lim.y);
+  const f2v u = fma2((f2v){xb, yb}, f2s(256.0f), f2s(256.5f));
+  const uint32_t ux = (uint32_t)(int)u.x, uy = (uint32_t)(int)u.y;       // >= 0 after the clamp
+  const uint32_t t = *(const uint32_t*)(B.img8 + (vofs + (__umul24(uy >> 8, stride) + (ux >> 8)) * 4u));
+  const float ax = (float)(ux & 255u) * 0.00390625f;
+  const float ay = (float)(uy & 255u) * 0.00390625f;
+  const f2v lo = (f2v){(float)(t & 255u), (float)((t >> 16) & 255u)};
+  const f2v hi = (f2v){(float)((t >> 8) & 255u), (float)(t >> 24)};
+  const f2v r = fma2(f2s(ax), hi - lo, lo);
+  return __builtin_fmaf(ay, r.y - r.x, r.x);
+}
+
 template <bool U8> DEV float sample_src(const DevBufs& B, int v, int W, int H, float sx, float sy) {
   if constexpr (U8) return sample_quad8(B.imgq8[v], W, H, sx, sy);
   else return sample_quad(B.imgq[v], W, H, sx, sy);
@@ -260,20 +321,27 @@ DEV float ncc_finalize(float s_ref, float s_rr, float s_w, float s_src, float s_
 
 // Generic bilateral NCC of one patch, weights computed per tap (NCC-New neighbour patches and
 // non-default radius/increment).  Same arithmetic order as the oracle's PatchNCC.
-template <bool U8>
-DEV float patch_ncc_generic(const PassConst& pc, const DevBufs& B, int v, const Homog& H,
-                            int cx, int cy, float rcp, int radius, int increment) {
+template <bool U8, bool FAST>
+DEV void generic_taps(const PassConst& pc, const DevBufs& B, int v, const Homog& H, int cx, int cy, float rcp,
+                      int radius, int increment, float* acc) {
   const int W = pc.W, Hh = pc.H;
   const float ss = pc.P.sigma_spatial, sc = pc.P.sigma_color;
   float s_ref = 0, s_rr = 0, s_src = 0, s_ss = 0, s_rs = 0, s_w = 0;
   for (int i = -radius; i <= radius; i += increment) {
     float r_ref = 0, r_src = 0, r_rr = 0, r_ss = 0, r_rs = 0, r_w = 0;
     const int x = cx + i;
+    const float xf = (float)x;
+    const float bx = __builtin_fmaf(H.h[0], xf, H.h[2]);
+    const float by = __builtin_fmaf(H.h[3], xf, H.h[5]);
+    const float bz = __builtin_fmaf(H.h[6], xf, H.h[8]);
     for (int j = -radius; j <= radius; j += increment) {
       const int y = cy + j;
       const float rp = ref_texel(B.ref, W, Hh, x, y);
-      const float2 sp_ = project_h(H, (float)x, (float)y);
-      const float sp = sample_src<U8>(B, v, W, Hh, sp_.x, sp_.y);
+      const float yf = (float)y;
+      const float qx = __builtin_fmaf(H.h[1], yf, bx);
+      const float qy = __builtin_fmaf(H.h[4], yf, by);
+      const float iz = rcp_sel<FAST>(__builtin_fmaf(H.h[7], yf, bz));
+      const float sp = sample_src<U8>(B, v, W, Hh, qx * iz, qy * iz);
       const float w = bilateral_weight(i, j, rp, rcp, ss, sc);
       const float wr = w * rp;
       r_ref = r_ref + wr;
@@ -286,8 +354,21 @@ DEV float patch_ncc_generic(const PassConst& pc, const DevBufs& B, int v, const 
     }
     s_ref += r_ref; s_rr += r_rr; s_src += r_src; s_ss += r_ss; s_rs += r_rs; s_w += r_w;
   }
+  acc[0] = s_ref; acc[1] = s_rr; acc[2] = s_src; acc[3] = s_ss; acc[4] = s_rs; acc[5] = s_w;
+}
+
+// Generic bilateral NCC of one patch, weights computed per tap (NCC-New neighbour patches and
+// non-default radius/increment).  Same arithmetic order as the oracle's PatchNCC.
+template <bool U8>
+DEV float patch_ncc_generic(const PassConst& pc, const DevBufs& B, int v, const Homog& H,
+                            int cx, int cy, float rcp, int radius, int increment) {
+  float a[6];
+  if (rcp_range_ok(H, (float)(cx - radius), (float)(cx + radius), (float)(cy - radius), (float)(cy + radius)))
+    generic_taps<U8, true>(pc, B, v, H, cx, cy, rcp, radius, increment, a);
+  else
+    generic_taps<U8, false>(pc, B, v, H, cx, cy, rcp, radius, increment, a);
   if (B.cnt) { const unsigned long long n = (unsigned long long)(2 * radius / increment + 1); count_work(B, 0, n * n); }
-  return ncc_finalize(s_ref, s_rr, s_w, s_src, s_ss, s_rs);
+  return ncc_finalize(a[0], a[1], a[5], a[2], a[3], a[4]);
 }
 
 DEV bool center_outside(const PassConst& pc, int v, const Homog& H, int px, int py) {
@@ -339,11 +420,8 @@ DEV void make_patch36(Patch36& P, const PassConst& pc, const DevBufs& B, int px,
   }
   P.s_ref = s_ref; P.s_rr = s_rr; P.s_w = s_w;
 }
-template <bool U8>
-DEV float ncc_old_patch36(const Patch36& P, const PassConst& pc, const DevBufs& B, int v, const float4& pl) {
-  const Homog H = make_homography(pc, v, pl);
-  if (center_outside(pc, v, H, P.px, P.py)) { count_work(B, 1, 0); return 2.0f; }
-  count_work(B, 1, 36);
+template <bool U8, bool FAST>
+DEV void patch36_taps(const Patch36& P, const PassConst& pc, const DevBufs& B, int v, const Homog& H, float* acc) {
   const int W = pc.W, Hh = pc.H;
   float s_src = 0, s_ss = 0, s_rs = 0;
 #pragma unroll
@@ -358,8 +436,7 @@ DEV float ncc_old_patch36(const Patch36& P, const PassConst& pc, const DevBufs& 
       const float y = (float)(P.py - 5 + 2 * b);
       const float qx = __builtin_fmaf(H.h[1], y, bx);
       const float qy = __builtin_fmaf(H.h[4], y, by);
-      const float qz = __builtin_fmaf(H.h[7], y, bz);
-      const float iz = 1.0f / qz;
+      const float iz = rcp_sel<FAST>(__builtin_fmaf(H.h[7], y, bz));
       const float sp = sample_src<U8>(B, v, W, Hh, qx * iz, qy * iz);
       const float w = P.w[a * 6 + b], wr = P.wr[a * 6 + b];
       r_src = __builtin_fmaf(w, sp, r_src);
@@ -369,7 +446,19 @@ DEV float ncc_old_patch36(const Patch36& P, const PassConst& pc, const DevBufs& 
     }
     s_src += r_src; s_ss += r_ss; s_rs += r_rs;
   }
-  return ncc_finalize(P.s_ref, P.s_rr, P.s_w, s_src, s_ss, s_rs);
+  acc[0] = s_src; acc[1] = s_ss; acc[2] = s_rs;
+}
+template <bool U8>
+DEV float ncc_old_patch36(const Patch36& P, const PassConst& pc, const DevBufs& B, int v, const float4& pl) {
+  const Homog H = make_homography(pc, v, pl);
+  if (center_outside(pc, v, H, P.px, P.py)) { count_work(B, 1, 0); return 2.0f; }
+  count_work(B, 1, 36);
+  float a[3];
+  if (rcp_range_ok(H, (float)(P.px - 5), (float)(P.px + 5), (float)(P.py - 5), (float)(P.py + 5)))
+    patch36_taps<U8, true>(P, pc, B, v, H, a);
+  else
+    patch36_taps<U8, false>(P, pc, B, v, H, a);
+  return ncc_finalize(P.s_ref, P.s_rr, P.s_w, a[0], a[1], a[2]);
 }
 
 // Old NCC through the cached patch when the pass uses the default 5/2 patch, else generic.

@@ -19,7 +19,7 @@ DEV void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// 36-tap reference patch in LDS: w[36], wr[36], rp[36] (grey level) for pixel (px, py).
+// 36-tap reference patch in LDS: (w, w*grey) pairs [36][2], then rp[36] (grey level), pixel (px, py).
 // Lane `t` of the group computes taps t, t+stride, ...
 DEV void patch_lds_build(float* pw, const PassConst& pc, const DevBufs& B, int px, int py, int t, int stride) {
   const float rc = ref_texel(B.ref, pc.W, pc.H, px, py);
@@ -27,8 +27,8 @@ DEV void patch_lds_build(float* pw, const PassConst& pc, const DevBufs& B, int p
     const int i = -5 + 2 * (k / 6), j = -5 + 2 * (k % 6);
     const float rp = ref_texel(B.ref, pc.W, pc.H, px + i, py + j);
     const float w = bilateral_weight(i, j, rp, rc, pc.P.sigma_spatial, pc.P.sigma_color);
-    pw[k] = w;
-    pw[36 + k] = w * rp;
+    pw[2 * k] = w;
+    pw[2 * k + 1] = w * rp;
     pw[72 + k] = rp;
   }
 }
@@ -40,7 +40,7 @@ DEV void patch_lds_sums(const float* pw, float& s_ref, float& s_rr, float& s_w) 
     float r_ref = 0, r_rr = 0, r_w = 0;
 #pragma unroll
     for (int b = 0; b < 6; ++b) {
-      const float w = pw[a * 6 + b], wr = pw[36 + a * 6 + b], rp = pw[72 + a * 6 + b];
+      const float w = pw[2 * (a * 6 + b)], wr = pw[2 * (a * 6 + b) + 1], rp = pw[72 + a * 6 + b];
       r_ref = r_ref + wr;
       r_rr = __builtin_fmaf(wr, rp, r_rr);
       r_w = r_w + w;
@@ -50,38 +50,78 @@ DEV void patch_lds_sums(const float* pw, float& s_ref, float& s_rr, float& s_w) 
   s_ref = a_ref; s_rr = a_rr; s_w = a_w;
 }
 // Old NCC with the patch read from LDS (same arithmetic as ncc_old_patch36)
+template <bool U8, bool FAST>
+DEV void lds_taps(const float* pw, int px, int py, const PassConst& pc, const DevBufs& B, int v, const Homog& H,
+                  float* acc) {
+  const int W = pc.W, Hh = pc.H;
+  if constexpr (U8 && FAST && DPE_PACKED_TAP) {
+    // packed form: (r_src, r_rs) accumulate as one pair; weights are (w, w*grey) pairs in LDS
+    const uint32_t vofs = (uint32_t)v * B.img8_view, stride = (uint32_t)(W + 2);
+    const f2v lim = (f2v){(float)W, (float)Hh};
+    const f2v* wp = (const f2v*)pw;
+    f2v s_sr = f2s(0.0f);
+    float s_ss = 0;
+#if DPE_UNROLL_ROWS
+#pragma unroll
+#else
+#pragma unroll 1
+#endif
+    for (int a = 0; a < 6; ++a) {
+      const float x = (float)(px - 5 + 2 * a);
+      const f2v bxy = fma2((f2v){H.h[0], H.h[3]}, f2s(x), (f2v){H.h[2], H.h[5]});
+      const float bz = __builtin_fmaf(H.h[6], x, H.h[8]);
+      f2v r_sr = f2s(0.0f);
+      float r_ss = 0;
+#pragma unroll
+      for (int b = 0; b < 6; ++b) {
+        const float sp = tap_u8_fast(B, vofs, stride, lim, H.h, bxy, bz, (float)(py - 5 + 2 * b));
+        const f2v w = wp[a * 6 + b];
+        r_sr = fma2(w, f2s(sp), r_sr);
+        const float ws = w.x * sp;
+        r_ss = __builtin_fmaf(ws, sp, r_ss);
+      }
+      s_sr += r_sr; s_ss += r_ss;
+    }
+    acc[0] = s_sr.x; acc[1] = s_ss; acc[2] = s_sr.y;
+  } else {
+    float s_src = 0, s_ss = 0, s_rs = 0;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+      const float x = (float)(px - 5 + 2 * a);
+      const float bx = __builtin_fmaf(H.h[0], x, H.h[2]);
+      const float by = __builtin_fmaf(H.h[3], x, H.h[5]);
+      const float bz = __builtin_fmaf(H.h[6], x, H.h[8]);
+      float r_src = 0, r_ss = 0, r_rs = 0;
+#pragma unroll
+      for (int b = 0; b < 6; ++b) {
+        const float y = (float)(py - 5 + 2 * b);
+        const float qx = __builtin_fmaf(H.h[1], y, bx);
+        const float qy = __builtin_fmaf(H.h[4], y, by);
+        const float iz = rcp_sel<FAST>(__builtin_fmaf(H.h[7], y, bz));
+        const float sp = sample_src<U8>(B, v, W, Hh, qx * iz, qy * iz);
+        const float w = pw[2 * (a * 6 + b)], wr = pw[2 * (a * 6 + b) + 1];
+        r_src = __builtin_fmaf(w, sp, r_src);
+        const float ws = w * sp;
+        r_ss = __builtin_fmaf(ws, sp, r_ss);
+        r_rs = __builtin_fmaf(wr, sp, r_rs);
+      }
+      s_src += r_src; s_ss += r_ss; s_rs += r_rs;
+    }
+    acc[0] = s_src; acc[1] = s_ss; acc[2] = s_rs;
+  }
+}
 template <bool U8>
 DEV float ncc_old_lds(const float* pw, float s_ref, float s_rr, float s_w, int px, int py, const PassConst& pc,
                       const DevBufs& B, int v, const float4& pl) {
   const Homog H = make_homography(pc, v, pl);
   if (center_outside(pc, v, H, px, py)) { count_work(B, 1, 0); return 2.0f; }
   count_work(B, 1, 36);
-  const int W = pc.W, Hh = pc.H;
-  float s_src = 0, s_ss = 0, s_rs = 0;
-#pragma unroll
-  for (int a = 0; a < 6; ++a) {
-    const float x = (float)(px - 5 + 2 * a);
-    const float bx = __builtin_fmaf(H.h[0], x, H.h[2]);
-    const float by = __builtin_fmaf(H.h[3], x, H.h[5]);
-    const float bz = __builtin_fmaf(H.h[6], x, H.h[8]);
-    float r_src = 0, r_ss = 0, r_rs = 0;
-#pragma unroll
-    for (int b = 0; b < 6; ++b) {
-      const float y = (float)(py - 5 + 2 * b);
-      const float qx = __builtin_fmaf(H.h[1], y, bx);
-      const float qy = __builtin_fmaf(H.h[4], y, by);
-      const float qz = __builtin_fmaf(H.h[7], y, bz);
-      const float iz = 1.0f / qz;
-      const float sp = sample_src<U8>(B, v, W, Hh, qx * iz, qy * iz);
-      const float w = pw[a * 6 + b], wr = pw[36 + a * 6 + b];
-      r_src = __builtin_fmaf(w, sp, r_src);
-      const float ws = w * sp;
-      r_ss = __builtin_fmaf(ws, sp, r_ss);
-      r_rs = __builtin_fmaf(wr, sp, r_rs);
-    }
-    s_src += r_src; s_ss += r_ss; s_rs += r_rs;
-  }
-  return ncc_finalize(s_ref, s_rr, s_w, s_src, s_ss, s_rs);
+  float a[3];
+  if (rcp_range_ok(H, (float)(px - 5), (float)(px + 5), (float)(py - 5), (float)(py + 5)))
+    lds_taps<U8, true>(pw, px, py, pc, B, v, H, a);
+  else
+    lds_taps<U8, false>(pw, px, py, pc, B, v, H, a);
+  return ncc_finalize(s_ref, s_rr, s_w, a[0], a[1], a[2]);
 }
 
 template <bool U8>
@@ -112,7 +152,7 @@ DEV void baseline_and_weights(const PassConst& pc, uint32_t sel, const uint8_t* 
 // ------------------------------------------------------------------------------ DepthToWeak
 // grid: one wave per pixel, 4 waves per 256-thread workgroup.
 template <bool U8>
-__global__ void __launch_bounds__(256) k_depth_to_weak(const PassConst* __restrict__ pcp, DevBufs B) {   // DPE.cu:2593-2747
+__global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_depth_to_weak(const PassConst* __restrict__ pcp, DevBufs B) {   // DPE.cu:2593-2747
   __shared__ float s_patch[4][108];
   __shared__ float s_pc[4][64];
   const PassConst& pc = *pcp;
@@ -198,7 +238,7 @@ __global__ void __launch_bounds__(256) k_depth_to_weak(const PassConst* __restri
 // grid: five pixels per wave (12 lanes each: lanes 0..10 = hypotheses -5..5, lane 11 = cost at
 // the current depth), 4 waves per 256-thread workgroup.
 template <bool U8>
-__global__ void __launch_bounds__(256) k_local_refine(const PassConst* __restrict__ pcp, DevBufs B) {   // DPE.cu:2749-2835
+__global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_local_refine(const PassConst* __restrict__ pcp, DevBufs B) {   // DPE.cu:2749-2835
   __shared__ float s_patch[4][5][108];
   __shared__ float s_tc[4][5][12];
   const PassConst& pc = *pcp;

@@ -240,7 +240,7 @@ __host__ __device__ inline int strong_lds_per_wave(int P, int C, int nv) {
 }
 
 template <bool U8, bool EDGE>
-__global__ void __launch_bounds__(256) k_strong_coop(const PassConst* __restrict__ pcp, DevBufs B, int iter,
+__global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_strong_coop(const PassConst* __restrict__ pcp, DevBufs B, int iter,
                                                      const int* __restrict__ list, const int* __restrict__ nlist_p) {
   extern __shared__ float4 lds4[];
   float* lds = (float*)lds4;
@@ -450,8 +450,8 @@ __global__ void __launch_bounds__(256) k_strong_coop(const PassConst* __restrict
 // plane- and view-independent, so they are tabulated once per pixel in LDS together with the
 // reference sums of each patch; an NCC job is then projection + bilinear fetch + 3 FMAs per tap.
 struct WeakTab {
-  const float* tcw; const float* tcwr;    // centre patch  w[n_c^2], w*grey[n_c^2]
-  const float* tnw; const float* tnwr;    // neighbour k=1..8: [(k-1)*9 + t]
+  const float* tc;                        // centre patch (w, w*grey) pairs [n_c^2][2]
+  const float* tn;                        // neighbour k=1..8: pairs at [((k-1)*9 + t)*2]
   const float* sums;                      // [9][3]: s_ref, s_rr, s_w of each tabulated patch
   const short2* nbl;                      // [9] neighbour pixels (nb[0] = the pixel itself)
   const uint32_t* nsv;                    // [9] selected_views of the neighbours
@@ -461,34 +461,67 @@ struct WeakTab {
 };
 
 // patch NCC with tabulated weights; the same tap order and arithmetic as patch_ncc_generic
+template <bool U8, bool FAST>
+DEV void tab_taps(const PassConst& pc, const DevBufs& B, int v, const Homog& H, int cx, int cy, int rad, int inc,
+                  int n, const float* __restrict__ tw, float* acc) {
+  const int W = pc.W, Hh = pc.H;
+  const f2v* wp = (const f2v*)tw;            // (w, w*grey) pairs
+  if constexpr (U8 && FAST && DPE_PACKED_TAP) {
+    const uint32_t vofs = (uint32_t)v * B.img8_view, stride = (uint32_t)(W + 2);
+    const f2v lim = (f2v){(float)W, (float)Hh};
+    f2v s_sr = f2s(0.0f);
+    float s_ss = 0;
+    for (int a = 0; a < n; ++a) {
+      const float xf = (float)(cx - rad + a * inc);
+      const f2v bxy = fma2((f2v){H.h[0], H.h[3]}, f2s(xf), (f2v){H.h[2], H.h[5]});
+      const float bz = __builtin_fmaf(H.h[6], xf, H.h[8]);
+      f2v r_sr = f2s(0.0f);
+      float r_ss = 0;
+      for (int b = 0; b < n; ++b) {
+        const float sp = tap_u8_fast(B, vofs, stride, lim, H.h, bxy, bz, (float)(cy - rad + b * inc));
+        const f2v w = wp[a * n + b];
+        r_sr = fma2(w, f2s(sp), r_sr);
+        const float ws = w.x * sp;
+        r_ss = __builtin_fmaf(ws, sp, r_ss);
+      }
+      s_sr += r_sr; s_ss += r_ss;
+    }
+    acc[0] = s_sr.x; acc[1] = s_ss; acc[2] = s_sr.y;
+  } else {
+    float s_src = 0, s_ss = 0, s_rs = 0;
+    for (int a = 0; a < n; ++a) {
+      const float xf = (float)(cx - rad + a * inc);
+      const float bx = __builtin_fmaf(H.h[0], xf, H.h[2]);
+      const float by = __builtin_fmaf(H.h[3], xf, H.h[5]);
+      const float bz = __builtin_fmaf(H.h[6], xf, H.h[8]);
+      float r_src = 0, r_ss = 0, r_rs = 0;
+      for (int b = 0; b < n; ++b) {
+        const float yf = (float)(cy - rad + b * inc);
+        const float qx = __builtin_fmaf(H.h[1], yf, bx);
+        const float qy = __builtin_fmaf(H.h[4], yf, by);
+        const float iz = rcp_sel<FAST>(__builtin_fmaf(H.h[7], yf, bz));
+        const float sp = sample_src<U8>(B, v, W, Hh, qx * iz, qy * iz);
+        const f2v w = wp[a * n + b];
+        r_src = __builtin_fmaf(w.x, sp, r_src);
+        const float ws = w.x * sp;
+        r_ss = __builtin_fmaf(ws, sp, r_ss);
+        r_rs = __builtin_fmaf(w.y, sp, r_rs);
+      }
+      s_src += r_src; s_ss += r_ss; s_rs += r_rs;
+    }
+    acc[0] = s_src; acc[1] = s_ss; acc[2] = s_rs;
+  }
+}
 template <bool U8>
 DEV float patch_ncc_tab(const PassConst& pc, const DevBufs& B, int v, const Homog& H, int cx, int cy, int rad, int inc,
-                        int n, const float* __restrict__ tw, const float* __restrict__ twr, const float* sm) {
-  const int W = pc.W, Hh = pc.H;
-  float s_src = 0, s_ss = 0, s_rs = 0;
-  for (int a = 0; a < n; ++a) {
-    const float xf = (float)(cx - rad + a * inc);
-    const float bx = __builtin_fmaf(H.h[0], xf, H.h[2]);
-    const float by = __builtin_fmaf(H.h[3], xf, H.h[5]);
-    const float bz = __builtin_fmaf(H.h[6], xf, H.h[8]);
-    float r_src = 0, r_ss = 0, r_rs = 0;
-    for (int b = 0; b < n; ++b) {
-      const float yf = (float)(cy - rad + b * inc);
-      const float qx = __builtin_fmaf(H.h[1], yf, bx);
-      const float qy = __builtin_fmaf(H.h[4], yf, by);
-      const float qz = __builtin_fmaf(H.h[7], yf, bz);
-      const float iz = 1.0f / qz;
-      const float sp = sample_src<U8>(B, v, W, Hh, qx * iz, qy * iz);
-      const float w = tw[a * n + b], wr = twr[a * n + b];
-      r_src = __builtin_fmaf(w, sp, r_src);
-      const float ws = w * sp;
-      r_ss = __builtin_fmaf(ws, sp, r_ss);
-      r_rs = __builtin_fmaf(wr, sp, r_rs);
-    }
-    s_src += r_src; s_ss += r_ss; s_rs += r_rs;
-  }
+                        int n, const float* __restrict__ tw, const float* sm) {
+  float a[3];
+  if (rcp_range_ok(H, (float)(cx - rad), (float)(cx + rad), (float)(cy - rad), (float)(cy + rad)))
+    tab_taps<U8, true>(pc, B, v, H, cx, cy, rad, inc, n, tw, a);
+  else
+    tab_taps<U8, false>(pc, B, v, H, cx, cy, rad, inc, n, tw, a);
   count_work(B, 0, (unsigned long long)(n * n));
-  return ncc_finalize(sm[0], sm[1], sm[2], s_src, s_ss, s_rs);
+  return ncc_finalize(sm[0], sm[1], sm[2], a[0], a[1], a[2]);
 }
 
 // ComputeBilateralNCCNew (DPE.cu:557-690) of the tabulated weak pixel (px, py)
@@ -513,12 +546,12 @@ DEV float ncc_new_tab(const PassConst& pc, const DevBufs& B, const WeakTab& T, i
     }
     float tc;
     if (k == 0) {
-      tc = T.tab_c ? patch_ncc_tab<U8>(pc, B, v, H, np.x, np.y, T.rad_c, T.inc_c, T.n_c, T.tcw, T.tcwr, T.sums)
+      tc = T.tab_c ? patch_ncc_tab<U8>(pc, B, v, H, np.x, np.y, T.rad_c, T.inc_c, T.n_c, T.tc, T.sums)
                    : patch_ncc_generic<U8>(pc, B, v, H, np.x, np.y, T.rc, T.rad_c, T.inc_c);
       center_cost = tc;
     } else {
-      tc = T.tab_n ? patch_ncc_tab<U8>(pc, B, v, H, np.x, np.y, T.rad_n, T.inc_n, T.n_n, T.tnw + (k - 1) * 9,
-                                       T.tnwr + (k - 1) * 9, T.sums + 3 * k)
+      tc = T.tab_n ? patch_ncc_tab<U8>(pc, B, v, H, np.x, np.y, T.rad_n, T.inc_n, T.n_n, T.tn + (k - 1) * 18,
+                                       T.sums + 3 * k)
                    : patch_ncc_generic<U8>(pc, B, v, H, np.x, np.y, T.rc, T.rad_n, T.inc_n);
       strong_cost += tc; strong_count++;
     }
@@ -535,7 +568,7 @@ __host__ __device__ inline int weak_lds_per_pixel(int nv) { return (480 + 17 * n
 // CheckerboardPropagationWeak (DPE.cu:1668-1862) + PlaneHypothesisRefinementWeak (:1120-1212).
 // C lanes per pixel, 64/C pixels per wave, blockDim.x/64 waves per workgroup.
 template <bool U8, int C>
-__global__ void __launch_bounds__(256) k_weak_coop(const PassConst* __restrict__ pcp, DevBufs B, int iter,
+__global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassConst* __restrict__ pcp, DevBufs B, int iter,
                                                    const int* __restrict__ list, const int* __restrict__ nlist_p) {
   extern __shared__ float4 lds4[];
   constexpr int P = 64 / C;
@@ -556,8 +589,8 @@ __global__ void __launch_bounds__(256) k_weak_coop(const PassConst* __restrict__
   const int S = weak_lds_per_pixel(nv);
   float* pb = (float*)lds4 + (size_t)(wave * P + ps) * S;
   float* pw = pb;                                        // [108] Old-NCC patch (patch_lds_build)
-  float* tcw = pb + 108; float* tcwr = pb + 144;         // centre patch table
-  float* tnw = pb + 180; float* tnwr = pb + 252;         // neighbour patch tables [8][9]
+  float* tcp = pb + 108;                                 // centre patch table, pairs [36][2]
+  float* tnp = pb + 180;                                 // neighbour patch tables, pairs [8][9][2]
   float* sums = pb + 324;                                // [9][3]
   float* osum = pb + 352;                                // [3] Old-NCC patch sums
   float4* cpl = (float4*)(pb + 356);                     // [8] candidate planes
@@ -585,7 +618,7 @@ __global__ void __launch_bounds__(256) k_weak_coop(const PassConst* __restrict__
   T.tab_c = T.n_c >= 1 && T.n_c <= 6;
   T.tab_n = T.n_n >= 1 && T.n_n <= 3;
   T.rc = active ? ref_texel(B.ref, W, Hh, x, y) : 0.0f;
-  T.tcw = tcw; T.tcwr = tcwr; T.tnw = tnw; T.tnwr = tnwr; T.sums = sums; T.nbl = nbl; T.nsv = nsv;
+  T.tc = tcp; T.tn = tnp; T.sums = sums; T.nbl = nbl; T.nsv = nsv;
   const short2* nbg = B.nb + (size_t)center * 9;
 
   // ---- phase 1: neighbours, weight tables, Old-NCC patch, candidate rows
@@ -607,8 +640,8 @@ __global__ void __launch_bounds__(256) k_weak_coop(const PassConst* __restrict__
       const int i = -rad + (tt / n) * inc, j = -rad + (tt % n) * inc;
       const float rp = ref_texel(B.ref, W, Hh, np.x + i, np.y + j);
       const float w = bilateral_weight(i, j, rp, T.rc, ss, sc);
-      if (k == 0) { tcw[tt] = w; tcwr[tt] = w * rp; }
-      else { tnw[(k - 1) * 9 + tt] = w; tnwr[(k - 1) * 9 + tt] = w * rp; }
+      float* dst = k == 0 ? tcp + 2 * tt : tnp + 2 * ((k - 1) * 9 + tt);
+      dst[0] = w; dst[1] = w * rp;
     }
     for (int i = c; i < 8; i += C) {
       const short2 np = nbg[i + 1];
@@ -625,14 +658,13 @@ __global__ void __launch_bounds__(256) k_weak_coop(const PassConst* __restrict__
       const short2 np = nbl[k];
       if (np.x == -1 || np.y == -1 || !(k == 0 ? T.tab_c : T.tab_n)) continue;
       const int n = k == 0 ? T.n_c : T.n_n, rad = k == 0 ? T.rad_c : T.rad_n, inc = k == 0 ? T.inc_c : T.inc_n;
-      const float* tw = k == 0 ? tcw : tnw + (k - 1) * 9;
-      const float* twr = k == 0 ? tcwr : tnwr + (k - 1) * 9;
+      const float* tp = k == 0 ? tcp : tnp + (k - 1) * 18;
       float a_ref = 0, a_rr = 0, a_w = 0;
       for (int a = 0; a < n; ++a) {
         float r_ref = 0, r_rr = 0, r_w = 0;
         for (int b = 0; b < n; ++b) {
           const float rp = ref_texel(B.ref, W, Hh, np.x - rad + a * inc, np.y - rad + b * inc);
-          const float w = tw[a * n + b], wr = twr[a * n + b];
+          const float w = tp[2 * (a * n + b)], wr = tp[2 * (a * n + b) + 1];
           r_ref = r_ref + wr;
           r_rr = __builtin_fmaf(wr, rp, r_rr);
           r_w = r_w + w;

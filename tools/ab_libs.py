@@ -1,0 +1,43 @@
+"""A/B of several builds of libdpe_mvs.so on the bench workload, interleaved in one process (the
+scene is generated once).  Usage: python tools/ab_libs.py lib/variants/*.so"""
+import ctypes as C
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "dpe-mvs_amd"))
+import bench  # noqa: E402
+from DPE_MVS import _abi, native, synthetic  # noqa: E402
+
+sc = synthetic.make_scene(1600, 1200, 10)
+p = bench.workload_params(_abi, 10)
+inp = synthetic.pass_input(sc, p, depths=synthetic.src_depths(sc))
+st = synthetic.gt_state(sc)
+libs = sys.argv[1:]
+ctxs = []
+for path in libs:
+    lib = native.load_library(path)
+    ctx = lib.dpe_create(0)
+    bufs = _abi.PassBuffers(inp, st)
+    assert lib.dpe_pm_stage(ctx, C.byref(bufs.inp), C.byref(bufs.st)) == 0, lib.dpe_last_error()
+    lib.dpe_set_timing(ctx, 1)
+    ctxs.append((path, lib, ctx, bufs))
+res = {path: [] for path in libs}
+ref = None
+for rnd in range(3):
+    for path, lib, ctx, bufs in ctxs:
+        assert lib.dpe_pm_execute(ctx, None) == 0
+        assert lib.dpe_pm_fetch(ctx, C.byref(bufs.st)) == 0
+        out = bufs.planes.tobytes()
+        if ref is None:
+            ref = out
+        assert out == ref, f"{path}: output differs from {libs[0]}"
+        buf = (C.c_float * 9)()
+        lib.dpe_pm_last_timings(ctx, buf, 9)
+        res[path].append([float(x) for x in buf])
+names = ["total"] + native.CLASSES
+for path in libs:
+    best = min(res[path], key=lambda t: t[0])
+    print(os.path.basename(path), json.dumps({k: round(v, 2) for k, v in zip(names, best)}), flush=True)
