@@ -1,4 +1,5 @@
-"""Command line, same positional arguments as the reference's `DPE` binary (main.cpp:602-635):
+"""Python launcher with the positional arguments of the reference's `DPE` binary (main.cpp:602-635);
+the native command line is dpe-mvs_amd/bin/dpe (same arguments, RCCL across ranks):
 
     python -m DPE_MVS dense_folder [gpu_index] [verbose] [viz] [fusion] [depth] [normal] [weak] [edge]
 
@@ -32,7 +33,7 @@ def main(argv: list) -> int:
             return pipeline.run_dpe_pipeline(argv[1], local, verbose, fusion, viz, depth, normal, weak, edge, dist=dist)
         finally:
             dist.destroy_process_group()
-    return pipeline.run_dpe_pipeline(argv[1], gpu_index, verbose, fusion, viz, depth, normal, weak, edge)
+    return pipeline.dpe_mvs(argv[1], gpu_index, verbose, fusion, viz, depth, normal, weak, edge)
 
 
 if __name__ == "__main__":

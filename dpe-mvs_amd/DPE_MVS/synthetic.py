@@ -290,7 +290,7 @@ def write_dense_folder(folder: str, W: int, H: int, n_views: int, seed: int = SC
         os.makedirs(rf, exist_ok=True)
         for s in range(rounds):
             f = 1.0 / (1 << s)
-            w, h = pipeline._std_round(np.float32(W) * np.float32(f)), pipeline._std_round(np.float32(H) * np.float32(f))
+            w, h = pipeline.std_round(np.float32(W) * np.float32(f)), pipeline.std_round(np.float32(H) * np.float32(f))
             e, lab = _labels_edges_at(v["sid"], w, h)
             pipeline.write_bin_mat(os.path.join(rf, f"edges_{s}.dmb"), e)
             pipeline.write_bin_mat(os.path.join(rf, f"labels_{s}.dmb"), lab)

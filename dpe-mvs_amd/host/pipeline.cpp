@@ -1,0 +1,448 @@
+// pipeline.cpp — RunDPEPipeline (main.cpp:474-600) over the C-ABI PatchMatch pass.
+//
+// Kept from the reference: the dense_folder contract (images/%08d.jpg, cams/%08d_cam.txt, pair.txt
+// in; DPE/%08d/ results; edges_<s>.dmb / labels_<s>.dmb read from the result folders), the
+// coarse-to-fine schedule and its per-pass parameters (main.cpp:490-570), InuputInitialization's
+// rescaling rules (DPE.cpp:733-914), the ProcessProblem epilogue (main.cpp:423-446) and the final
+// .npy outputs (main.cpp:99-260).
+//
+// Different by design: every image is decoded once and its pyramid levels cached; per-image state
+// (depth, normal, weak, selected views) stays in memory between passes instead of .dmb round
+// trips; problems are split in contiguous blocks over ranks (one process per GPU) and the depth
+// maps are all-gathered after every pass; "reference" schedule = the reference's serial order,
+// "jacobi" = each pass reads the previous pass's depths (forced when world_size > 1).
+//
+// Not part of this build: EdgeSegment (the edge/label maps must exist), RunFusion
+// (fusion=true fails), the viz medium results (ignored).
+#include "host.h"
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <filesystem>
+#include <fstream>
+#include <map>
+#include <memory>
+#include <sstream>
+
+namespace fs = std::filesystem;
+
+namespace dpe_host {
+namespace {
+
+thread_local std::string g_err;
+const char* kOutName = "DPE";
+
+struct Problem {   // main.h:108-118
+  int index = 0, ref_image_id = 0;
+  std::vector<int> src_image_ids;
+  std::string dense_folder, result_folder;
+  int scale_size = 1;
+  DpePatchMatchParams params;
+  int iteration = 0;
+};
+
+struct DepthMap { int w = 0, h = 0; std::vector<float> d; };
+
+struct ImageState {   // depths.dmb / normals.dmb / weak.bin / selected_views.bin of one image
+  int w = 0, h = 0;
+  std::vector<float> depth, normal;     // normal: [h][w][3]
+  std::vector<uint8_t> weak;
+  std::vector<uint32_t> sel;
+};
+
+int std_round(float v) { return (int)std::round(v); }   // std::round: half away from zero
+
+bool generate_sample_list(const std::string& dense, std::vector<Problem>& probs, std::string& err) {   // main.cpp:264-308
+  std::ifstream f(fs::path(dense) / "pair.txt");
+  if (!f) { err = "cannot read pair.txt in " + dense; return false; }
+  std::string line;
+  std::getline(f, line);
+  int n = 0;
+  std::istringstream(line) >> n;
+  for (int i = 0; i < n; ++i) {
+    Problem p;
+    dpe_params_default(&p.params);
+    p.index = i;
+    std::getline(f, line);
+    std::istringstream(line) >> p.ref_image_id;
+    p.dense_folder = dense;
+    p.result_folder = (fs::path(dense) / kOutName / fmt_index(p.ref_image_id)).string();
+    std::error_code ec;
+    fs::create_directories(p.result_folder, ec);
+    std::getline(f, line);
+    std::istringstream is(line);
+    int m = 0;
+    is >> m;
+    for (int j = 0; j < m; ++j) {
+      int id; float score;
+      is >> id >> score;
+      if (score <= 0.0f) continue;
+      p.src_image_ids.push_back(id);
+    }
+    probs.push_back(std::move(p));
+  }
+  return true;
+}
+
+class ImageCache {
+ public:
+  explicit ImageCache(std::string folder) : folder_(std::move(folder)) {}
+  const std::vector<float>* full(int idx, int& w, int& h, std::string& err) {
+    auto it = full_.find(idx);
+    if (it == full_.end()) {
+      GrayImage g;
+      if (!read_gray((fs::path(folder_) / "images" / (fmt_index(idx) + ".jpg")).string(), g, err)) return nullptr;
+      Level L{g.w, g.h, std::vector<float>(g.px.begin(), g.px.end())};
+      it = full_.emplace(idx, std::move(L)).first;
+    }
+    w = it->second.w; h = it->second.h;
+    return &it->second.px;
+  }
+  const std::vector<float>* level(int idx, int scale, int& w, int& h, std::string& err) {
+    int fw, fh;
+    const std::vector<float>* f = full(idx, fw, fh, err);
+    if (!f) return nullptr;
+    if (scale == 1) { w = fw; h = fh; return f; }
+    const auto key = std::make_pair(idx, scale);
+    auto it = lvl_.find(key);
+    if (it == lvl_.end()) {
+      const float factor = 1.0f / (float)scale;
+      const int nw = std_round(fw * factor), nh = std_round(fh * factor);
+      Level L{nw, nh, std::vector<float>((size_t)nw * nh)};
+      resize_linear(f->data(), fw, fh, L.px.data(), nw, nh);
+      it = lvl_.emplace(key, std::move(L)).first;
+    }
+    w = it->second.w; h = it->second.h;
+    return &it->second.px;
+  }
+
+ private:
+  struct Level { int w, h; std::vector<float> px; };
+  std::string folder_;
+  std::map<int, Level> full_;
+  std::map<std::pair<int, int>, Level> lvl_;
+};
+
+int scale_index(int scale_size) { int s = 0; while ((1 << s) < scale_size) s++; return s; }
+
+void pass_params(DpePatchMatchParams& p, int i, int j) {   // main.cpp:510-556 (j = -1: first pass of round i)
+  if (j < 0) {
+    if (i == 0) { p.state = DPE_FIRST_INIT; p.use_APD = false; p.use_edge = false; }
+    else {
+      p.state = DPE_REFINE_INIT; p.use_APD = true; p.use_edge = true;
+      p.ransac_threshold = (float)(0.01 - i * 0.00125);
+      p.rotate_time = std::min((int)std::pow(2, i), 4);
+    }
+    p.geom_consistency = false;
+    p.max_iterations = 3;
+    p.weak_peak_radius = 6;
+  } else {
+    p.state = DPE_REFINE_ITER;
+    p.use_APD = i != 0; p.use_edge = i != 0;
+    p.ransac_threshold = (float)(0.01 - i * 0.00125);
+    p.rotate_time = std::min((int)std::pow(2, i), 4);
+    p.geom_consistency = true;
+    p.max_iterations = 3;
+    p.weak_peak_radius = std::max(4 - 2 * j, 2);
+  }
+}
+
+template <class T>
+std::vector<T> rescaled(const std::vector<T>& src, int w, int h, int nw, int nh, int ch = 1) {
+  if (w == nw && h == nh) return src;
+  std::vector<T> dst((size_t)nw * nh * ch, T(0));
+  rescale_nearest(src.data(), w, h, dst.data(), nw, nh, (int)sizeof(T) * ch);
+  return dst;
+}
+
+bool read_support(const Problem& p, const std::string& name, Mat& m, std::string& err) {
+  const std::string path = (fs::path(p.result_folder) / name).string();
+  if (!fs::exists(path)) {
+    err = path + " missing: the EdgeSegment edge/label precompute (DPE.cpp:9-291) is not part of this build "
+                 "(SURVEY.md §8f); provide edges_<s>.dmb / labels_<s>.dmb";
+    return false;
+  }
+  return read_bin_mat(path, m, err);
+}
+
+struct Runner {
+  dpe_pass_runner_fn fn = nullptr;
+  void* user = nullptr;
+  DpeContext* ctx = nullptr;
+  ~Runner() { if (ctx) dpe_destroy(ctx); }
+};
+int native_runner(void* user, const DpePassInput* in, const DpePassState* st) {
+  return dpe_pm_run(static_cast<DpeContext*>(user), in, st);
+}
+
+// InuputInitialization + SupportInitialization (DPE.cpp:733-914, 1025-1052), the pass, the epilogue
+bool process_problem(Problem& p, ImageCache& cache, std::map<int, ImageState>& states,
+                     const std::map<int, DepthMap>& depth_src, const DpePipelineOptions& opt, Runner& run,
+                     std::string& err) {
+  DpePatchMatchParams& P = p.params;
+  std::vector<int> ids{p.ref_image_id};
+  ids.insert(ids.end(), p.src_image_ids.begin(), p.src_image_ids.end());
+  if ((int)ids.size() > DPE_MAX_IMAGES) { err = "Can't process so much images: " + std::to_string(ids.size()); return false; }
+  int fw, fh;
+  if (!cache.full(ids[0], fw, fh, err)) return false;
+  std::vector<const float*> images;
+  std::vector<DpeCamera> cams(ids.size());
+  int W = 0, H = 0;
+  for (size_t k = 0; k < ids.size(); ++k) {
+    DpeCamera& cam = cams[k];
+    if (!read_camera((fs::path(p.dense_folder) / "cams" / (fmt_index(ids[k]) + "_cam.txt")).string(), cam, err)) return false;
+    cam.width = fw; cam.height = fh;
+    int w, h;
+    const std::vector<float>* img = cache.level(ids[k], p.scale_size, w, h, err);
+    if (!img) return false;
+    if (p.scale_size != 1) {
+      const float sx = w / (float)fw, sy = h / (float)fh;
+      cam.K[0] *= sx; cam.K[2] *= sx; cam.K[4] *= sy; cam.K[5] *= sy;
+      cam.width = w; cam.height = h;
+    }
+    if (k == 0) { W = w; H = h; }
+    images.push_back(img->data());
+  }
+  const size_t L = (size_t)W * H;
+  P.depth_min = cams[0].depth_min * 0.6f;
+  P.depth_max = cams[0].depth_max * 1.2f;
+  P.num_images = (int)ids.size();
+  std::vector<std::vector<float>> dep_store;
+  std::vector<const float*> depths(ids.size(), nullptr);
+  if (P.geom_consistency) {
+    dep_store.reserve(ids.size());
+    for (size_t k = 1; k < ids.size(); ++k) {
+      auto it = depth_src.find(ids[k]);
+      if (it == depth_src.end()) { err = "no depth map of source image " + std::to_string(ids[k]); return false; }
+      dep_store.push_back(rescaled(it->second.d, it->second.w, it->second.h, W, H));
+      depths[k] = dep_store.back().data();
+    }
+  }
+  const ImageState* prev = states.count(p.ref_image_id) ? &states.at(p.ref_image_id) : nullptr;
+  std::vector<float> planes(L * 4, 0.0f);
+  std::vector<uint8_t> weak(L, DPE_STRONG);
+  std::vector<uint32_t> sel(L, 0u);
+  if (P.use_APD) {
+    if (!prev) { err = "Can't find weak info of image " + std::to_string(p.ref_image_id); return false; }
+    weak = rescaled(prev->weak, prev->w, prev->h, W, H);
+  }
+  if (P.state != DPE_FIRST_INIT) {
+    if (!prev) { err = "no prior depth/normal of image " + std::to_string(p.ref_image_id); return false; }
+    const std::vector<float> d = rescaled(prev->depth, prev->w, prev->h, W, H);
+    const std::vector<float> n = rescaled(prev->normal, prev->w, prev->h, W, H, 3);
+    for (size_t i = 0; i < L; ++i) {
+      planes[4 * i + 0] = n[3 * i + 0]; planes[4 * i + 1] = n[3 * i + 1]; planes[4 * i + 2] = n[3 * i + 2];
+      planes[4 * i + 3] = d[i];
+    }
+    sel = rescaled(prev->sel, prev->w, prev->h, W, H);
+  }
+  DpePassInput in;
+  std::memset(&in, 0, sizeof(in));
+  in.width = W; in.height = H; in.num_images = (int)ids.size();
+  in.images = images.data();
+  in.cams = cams.data();
+  in.depths = P.geom_consistency ? depths.data() : nullptr;
+  Mat edge, edge_low, label;
+  if (P.use_edge || P.use_limit) {
+    const int s = scale_index(p.scale_size);
+    const int max_s = P.high_res_img ? scale_index(P.max_scale_size) : s;
+    if (!read_support(p, "edges_" + std::to_string(s) + ".dmb", edge, err)) return false;
+    if (!read_support(p, "edges_" + std::to_string(max_s) + ".dmb", edge_low, err)) return false;
+    if (edge.rows != H || edge.cols != W || edge.type != CV_8UC1) { err = "edge map size/type mismatch in " + p.result_folder; return false; }
+    in.edge = edge.ptr<uint8_t>();
+    in.edge_low_res = edge_low.ptr<uint8_t>();
+    in.low_width = edge_low.cols; in.low_height = edge_low.rows;
+  }
+  if (P.use_label) {
+    if (!read_support(p, "labels_" + std::to_string(scale_index(p.scale_size)) + ".dmb", label, err)) return false;
+    if (label.rows != H || label.cols != W || label.type != CV_32SC1) { err = "label map size/type mismatch in " + p.result_folder; return false; }
+    in.label = label.ptr<int32_t>();
+  }
+  in.params = P;
+  in.seed = opt.base_seed ^ ((uint64_t)p.ref_image_id * 0x9E3779B97F4A7C15ull);
+  in.pass_salt = (uint32_t)p.iteration;
+  std::vector<float> costs(L);
+  DpePassState st{planes.data(), weak.data(), sel.data(), costs.data()};
+  const int rc = run.fn(run.user, &in, &st);
+  if (rc != 0) {
+    err = "PatchMatch pass failed (" + std::to_string(rc) + "): " + (run.ctx ? std::string(dpe_last_error()) : "runner");
+    return false;
+  }
+  // epilogue (main.cpp:423-437): depth outside [dmin, dmax] -> 0 and UNKNOWN
+  ImageState s;
+  s.w = W; s.h = H;
+  s.depth.resize(L); s.normal.resize(L * 3); s.weak = weak; s.sel = sel;
+  for (size_t i = 0; i < L; ++i) {
+    float d = planes[4 * i + 3];
+    if (d < P.depth_min || d > P.depth_max) { d = 0.0f; s.weak[i] = DPE_UNKNOWN; }
+    s.depth[i] = d;
+    s.normal[3 * i + 0] = planes[4 * i + 0]; s.normal[3 * i + 1] = planes[4 * i + 1]; s.normal[3 * i + 2] = planes[4 * i + 2];
+  }
+  if (opt.keep_intermediate) {
+    Mat m;
+    m.create(H, W, CV_32FC1); std::memcpy(m.data.data(), s.depth.data(), L * 4);
+    if (!write_bin_mat((fs::path(p.result_folder) / "depths.dmb").string(), m, err)) return false;
+    m.create(H, W, CV_32FC3); std::memcpy(m.data.data(), s.normal.data(), L * 12);
+    if (!write_bin_mat((fs::path(p.result_folder) / "normals.dmb").string(), m, err)) return false;
+    m.create(H, W, CV_8UC1); std::memcpy(m.data.data(), s.weak.data(), L);
+    if (!write_bin_mat((fs::path(p.result_folder) / "weak.bin").string(), m, err)) return false;
+    m.create(H, W, CV_32SC1); std::memcpy(m.data.data(), s.sel.data(), L * 4);
+    if (!write_bin_mat((fs::path(p.result_folder) / "selected_views.bin").string(), m, err)) return false;
+  }
+  states[p.ref_image_id] = std::move(s);
+  return true;
+}
+
+bool write_outputs(const Problem& p, const ImageState& s, const DpePipelineOptions& opt, std::string& err) {   // main.cpp:572-578
+  const std::vector<int64_t> hw{s.h, s.w};
+  const fs::path rf(p.result_folder);
+  if (opt.depth) {
+    std::vector<float> d = s.depth;
+    for (size_t i = 0; i < d.size(); ++i) if (s.weak[i] == DPE_UNKNOWN) d[i] = 0.0f;   // ZeroDepthForUnknown
+    if (!write_npy((rf / "depth.npy").string(), d.data(), hw, "<f4", 4, err)) return false;
+  }
+  if (opt.normal && !write_npy((rf / "normal.npy").string(), s.normal.data(), {s.h, s.w, 3}, "<f4", 4, err)) return false;
+  if (opt.weak) {
+    std::vector<int8_t> e(s.weak.size());
+    for (size_t i = 0; i < e.size(); ++i) e[i] = s.weak[i] == DPE_WEAK ? 1 : (s.weak[i] == DPE_STRONG ? 2 : 0);
+    if (!write_npy((rf / "weak.npy").string(), e.data(), hw, "|i1", 1, err)) return false;
+  }
+  if (opt.edge) {
+    for (int idx = 0; idx < 8; ++idx) {
+      const fs::path ep = rf / ("edges_" + std::to_string(idx) + ".dmb");
+      if (!fs::exists(ep)) continue;
+      Mat m;
+      if (!read_bin_mat(ep.string(), m, err)) return false;
+      std::vector<int8_t> b(m.data.size());
+      for (size_t i = 0; i < b.size(); ++i) b[i] = m.data[i] > 0 ? 1 : 0;
+      if (!write_npy((rf / "edge.npy").string(), b.data(), {m.rows, m.cols}, "|i1", 1, err)) return false;
+      break;
+    }
+  }
+  return true;
+}
+
+int run(const char* dense_folder, const DpePipelineOptions& opt) {
+  std::string& err = g_err;
+  err.clear();
+  if (opt.fusion) { err = "fusion=true: RunFusion (DPE.cpp:1220-1370) is not part of this build (SURVEY.md §8f)"; return 1; }
+  const int world = std::max(1, opt.world_size), rank = opt.rank;
+  if (world > 1 && !opt.allgather) { err = "world_size > 1 needs an all-gather"; return 1; }
+  if (rank < 0 || rank >= world) { err = "bad rank"; return 1; }
+  const bool jacobi = world > 1 || opt.schedule == DPE_SCHEDULE_JACOBI;
+  const std::string dense(dense_folder);
+  std::error_code ec;
+  fs::create_directories(fs::path(dense) / kOutName, ec);
+  std::vector<Problem> problems;
+  if (!generate_sample_list(dense, problems, err)) return 1;
+  ImageCache cache(dense);
+  {   // CheckImages (main.cpp:310-329)
+    int w0 = 0, h0 = 0;
+    bool ok = !problems.empty();
+    for (size_t i = 0; ok && i < problems.size(); ++i) {
+      int w, h;
+      if (!cache.full(problems[i].ref_image_id, w, h, err)) ok = false;
+      else if (i == 0) { w0 = w; h0 = h; }
+      else if (w != w0 || h != h0) ok = false;
+    }
+    if (!ok) { err = "Images may error, check it! " + err; std::fprintf(stderr, "Images may error, check it!\n"); return 1; }
+  }
+  const int n = (int)problems.size();
+  std::vector<std::vector<int>> blocks(world);
+  for (int r = 0; r < world; ++r) for (int i = r * n / world; i < (r + 1) * n / world; ++i) blocks[r].push_back(i);
+  Runner runner;
+  if (opt.runner) { runner.fn = opt.runner; runner.user = opt.runner_user; }
+  else {
+    runner.ctx = dpe_create(opt.gpu_index);
+    if (!runner.ctx) { err = std::string("dpe_create: ") + dpe_last_error(); return 1; }
+    runner.fn = native_runner; runner.user = runner.ctx;
+  }
+  int w0, h0;
+  cache.full(problems[0].ref_image_id, w0, h0, err);
+  int round_num = 1, max_size = std::max(w0, h0);   // ComputeRoundNum (main.cpp:390-408)
+  while (max_size > 800) { max_size /= 2; round_num++; }
+  round_num = std::max(round_num, 2);
+  if (opt.verbose && rank == 0) {
+    std::printf("There are %d images to be processed!\n", n);
+    std::printf("There are %d resolution stages for coarse-to-fine processing!\n", round_num);
+    std::printf("Iteration nums: %d\n", round_num * 4);
+  }
+  for (auto& p : problems) p.params.max_scale_size = std::max(1, (int)std::pow(2, round_num - 1));
+  std::map<int, ImageState> states;
+  std::map<int, DepthMap> depth_cur;
+  int iteration_index = 0;
+  for (int i = 0; i < round_num; ++i) {
+    for (int j = -1; j < 3; ++j) {
+      const std::map<int, DepthMap> snapshot = jacobi ? depth_cur : std::map<int, DepthMap>{};
+      const auto& depth_src = jacobi ? snapshot : depth_cur;
+      int pw = 0, ph = 0;
+      for (int pi : blocks[rank]) {
+        Problem& p = problems[pi];
+        p.iteration = iteration_index;
+        p.scale_size = (int)std::pow(2, round_num - 1 - i);
+        p.params.scale_size = p.scale_size;
+        pass_params(p.params, i, j);
+        if (!process_problem(p, cache, states, depth_src, opt, runner, err)) return 1;
+        const ImageState& s = states[p.ref_image_id];
+        depth_cur[p.ref_image_id] = DepthMap{s.w, s.h, s.depth};
+        pw = s.w; ph = s.h;
+      }
+      if (world > 1) {   // all-gather of the depth maps (the pass's only cross-image data)
+        if (blocks[rank].empty()) { err = "empty rank block"; return 1; }
+        size_t nmax = 0;
+        for (auto& b : blocks) nmax = std::max(nmax, b.size());
+        const size_t per = (size_t)pw * ph;
+        std::vector<float> send(nmax * per, 0.0f), recv(nmax * per * world);
+        for (size_t k = 0; k < blocks[rank].size(); ++k) {
+          const auto& d = depth_cur[problems[blocks[rank][k]].ref_image_id];
+          std::memcpy(send.data() + k * per, d.d.data(), per * 4);
+        }
+        if (opt.allgather(opt.allgather_user, send.data(), send.size(), recv.data()) != 0) { err = "all-gather failed"; return 1; }
+        for (int r = 0; r < world; ++r)
+          for (size_t k = 0; k < blocks[r].size(); ++k) {
+            const float* src = recv.data() + ((size_t)r * nmax + k) * per;
+            depth_cur[problems[blocks[r][k]].ref_image_id] = DepthMap{pw, ph, std::vector<float>(src, src + per)};
+          }
+      }
+      if (opt.verbose && rank == 0) std::printf("Iteration %d / %d done\n", iteration_index + 1, round_num * 4);
+      iteration_index++;
+    }
+  }
+  for (int pi : blocks[rank]) {
+    const Problem& p = problems[pi];
+    if (!write_outputs(p, states[p.ref_image_id], opt, err)) return 1;
+  }
+  if (opt.verbose && rank == 0) std::printf("All done\n");
+  return 0;
+}
+
+}  // namespace
+}  // namespace dpe_host
+
+extern "C" {
+
+void dpe_pipeline_default_options(DpePipelineOptions* o) {
+  std::memset(o, 0, sizeof(*o));
+  o->gpu_index = 0;
+  o->verbose = true; o->fusion = false; o->viz = false;
+  o->depth = true; o->normal = false; o->weak = false; o->edge = false;
+  o->schedule = DPE_SCHEDULE_REFERENCE;
+  o->rank = 0; o->world_size = 1;
+  o->base_seed = 0x5EED;
+}
+
+int dpe_run_pipeline(const char* dense_folder, const DpePipelineOptions* opt) {
+  DpePipelineOptions o;
+  if (opt) o = *opt; else dpe_pipeline_default_options(&o);
+  try {
+    return dpe_host::run(dense_folder, o);
+  } catch (const std::exception& e) {
+    dpe_host::g_err = e.what();
+    return 1;
+  }
+}
+
+const char* dpe_pipeline_last_error(void) { return dpe_host::g_err.c_str(); }
+
+}  // extern "C"

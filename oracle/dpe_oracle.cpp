@@ -1761,4 +1761,10 @@ float oracle_sample(const float* img, int W, int H, float sx, float sy) {
   return OracleSample(S, im, sx, sy);
 }
 
+// dpe_pass_runner_fn (include/dpe_host.h) over the restatement, so tests can drive the C++ host
+// pipeline with the oracle in place of the GPU; `user` points to the thread count (int).
+int oracle_pass_runner(void* user, const DpePassInput* in, const DpePassState* st) {
+  return oracle_pm_run(in, st, user ? *static_cast<int*>(user) : 1);
+}
+
 }  // extern "C"

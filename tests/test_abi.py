@@ -55,3 +55,30 @@ def test_struct_layouts():
 def test_enum_values():
     assert (_abi.WEAK, _abi.STRONG, _abi.UNKNOWN) == (0, 1, 2)
     assert (_abi.FIRST_INIT, _abi.REFINE_INIT, _abi.REFINE_ITER) == (0, 1, 2)
+
+
+HOST_HEADER = os.path.join(ROOT, "include", "dpe_host.h")
+HOST_LIB = os.path.join(ROOT, "dpe-mvs_amd", "lib", "libdpe_host.so")
+
+
+def test_host_library_exports_every_declared_symbol():
+    src = re.sub(r"/\*.*?\*/", "", open(HOST_HEADER).read(), flags=re.S)
+    declared = sorted(set(re.findall(r"^\s*[A-Za-z_][\w\s\*]*?\b(dpe_\w+)\s*\(", src, flags=re.M)))
+    assert "dpe_run_pipeline" in declared
+    out = subprocess.run(["nm", "-D", "--defined-only", HOST_LIB], capture_output=True, text=True, check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if line.strip()}
+    missing = [f for f in declared if f not in exported]
+    assert not missing, missing
+
+
+def test_pipeline_options_layout_matches_header():
+    # the ctypes mirror of DpePipelineOptions must agree with the C struct: probe the C defaults
+    from DPE_MVS import pipeline
+    o = pipeline.DpePipelineOptions()
+    pipeline.lib().dpe_pipeline_default_options(C.byref(o))
+    assert (o.verbose, o.fusion, o.depth, o.normal, o.world_size, o.base_seed) == (True, False, True, False, 1, 0x5EED)
+
+
+def test_pybind_module_exposes_dpe_mvs():
+    from DPE_MVS import _dpe
+    assert "gpu_index" in _dpe.dpe_mvs.__doc__

@@ -1,13 +1,17 @@
-"""Host pipeline (DPE_MVS.pipeline): file formats, resampling quirks, the coarse-to-fine schedule and
-the multi-rank (one process per GPU) schedule.
+"""Host pipeline (C++ libdpe_host, include/dpe_host.h): file formats, JPEG luma decode, resampling
+quirks, the coarse-to-fine schedule and the multi-rank (one process per GPU) schedule.
 
-The pass executor is injected: CPU tests use the oracle (tests are allowed to; the product entry
-dpe_mvs() always uses the HIP library), the GPU test compares the HIP library with the oracle
-through the whole pipeline.
+The pass executor is injected through the C-ABI runner hook: CPU tests hand the C++ pipeline the
+oracle's `oracle_pass_runner` (tests may use the oracle; the product entries -- dpe_mvs(), bin/dpe --
+always use the HIP library); the GPU test runs the same pipeline on the HIP library and checks
+the outputs are bit-identical.
 """
+import ctypes as C
+import io
 import os
 import shutil
 import socket
+import subprocess
 
 import numpy as np
 import pytest
@@ -15,16 +19,14 @@ import pytest
 import oracle
 from DPE_MVS import _abi, pipeline, synthetic
 
-
-class OracleRunner:
-    def run(self, pass_input, state):
-        return oracle.run_pass(pass_input, state, threads=4)
-
-    def close(self):
-        pass
-
-
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUTS = ("depth.npy", "normal.npy", "weak.npy", "edge.npy")
+_THREADS = C.c_int(4)
+
+
+def oracle_runner():
+    fn = oracle.lib().oracle_pass_runner
+    return (C.cast(fn, C.c_void_p), C.addressof(_THREADS))
 
 
 def _outputs(folder, n):
@@ -50,26 +52,17 @@ def test_bin_mat_roundtrip(tmp_path):
               np.array([[0, 1, 2]], np.uint8), np.array([[-1, 0, 7]], np.int32)):
         p = str(tmp_path / "m.dmb")
         pipeline.write_bin_mat(p, a)
-        raw = open(p, "rb").read()
-        assert np.frombuffer(raw[:16], np.int32)[0] == 1            # version
+        assert np.frombuffer(open(p, "rb").read()[:16], np.int32)[0] == 1
         b = pipeline.read_bin_mat(p)
         assert b.dtype == a.dtype and b.shape == a.shape and np.array_equal(a, b)
 
 
-def test_bin_mat_rejects_bad_version(tmp_path):
-    p = str(tmp_path / "bad.dmb")
-    with open(p, "wb") as f:
-        f.write(np.array([2, 1, 1, 5], np.int32).tobytes() + b"\0\0\0\0")
-    with pytest.raises(pipeline.PipelineError):
-        pipeline.read_bin_mat(p)
-
-
-def test_camera_roundtrip_and_centre(tmp_path):
+def test_camera_reader(tmp_path):
     sc = synthetic.make_scene(32, 24, 2)
     v = sc["views"][1]
     p = str(tmp_path / "c.txt")
     pipeline.write_camera(p, v["K"], v["R"], v["t"], 2.5, 9.0)
-    cam = pipeline.read_camera(p)
+    cam = pipeline.read_camera(p)                                    # C++ ReadCamera
     assert np.allclose(np.array(cam.K[:]).reshape(3, 3), v["K"], rtol=1e-6)
     assert np.allclose(np.array(cam.R[:]).reshape(3, 3), v["R"], atol=1e-6)
     assert np.allclose(cam.c[:], v["C"], atol=1e-5)                 # c = -R^T t (DPE.cpp:363-367)
@@ -84,21 +77,53 @@ def test_camera_two_number_depth_line_gives_zero_max(tmp_path):
     assert cam.depth_min == 425.0 and cam.depth_max == 0.0
 
 
-def test_pair_parsing_drops_nonpositive_scores(tmp_path):
-    with open(tmp_path / "pair.txt", "w") as f:
-        f.write("2\n0\n3 1 10.0 2 0.0 3 -1\n1\n1 0 5.5\n")
-    probs = pipeline.generate_sample_list(str(tmp_path))
-    assert [p.ref_image_id for p in probs] == [0, 1]
-    assert probs[0].src_image_ids == [1] and probs[1].src_image_ids == [0]
-    assert os.path.isdir(tmp_path / "DPE" / "00000001")
+# ------------------------------------------------------------------------------ JPEG luma decode
+def _pil_luma(buf):
+    from PIL import Image
+    im = Image.open(io.BytesIO(buf))
+    im.draft("L", im.size)          # libjpeg JCS_GRAYSCALE output, as cv::imread(IMREAD_GRAYSCALE)
+    return np.asarray(im.convert("L"))
+
+
+@pytest.mark.parametrize("mode,sub,restart", [("L", None, 0), ("L", None, 3), ("RGB", 0, 0), ("RGB", 2, 0),
+                                              ("RGB", 2, 5), ("RGB", 1, 0)])
+def test_jpeg_luma_matches_libjpeg(tmp_path, mode, sub, restart):
+    from PIL import Image
+    rng = np.random.default_rng(3)
+    h, w = 61, 83                                                    # not multiples of 8 / 16
+    base = synthetic.make_scene(w, h, 1)["images"][0].astype(np.uint8)
+    img = np.stack([base, np.roll(base, 7, 1), 255 - base], -1) if mode == "RGB" else base
+    img = np.clip(img.astype(int) + rng.integers(-20, 20, img.shape), 0, 255).astype(np.uint8)
+    kw = dict(format="JPEG", quality=88)
+    if sub is not None:
+        kw["subsampling"] = sub
+    if restart:
+        kw["restart_marker_blocks"] = restart
+    bio = io.BytesIO()
+    Image.fromarray(img, mode=mode).save(bio, **kw)
+    p = str(tmp_path / "x.jpg")
+    open(p, "wb").write(bio.getvalue())
+    ours = pipeline.read_gray(p)
+    ref = _pil_luma(bio.getvalue())
+    assert ours.shape == ref.shape and np.array_equal(ours, ref)
+
+
+def test_pgm_and_unsupported(tmp_path):
+    p = str(tmp_path / "a.pgm")
+    a = np.arange(12, dtype=np.uint8).reshape(3, 4)
+    open(p, "wb").write(b"P5\n4 3\n255\n" + a.tobytes())
+    assert np.array_equal(pipeline.read_gray(p), a)
+    q = str(tmp_path / "b.png")
+    open(q, "wb").write(b"\x89PNG....")
+    with pytest.raises(pipeline.PipelineError):
+        pipeline.read_gray(q)
 
 
 # ------------------------------------------------------------------------------ resampling
 def test_resize_linear_half_is_2x2_mean():
     img = np.random.default_rng(0).integers(0, 256, (8, 10)).astype(np.float32)
     out = pipeline.resize_linear(img, 5, 4)
-    ref = img.reshape(4, 2, 5, 2).mean(axis=(1, 3))
-    assert np.allclose(out, ref, atol=1e-5)
+    assert np.allclose(out, img.reshape(4, 2, 5, 2).mean(axis=(1, 3)), atol=1e-5)
 
 
 def test_resize_linear_identity_and_border_clamp():
@@ -110,49 +135,36 @@ def test_resize_linear_identity_and_border_clamp():
 
 def test_rescale_swapped_factors_quirk():
     # RescaleMatToTargetSize uses o_r = r / scale_x, o_c = c / scale_y (DPE.cpp:1157-1158)
-    src = np.arange(6 * 4, dtype=np.int32).reshape(6, 4)            # rows 6, cols 4
-    dst = pipeline.rescale_to(src, 8, 12)                            # scale_x = 2, scale_y = 2
-    assert dst.shape == (12, 8)
-    assert dst[5, 3] == src[5 // 2, 3 // 2]
+    src = np.arange(6 * 4, dtype=np.int32).reshape(6, 4)
+    dst = pipeline.rescale_to(src, 8, 12)                            # scale_x = scale_y = 2
+    assert dst.shape == (12, 8) and dst[5, 3] == src[5 // 2, 3 // 2]
     src2 = np.arange(4 * 8, dtype=np.int32).reshape(4, 8)
     d2 = pipeline.rescale_to(src2, 16, 4)                            # scale_x = 2, scale_y = 1
-    # row index divided by the x factor, column index by the y factor
-    assert d2[3, 5] == src2[int(3 / 2.0), int(5 / 1.0)]
-    assert d2[3, 9] == 0                                              # o_c = 9 >= cols: left unset
+    assert d2[3, 5] == src2[int(3 / 2.0), 5]
+    assert d2[3, 9] == 0                                             # o_c = 9 >= cols: left unset
+    n = np.arange(2 * 3 * 3, dtype=np.float32).reshape(2, 3, 3)    # 3-channel (normals)
+    assert np.array_equal(pipeline.rescale_to(n, 6, 4)[3, 5], n[1, 2])
 
 
-def test_schedule_parameters():
-    p = pipeline.Problem(0, 0, [1], "", "")
-    pipeline._pass_params(p, 0, -1)
-    assert p.params.state == _abi.FIRST_INIT and not p.params.use_APD and not p.params.geom_consistency
-    pipeline._pass_params(p, 1, -1)
-    assert p.params.state == _abi.REFINE_INIT and p.params.use_edge and p.params.weak_peak_radius == 6
-    assert p.params.rotate_time == 2 and p.params.ransac_threshold == pytest.approx(0.00875)
-    pipeline._pass_params(p, 1, 0)
-    assert p.params.state == _abi.REFINE_ITER and p.params.geom_consistency and p.params.weak_peak_radius == 4
-    pipeline._pass_params(p, 2, 2)
-    assert p.params.rotate_time == 4 and p.params.weak_peak_radius == 2
-
-
+# ------------------------------------------------------------------------------ pipeline
 def test_missing_edges_is_a_clear_error(tmp_path, dense4):
     d = _copy(dense4, tmp_path, "noedge")
     os.remove(os.path.join(d, "DPE", "00000000", "edges_1.dmb"))
     with pytest.raises(pipeline.PipelineError, match="EdgeSegment"):
-        pipeline.run_dpe_pipeline(d, runner=OracleRunner(), verbose=False)
+        pipeline.run_dpe_pipeline(d, runner=oracle_runner(), verbose=False)
 
 
 def test_fusion_not_built(dense4):
     with pytest.raises(pipeline.PipelineError, match="RunFusion"):
-        pipeline.run_dpe_pipeline(dense4, runner=OracleRunner(), fusion=True, verbose=False)
+        pipeline.run_dpe_pipeline(dense4, runner=oracle_runner(), fusion=True, verbose=False)
 
 
-# ------------------------------------------------------------------------------ end to end
 def test_pipeline_end_to_end(tmp_path, dense4):
     d = _copy(dense4, tmp_path, "e2e")
-    assert pipeline.run_dpe_pipeline(d, runner=OracleRunner(), normal=True, weak=True, edge=True, verbose=False) == 0
+    assert pipeline.run_dpe_pipeline(d, runner=oracle_runner(), normal=True, weak=True, edge=True, verbose=False,
+                                     keep_intermediate=True) == 0
     out = _outputs(d, 4)
-    sc = synthetic.make_scene(64, 48, 4)
-    gt = sc["views"][0]["depth"]
+    gt = synthetic.make_scene(64, 48, 4)["views"][0]["depth"]
     dep = out[(0, "depth.npy")]
     assert dep.dtype == np.float32 and dep.shape == (48, 64)
     m = dep > 0
@@ -163,6 +175,9 @@ def test_pipeline_end_to_end(tmp_path, dense4):
     assert np.all(dep[w == 0] == 0)                                    # UNKNOWN -> depth 0
     assert out[(0, "normal.npy")].shape == (48, 64, 3)
     assert set(np.unique(out[(0, "edge.npy")])) <= {0, 1}
+    dmb = pipeline.read_bin_mat(os.path.join(d, "DPE", "00000000", "depths.dmb"))
+    wk = pipeline.read_bin_mat(os.path.join(d, "DPE", "00000000", "weak.bin"))
+    assert np.array_equal(np.where(wk == _abi.UNKNOWN, 0, dmb), dep)
 
 
 def _free_port():
@@ -179,9 +194,8 @@ def _rank_main(rank, world, port, folder):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        rc = pipeline.run_dpe_pipeline(folder, runner=OracleRunner(), normal=True, weak=True, edge=True,
-                                       verbose=False, dist=dist)
-        assert rc == 0
+        assert pipeline.run_dpe_pipeline(folder, runner=oracle_runner(), normal=True, weak=True, edge=True,
+                                         verbose=False, dist=dist) == 0
     finally:
         dist.destroy_process_group()
 
@@ -190,7 +204,7 @@ def test_two_rank_jacobi_matches_one_rank(tmp_path, dense4):
     import torch.multiprocessing as mp
     one = _copy(dense4, tmp_path, "one")
     two = _copy(dense4, tmp_path, "two")
-    assert pipeline.run_dpe_pipeline(one, runner=OracleRunner(), schedule="jacobi", normal=True, weak=True,
+    assert pipeline.run_dpe_pipeline(one, runner=oracle_runner(), schedule="jacobi", normal=True, weak=True,
                                      edge=True, verbose=False) == 0
     mp.start_processes(_rank_main, args=(2, _free_port(), two), nprocs=2, join=True, start_method="spawn")
     a, b = _outputs(one, 4), _outputs(two, 4)
@@ -198,22 +212,31 @@ def test_two_rank_jacobi_matches_one_rank(tmp_path, dense4):
         assert a[k].dtype == b[k].dtype and a[k].tobytes() == b[k].tobytes(), k
 
 
-def test_reference_schedule_differs_from_jacobi_only_by_order(tmp_path, dense4):
-    # same pipeline, serial (Gauss-Seidel) order: a valid reconstruction of similar quality
+def test_reference_schedule_reconstructs(tmp_path, dense4):
     d = _copy(dense4, tmp_path, "gs")
-    assert pipeline.run_dpe_pipeline(d, runner=OracleRunner(), verbose=False) == 0
+    assert pipeline.run_dpe_pipeline(d, runner=oracle_runner(), verbose=False) == 0
     dep = np.load(os.path.join(d, "DPE", "00000001", "depth.npy"))
     gt = synthetic.make_scene(64, 48, 4)["views"][1]["depth"]
     m = dep > 0
     assert np.median(np.abs(dep[m] - gt[m]) / gt[m]) < 0.03
 
 
+def test_cli_usage():
+    exe = os.path.join(ROOT, "dpe-mvs_amd", "bin", "dpe")
+    r = subprocess.run([exe], capture_output=True, text=True)
+    assert r.returncode != 0 and "USAGE" in r.stderr
+    from DPE_MVS.__main__ import main
+    assert main(["DPE"]) == 1
+
+
+# ------------------------------------------------------------------------------ GPU
 @pytest.mark.gpu
 def test_pipeline_hip_matches_oracle(tmp_path, dense4):
     a = _copy(dense4, tmp_path, "hip")
     b = _copy(dense4, tmp_path, "cpu")
-    assert pipeline.run_dpe_pipeline(a, normal=True, weak=True, verbose=False) == 0        # HIP runner
-    assert pipeline.run_dpe_pipeline(b, runner=OracleRunner(), normal=True, weak=True, verbose=False) == 0
+    from DPE_MVS import dpe_mvs
+    assert dpe_mvs(a, 0, False, False, False, True, True, True, False) == 0              # pybind entry, HIP
+    assert pipeline.run_dpe_pipeline(b, runner=oracle_runner(), normal=True, weak=True, verbose=False) == 0
     for i in range(4):
         for f in ("depth.npy", "normal.npy", "weak.npy"):
             x = np.load(os.path.join(a, "DPE", f"{i:08d}", f))
@@ -221,6 +244,12 @@ def test_pipeline_hip_matches_oracle(tmp_path, dense4):
             assert x.tobytes() == y.tobytes(), (i, f)
 
 
-def test_cli_usage():
-    from DPE_MVS.__main__ import main
-    assert main(["DPE"]) == 1
+@pytest.mark.gpu
+def test_cli_runs_on_gpu(tmp_path, dense4):
+    a = _copy(dense4, tmp_path, "cli")
+    exe = os.path.join(ROOT, "dpe-mvs_amd", "bin", "dpe")
+    r = subprocess.run([exe, a, "0", "1", "0", "0", "1", "1", "1", "1"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr
+    assert "All done" in r.stdout
+    for f in OUTS:
+        assert os.path.exists(os.path.join(a, "DPE", "00000003", f))
