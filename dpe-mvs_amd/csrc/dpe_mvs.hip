@@ -458,8 +458,12 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   else k_depth_to_weak<false><<<(unsigned)((L + 3) / 4), 256, 0, s>>>(dpc, Bc);
   end();
   Bc = begin(DPE_CLASS_LOCAL_REFINE);
-  if (c->img8) k_local_refine<true><<<(unsigned)((L + 19) / 20), 256, 0, s>>>(dpc, Bc);
-  else k_local_refine<false><<<(unsigned)((L + 19) / 20), 256, 0, s>>>(dpc, Bc);
+  {
+    const unsigned g = (unsigned)((L + 4 * kLrPix - 1) / (4 * kLrPix));
+    const size_t lds = (size_t)4 * kLrPix * 12 * nv * 2 * sizeof(float);
+    if (c->img8) k_local_refine_jobs<true><<<g, 256, lds, s>>>(dpc, Bc);
+    else k_local_refine_jobs<false><<<g, 256, lds, s>>>(dpc, Bc);
+  }
   end();
   HIPC(hipGetLastError());
   if (timing && nev > 0) {

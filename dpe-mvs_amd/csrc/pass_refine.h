@@ -235,82 +235,124 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_depth_to_weak(const Pass
 }
 
 // ------------------------------------------------------------------------------ LocalRefine
-// grid: five pixels per wave (12 lanes each: lanes 0..10 = hypotheses -5..5, lane 11 = cost at
-// the current depth), 4 waves per 256-thread workgroup.
+// LocalRefine with a flat job pool: a wave owns 4 pixels; every (pixel, hypothesis, selected view)
+// NCC is one job, dealt round-robin over the 64 lanes, so lanes stay busy whatever the pixels'
+// view counts are.  Per-hypothesis sums over views then run on one lane each, in ascending view
+// order (the reference's si loop), and the arg-min on the pixel's first lane.
+constexpr int kLrPix = 4;
 template <bool U8>
-__global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_local_refine(const PassConst* __restrict__ pcp, DevBufs B) {   // DPE.cu:2749-2835
-  __shared__ float s_patch[4][5][108];
-  __shared__ float s_tc[4][5][12];
+__global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_local_refine_jobs(const PassConst* __restrict__ pcp, DevBufs B) {   // DPE.cu:2749-2835
+  __shared__ float s_patch[4][kLrPix][108];
+  __shared__ float s_sum[4][kLrPix][3];
+  __shared__ float4 s_hyp[4][kLrPix][12];
+  extern __shared__ float s_dyn[];                // [4 waves][kLrPix][12][nv][2] job results
+  __shared__ float s_tc[4][kLrPix][12];
+  __shared__ uint8_t s_sel[4][kLrPix][DPE_MAX_IMAGES];
+  __shared__ int s_cnt[4][kLrPix][2];           // [0] selected views, [1] hypothesis mask (bit 11 = current)
   const PassConst& pc = *pcp;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int grp = lane / 12, g = lane % 12;
   const int W = pc.W;
   const long L = (long)W * pc.H;
-  const long pix = ((long)xcd_remap(blockIdx.x, gridDim.x, B.xcd_rows * 16 * ((pc.W + 19) / 20)) * 4 + wave) * 5 + grp;
-  const bool active = grp < 5 && pix < L;
-  const int x = active ? (int)(pix % W) : 0, y = active ? (int)(pix / W) : 0;
-  const int center = (int)(active ? pix : 0);
+  const long base = ((long)xcd_remap(blockIdx.x, gridDim.x, B.xcd_rows * 16 * ((pc.W + 15) / 16)) * 4 + wave) * kLrPix;
+  if (base >= L) return;                          // wave-uniform
   const DpeCamera& c0 = pc.cams[0];
-  bool go = active;
+  const bool fast = pc.P.strong_radius == 5 && pc.P.strong_increment == 2;
+  const uint32_t vmask = (pc.N - 1) >= 32 ? 0xFFFFFFFFu : ((1u << (pc.N - 1)) - 1u);
+  const int nv = pc.N - 1;
+  float* res = s_dyn + (size_t)wave * kLrPix * 12 * nv * 2;   // res[((p * 12 + h) * nv + k) * 2 + {0, 1}]
+  // ---- per pixel set-up: 16 lanes per pixel
+  const int gp = lane >> 4, gl = lane & 15;
+  const long pix = base + gp;
+  const bool act = pix < L;
+  const int x = act ? (int)(pix % W) : 0, y = act ? (int)(pix / W) : 0;
   float4 op = make_float4(0, 0, 0, 0);
-  float od = 0, base_line = 0, weight_normal = 0, disp = 0;
+  float od = 0, base_line = 0, weight_normal = 0;
   int valid = 0;
   uint32_t sel = 0;
-  const uint8_t* vw = B.vw + (size_t)DPE_MAX_IMAGES * center;
+  bool go = act;
+  if (go) { op = transform_normal_ref(c0, B.planes[pix]); od = op.w; if (od == 0) go = false; }
+  const uint8_t* vw = B.vw + (size_t)DPE_MAX_IMAGES * (act ? pix : 0);
   if (go) {
-    op = transform_normal_ref(c0, B.planes[center]);
-    od = op.w;
-    if (od == 0) go = false;
-  }
-  if (go) {
-    sel = B.sel[center];
+    sel = B.sel[pix];
     baseline_and_weights(pc, sel, vw, base_line, weight_normal, valid);
     if (weight_normal == 0 || valid == 0) go = false;
   }
-  const bool fast = pc.P.strong_radius == 5 && pc.P.strong_increment == 2;
-  float* pw = s_patch[wave][grp < 5 ? grp : 0];
-  if (go && fast) patch_lds_build(pw, pc, B, x, y, g, 12);
-  wave_sync();
-  float s_ref = 0, s_rr = 0, s_w = 0;
-  if (go && fast) patch_lds_sums(pw, s_ref, s_rr, s_w);
-  const uint32_t vmask = (pc.N - 1) >= 32 ? 0xFFFFFFFFu : ((1u << (pc.N - 1)) - 1u);
-  if (go) {
-    base_line /= valid;
-    disp = c0.K[0] * base_line / od;
-    float tc = 0.0f;
-    if (g < 11) {
-      const int pd = g - 5;
-      const float p_depth = c0.K[0] * base_line / (disp + (float)pd);
-      if (p_depth < pc.P.depth_min || p_depth > pc.P.depth_max) tc = __builtin_nanf("");   // skipped hypothesis
-      else {
-        float4 tp = op;
-        tp.w = dist2origin(c0, x, y, p_depth, tp);
-        // the pixel's own selected views in ascending order (same summation order as the
-        // reference's si loop; lanes of different pixels do not serialise on each other's views)
-        for (uint32_t bits = sel & vmask; bits; bits &= bits - 1) {
-          const int vi = __builtin_ctz(bits), si = vi + 1;
-          tc += (ncc_old_any<U8>(fast, pw, s_ref, s_rr, s_w, x, y, pc, B, si, tp) * vw[vi]);
-          if (pc.P.geom_consistency) tc += (pc.P.geom_factor * geom_cost(pc, B, x, y, si, tp) * vw[vi]);
-        }
-        tc /= weight_normal;
-      }
+  float* pw = s_patch[wave][gp];
+  if (go && fast) patch_lds_build(pw, pc, B, x, y, gl, 16);
+  float disp = 0.0f;
+  if (go) { base_line /= valid; disp = c0.K[0] * base_line / od; }
+  if (go && gl < 12) {                             // hypothesis gl (11 = the current depth)
+    bool ok = true;
+    float4 tp = op;
+    if (gl < 11) {
+      const float p_depth = c0.K[0] * base_line / (disp + (float)(gl - 5));
+      ok = !(p_depth < pc.P.depth_min || p_depth > pc.P.depth_max);
+      tp.w = dist2origin(c0, x, y, p_depth, tp);
     } else {
-      // cost at the current depth (DPE.cu:2776-2795, its own accumulation formula)
-      float4 tp = op;
       tp.w = dist2origin(c0, x, y, od, tp);
-      for (uint32_t bits = sel & vmask; bits; bits &= bits - 1) {
-        const int vi = __builtin_ctz(bits), si = vi + 1;
-        float t = ncc_old_any<U8>(fast, pw, s_ref, s_rr, s_w, x, y, pc, B, si, tp);
-        if (pc.P.geom_consistency) t += pc.P.geom_factor * geom_cost(pc, B, x, y, si, tp);
-        tc += (t * vw[vi]);
-      }
-      tc /= weight_normal;
     }
-    s_tc[wave][grp][g] = tc;
+    s_hyp[wave][gp][gl] = tp;
+    const uint64_t m = __ballot(ok) >> (gp * 16);
+    if (gl == 0) s_cnt[wave][gp][1] = (int)(m & 0xFFFu);
+  }
+  if (gl == 0) {
+    int ns = 0;
+    if (go) for (uint32_t bits = sel & vmask; bits; bits &= bits - 1) s_sel[wave][gp][ns++] = (uint8_t)__builtin_ctz(bits);
+    s_cnt[wave][gp][0] = ns;
+    if (!go) s_cnt[wave][gp][1] = 0;
   }
   wave_sync();
-  if (!go || g != 0) return;
-  const float* t = s_tc[wave][grp];
+  if (go && fast && gl == 0) patch_lds_sums(pw, s_sum[wave][gp][0], s_sum[wave][gp][1], s_sum[wave][gp][2]);
+  wave_sync();
+  // ---- flat job pool: (pixel, valid hypothesis, selected view)
+  int total = 0;
+#pragma unroll
+  for (int p = 0; p < kLrPix; ++p) total += __popc((unsigned)s_cnt[wave][p][1]) * s_cnt[wave][p][0];
+  for (int j = lane; j < total; j += 64) {
+    int p = 0, r = j;
+    for (;;) {
+      const int njp = __popc((unsigned)s_cnt[wave][p][1]) * s_cnt[wave][p][0];
+      if (r < njp) break;
+      r -= njp; ++p;
+    }
+    const int ns = s_cnt[wave][p][0];
+    unsigned m = (unsigned)s_cnt[wave][p][1];
+    for (int q = r / ns; q > 0; --q) m &= m - 1;     // the (r / ns)-th valid hypothesis
+    const int h = __builtin_ctz(m), k = r % ns;
+    const long px = base + p;
+    const int jx = (int)(px % W), jy = (int)(px / W);
+    const int si = s_sel[wave][p][k] + 1;
+    const float4 tp = s_hyp[wave][p][h];
+    const float* sm = s_sum[wave][p];
+    float* rr = res + ((p * 12 + h) * nv + k) * 2;
+    rr[0] = ncc_old_any<U8>(fast, s_patch[wave][p], sm[0], sm[1], sm[2], jx, jy, pc, B, si, tp);
+    if (pc.P.geom_consistency) rr[1] = geom_cost(pc, B, jx, jy, si, tp);
+  }
+  wave_sync();
+  // ---- per-hypothesis sums over views in ascending order (DPE.cu:2776-2795, 2805-2818)
+  if (go && gl < 12 && ((s_cnt[wave][gp][1] >> gl) & 1)) {
+    const int ns = s_cnt[wave][gp][0];
+    const bool geom = pc.P.geom_consistency;
+    const float gf = pc.P.geom_factor;
+    float tc = 0.0f;
+    for (int k = 0; k < ns; ++k) {
+      const int vi = s_sel[wave][gp][k];
+      const float* rr = res + ((gp * 12 + gl) * nv + k) * 2;
+      const float c = rr[0];
+      if (gl < 11) {
+        tc += (c * vw[vi]);
+        if (geom) tc += (gf * rr[1] * vw[vi]);
+      } else {
+        float t = c;
+        if (geom) t += gf * rr[1];
+        tc += (t * vw[vi]);
+      }
+    }
+    s_tc[wave][gp][gl] = tc / weight_normal;
+  }
+  wave_sync();
+  if (!go || gl != 0) return;
+  const float* t = s_tc[wave][gp];
   float min_cost = 2.0f, best_depth = od;
   for (int pd = -5; pd <= 5; ++pd) {
     const float p_depth = c0.K[0] * base_line / (disp + (float)pd);
@@ -318,7 +360,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_local_refine(const PassC
     const float tcv = t[pd + 5];
     if (tcv < min_cost) { min_cost = tcv; best_depth = p_depth; }
   }
-  if ((double)(t[11] - min_cost) > 0.1) B.planes[center].w = best_depth;
+  if ((double)(t[11] - min_cost) > 0.1) B.planes[pix].w = best_depth;
 }
 
 // ------------------------------------------------------------------------------ FindNearestStrongPoint
