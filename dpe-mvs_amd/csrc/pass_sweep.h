@@ -234,9 +234,23 @@ DEV int acmh_candidate(const PassConst& pc, const float* __restrict__ costs, int
 }
 
 // ------------------------------------------------------------------------------ strong sweep
-// LDS floats per wave for P pixels, C lanes each, nv source views (multiple of 4: float4 alignment)
+// LDS floats per wave for P pixels, C candidate lanes each, nv source views (multiple of 4)
 __host__ __device__ inline int strong_lds_per_wave(int P, int C, int nv) {
-  return (P * (160 + C + C * nv + 8 * nv) + 3) & ~3;
+  return (P * (165 + 2 * C + (C + 8) * nv) + 3) & ~3;
+}
+
+// Job pools of a wave: the NCCs of all its pixels are dealt round-robin over the 64 lanes, so a
+// lane's work does not depend on how many candidates / selected views its own pixel has.
+// (pixel p, item i) <- flat job j, given per-pixel job counts cnt[p].
+template <int P>
+DEV bool job_decode(const int* cnt, int j, int& p, int& r) {
+  r = j;
+#pragma unroll
+  for (int q = 0; q < P; ++q) {
+    if (r < cnt[q]) { p = q; return true; }
+    r -= cnt[q];
+  }
+  return false;
 }
 
 template <bool U8, bool EDGE>
@@ -252,26 +266,34 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_strong_coop(const PassCo
   const int ps = lane / C, c = lane % C;
   const int W = pc.W, nv = pc.N - 1;
   const DpeCamera& c0 = pc.cams[0];
-  const int gi = (xcd_remap(blockIdx.x, gridDim.x, B.xcd_rows * 16) * 4 + wave) * P + ps;
-  if ((xcd_remap(blockIdx.x, gridDim.x, B.xcd_rows * 16) * 4 + wave) * P >= nlist) return;   // wave-uniform tail
+  const int wbase = (xcd_remap(blockIdx.x, gridDim.x, B.xcd_rows * 16) * 4 + wave) * P;
+  if (wbase >= nlist) return;                          // wave-uniform tail
+  const int gi = wbase + ps;
   const bool active = gi < nlist;
   const int center = active ? list[gi] : 0;
   const int x = center % W, y = center / W;
-  // ---- LDS carve (per wave)
+  // ---- LDS carve (per wave; arrays indexed by pixel q where another pixel's data is read)
   float* wl = lds + (size_t)wave * strong_lds_per_wave(P, C, nv);
-  float4* hyp = (float4*)wl + ps * 5;                    // [P][5] float4
-  float* pw = wl + P * 20 + ps * 108;                    // [P][108] patch
-  float* cost = wl + P * 128 + ps * C * nv;              // [P][C][nv]
-  float* sp = wl + P * (128 + C * nv) + ps * nv;         // [P][nv]
-  float* cur = sp + P * nv;                              // [P][nv]   current-plane NCC per selected view
-  float* ref = wl + P * (128 + C * nv + 2 * nv) + ps * 5 * nv;   // [P][5][nv] refinement NCCs
-  float* fc = wl + P * (128 + C * nv + 7 * nv) + ps * 8;  // [P][8]  final costs
-  uint8_t* vwl = (uint8_t*)(wl + P * (136 + C * nv + 7 * nv)) + ps * 32;   // [P][32] view weights
-  int* ib = (int*)(wl + P * (144 + C * nv + 7 * nv)) + ps * (C + 16 + nv);
+  float4* hyp_all = (float4*)wl;                         // [P][5] float4
+  float* pw_all = wl + P * 20;                           // [P][108] patch
+  float* cost_all = wl + P * 128;                        // [P][C + 1][nv]; slot C = the current plane
+  float* sp = wl + P * (128 + (C + 1) * nv) + ps * nv;   // [P][nv]
+  float* ref_all = wl + P * (128 + (C + 2) * nv);        // [P][5][nv] refinement NCCs
+  float* fc = wl + P * (128 + (C + 7) * nv) + ps * 8;    // [P][8]  final costs
+  float* sums_all = wl + P * (136 + (C + 7) * nv);       // [P][4]  patch sums s_ref, s_rr, s_w
+  uint8_t* vwl = (uint8_t*)(wl + P * (140 + (C + 7) * nv)) + ps * 32;   // [P][32] view weights
+  int* ib_all = (int*)(wl + P * (148 + (C + 7) * nv));
+  const int ibs = 2 * C + 17 + nv;                       // ints per pixel
+  int* ib = ib_all + ps * ibs;
   int* posl = ib;                                        // [C] candidate positions (-1 = none)
   int* fin = ib + C;                                     // [8] final slot of direction d (-1 = zero vector)
-  int* misc = ib + C + 8;                                // [8] 0: nsel, 1: tsv
+  int* misc = ib + C + 8;                                // [8] 0: nsel, 1: job slots (candidates + current)
   int* sel_list = ib + C + 16;                           // [nv]
+  int* slots = ib + C + 16 + nv;                         // [C + 1] cost-vector jobs: candidate slots, then C
+  float4* hyp = hyp_all + ps * 5;
+  float* pw = pw_all + ps * 108;
+  float* cost = cost_all + ps * (C + 1) * nv;
+  float* ref = ref_all + ps * 5 * nv;
 
   const float* __restrict__ costs_s = B.costs_snap;
   const float4* __restrict__ planes_s = B.planes_snap;
@@ -291,14 +313,33 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_strong_coop(const PassCo
     posl[c] = pos;
   }
   wave_sync();
-  float s_ref = 0, s_rr = 0, s_w = 0;
-  if (active && fast) patch_lds_sums(pw, s_ref, s_rr, s_w);
-  // ---- phase 2: candidate cost vectors (lane = candidate)
-  if (active) {
-    const int pos = posl[c];
-    if (pos >= 0) {
-      const float4 pl = planes_s[pos];
-      for (int v = 1; v <= nv; ++v) cost[c * nv + v - 1] = ncc_old_any<U8>(fast, pw, s_ref, s_rr, s_w, x, y, pc, B, v, pl);
+  if (c == 0) {
+    int n = 0;
+    if (active) {
+      for (int k = 0; k < C; ++k) if (posl[k] >= 0) slots[n++] = k;
+      slots[n++] = C;
+      if (fast) patch_lds_sums(pw, sums_all[ps * 4 + 0], sums_all[ps * 4 + 1], sums_all[ps * 4 + 2]);
+    }
+    misc[1] = n;
+  }
+  wave_sync();
+  // ---- phase 2: cost vectors of every candidate and of the current plane, one flat pool
+  {
+    // view-major order: the lanes of one round gather from the same source image (cache locality)
+    int cnt[P], S = 0;
+#pragma unroll
+    for (int q = 0; q < P; ++q) { cnt[q] = ib_all[q * ibs + C + 8 + 1]; S += cnt[q]; }
+    int q, r;
+    for (int j = lane; j < S * nv; j += 64) {
+      job_decode<P>(cnt, j % S, q, r);
+      const int* iq = ib_all + q * ibs;
+      const int slot = iq[C + 16 + nv + r], v = j / S + 1;
+      const int cq = list[wbase + q];
+      const int qx = cq % W, qy = cq / W;
+      const float4 pl = slot < C ? planes_s[iq[slot]] : planes_s[cq];
+      const float* sm = sums_all + q * 4;
+      cost_all[(q * (C + 1) + slot) * nv + v - 1] =
+          ncc_old_any<U8>(fast, pw_all + q * 108, sm[0], sm[1], sm[2], qx, qy, pc, B, v, pl);
     }
   }
   wave_sync();
@@ -356,28 +397,26 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_strong_coop(const PassCo
   // ---- serial: samples + view weights (pixel lane 0)
   Rng rs;
   uint32_t tsv = 0; float wnorm = 0.0f;
-  if (active && c == 0) {
-    rng_init(rs, (uint32_t)center, pc.seed32, STREAM_ITER_BASE + 4 * iter + 0, pc.salt);
-    view_sample(sp, nv, rs, vwl, tsv, wnorm);
+  if (c == 0) {
     int ns = 0;
-    for (int i = 0; i < nv; ++i) if (vwl[i] > 0) sel_list[ns++] = i;
+    if (active) {
+      rng_init(rs, (uint32_t)center, pc.seed32, STREAM_ITER_BASE + 4 * iter + 0, pc.salt);
+      view_sample(sp, nv, rs, vwl, tsv, wnorm);
+      for (int i = 0; i < nv; ++i) if (vwl[i] > 0) sel_list[ns++] = i;
+      uint8_t* vwg = B.vw + (size_t)center * DPE_MAX_IMAGES;
+      for (int j = 0; j < DPE_MAX_IMAGES; ++j) vwg[j] = vwl[j];
+    }
     misc[0] = ns;
-    uint8_t* vwg = B.vw + (size_t)center * DPE_MAX_IMAGES;
-    for (int j = 0; j < DPE_MAX_IMAGES; ++j) vwg[j] = vwl[j];
   }
   wave_sync();
   const int nsel = active ? misc[0] : 0;
-  // ---- phase 5: final costs of the 8 directions + current-plane NCCs over the selected views
-  if (active) {
-    if (c < 8) {
-      float wn = 0.0f;
-      for (int i = 0; i < nv; ++i) wn += vwl[i];   // == weight_norm (same order: sum of vw > 0)
-      float f = 0.0f;
-      for (int j = 0; j < nv; ++j) { const int w = vwl[j]; if (w > 0) f += w * cst(c, j); }
-      fc[c] = f / wn;
-    }
-    const float4 curp = planes_s[center];
-    for (int k = c; k < nsel; k += C) cur[k] = ncc_old_any<U8>(fast, pw, s_ref, s_rr, s_w, x, y, pc, B, sel_list[k] + 1, curp);
+  // ---- phase 5: final costs of the 8 directions
+  if (active && c < 8) {
+    float wn = 0.0f;
+    for (int i = 0; i < nv; ++i) wn += vwl[i];   // == weight_norm (same order: sum of vw > 0)
+    float f = 0.0f;
+    for (int j = 0; j < nv; ++j) { const int w = vwl[j]; if (w > 0) f += w * cst(c, j); }
+    fc[c] = f / wn;
   }
   wave_sync();
   // ---- serial: propagation acceptance + refinement hypotheses (DPE.cu:1617-1654, 1065-1095)
@@ -387,7 +426,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_strong_coop(const PassCo
     int mi = 0; float mcost = fc[0];
     for (int i = 1; i < 8; ++i) if (fc[i] <= mcost) { mcost = fc[i]; mi = i; }
     const float4 curp = planes_s[center];
-    for (int k = 0; k < nsel; ++k) cost_now += vwl[sel_list[k]] * cur[k];
+    for (int k = 0; k < nsel; ++k) cost_now += vwl[sel_list[k]] * cost[C * nv + sel_list[k]];
     cost_now /= wnorm;
     cost_written = cost_now;
     B.costs[center] = cost_now;
@@ -416,11 +455,19 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_strong_coop(const PassCo
     hyp[0] = h0; hyp[1] = h1; hyp[2] = h2; hyp[3] = h3; hyp[4] = h4;
   }
   wave_sync();
-  // ---- phase 6: refinement NCCs, jobs (hypothesis, selected view)
-  if (active) {
-    for (int j = c; j < 5 * nsel; j += C) {
-      const int h = j / nsel, k = j % nsel;
-      ref[h * nv + k] = ncc_old_any<U8>(fast, pw, s_ref, s_rr, s_w, x, y, pc, B, sel_list[k] + 1, hyp[h]);
+  // ---- phase 6: refinement NCCs, one flat pool of (pixel, hypothesis, selected view)
+  {
+    int cnt[P];
+#pragma unroll
+    for (int q = 0; q < P; ++q) cnt[q] = 5 * ib_all[q * ibs + C + 8];
+    int q, r;
+    for (int j = lane; job_decode<P>(cnt, j, q, r); j += 64) {
+      const int* iq = ib_all + q * ibs;
+      const int h = r % 5, k = r / 5;                      // the 5 hypotheses of one view adjacent
+      const int cq = list[wbase + q];
+      const float* sm = sums_all + q * 4;
+      ref_all[(q * 5 + h) * nv + k] = ncc_old_any<U8>(fast, pw_all + q * 108, sm[0], sm[1], sm[2], cq % W, cq / W, pc,
+                                                      B, iq[C + 16 + k] + 1, hyp_all[q * 5 + h]);
     }
   }
   wave_sync();
