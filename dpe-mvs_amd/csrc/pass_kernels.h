@@ -35,13 +35,21 @@ __global__ void k_gen_edge_inform(const PassConst* __restrict__ pcp, DevBufs B) 
   if (pc.P.use_edge) {
     short2* en = B.edge_neigh + (size_t)center * 8;
     for (int i = 0; i < 8; i++) {
+      // first edge pixel along the ray; loads in batches of 8 (one latency per batch)
       short2 r = make_short2(-1, -1);
       const int dx = kDir[i][0], dy = kDir[i][1];
-      int nx = x + dx, ny = y + dy;
-      while (true) {
-        if (nx < 0 || nx >= W || ny < 0 || ny >= H) break;
-        if (B.edge[nx + ny * W]) { r = make_short2((short)nx, (short)ny); break; }
-        nx += dx; ny += dy;
+      // steps until the ray leaves the image
+      const int sx = dx > 0 ? W - 1 - x : (dx < 0 ? x : 1 << 30);
+      const int sy = dy > 0 ? H - 1 - y : (dy < 0 ? y : 1 << 30);
+      const int n = MINo(sx, sy);
+      for (int k0 = 1; k0 <= n; k0 += 8) {
+        uint8_t e[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) e[k] = (k0 + k <= n) ? B.edge[(x + (k0 + k) * dx) + (y + (k0 + k) * dy) * W] : 0;
+        int hit = -1;
+#pragma unroll
+        for (int k = 7; k >= 0; --k) if (e[k]) hit = k;
+        if (hit >= 0) { r = make_short2((short)(x + (k0 + hit) * dx), (short)(y + (k0 + hit) * dy)); break; }
       }
       en[i] = r;
     }
@@ -64,16 +72,26 @@ __global__ void k_gen_edge_inform(const PassConst* __restrict__ pcp, DevBufs B) 
     if (cl > 0) {
       short2* lb = B.lab_bound + (size_t)center * 8;
       for (int i = 0; i < 8; i++) {
+        // last pixel of the own label before the first -1 label (or the border); batches of 8 loads
         const int dx = kDir[i][0], dy = kDir[i][1];
-        int nx = x + dx, ny = y + dy, lx = -1, ly = -1;
-        while (true) {
-          if (nx < 0 || nx >= W || ny < 0 || ny >= H) break;
-          const int nl = B.label[nx + ny * W];
-          if (nl == cl) { lx = nx; ly = ny; }
-          else if (nl == -1) break;
-          nx += dx; ny += dy;
+        const int sx = dx > 0 ? W - 1 - x : (dx < 0 ? x : 1 << 30);
+        const int sy = dy > 0 ? H - 1 - y : (dy < 0 ? y : 1 << 30);
+        const int n = MINo(sx, sy);
+        int lk = -1;
+        bool stop = false;
+        for (int k0 = 1; k0 <= n && !stop; k0 += 8) {
+          int lab[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) lab[k] = (k0 + k <= n) ? B.label[(x + (k0 + k) * dx) + (y + (k0 + k) * dy) * W] : -1;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            if (stop) continue;
+            if (k0 + k > n) { stop = true; continue; }
+            if (lab[k] == cl) lk = k0 + k;
+            else if (lab[k] == -1) stop = true;
+          }
         }
-        lb[i] = make_short2((short)lx, (short)ly);
+        lb[i] = lk < 0 ? make_short2(-1, -1) : make_short2((short)(x + lk * dx), (short)(y + lk * dy));
       }
     }
   }
@@ -134,8 +152,10 @@ __global__ void __launch_bounds__(256) k_gen_neighbours(const PassConst* __restr
             short2 np = make_short2((short)f2i((float)x + dir.x * radius), (short)f2i((float)y + dir.y * radius));
             if (np.x < min_margin || np.y < min_margin || np.x >= W - min_margin || np.y >= H - min_margin) continue;
             int npc = np.x + np.y * W;
-            if (B.weak[npc] != DPE_STRONG) {
-              np = B.nearest[npc];
+            const uint8_t wk = B.weak[npc];
+            const short2 nn = B.nearest[npc];        // issued with weak[]: one latency, not two
+            if (wk != DPE_STRONG) {
+              np = nn;
               if (np.x == -1 || np.y == -1) continue;
               npc = np.x + np.y * W;
             }
@@ -196,27 +216,33 @@ __global__ void __launch_bounds__(256) k_gen_neighbours(const PassConst* __restr
   }
   if (strong_point_size <= 3) { B.weak_rel[center] = 0; return; }
 
-  short2 spv[64];
-  float3 spv3[64];
-  float3 spvn[64];
+  // support points compacted in place (strong_points doubles as spv[]); per point only the depth
+  // is kept: its 3-D point and normal are recomputed from (pixel, depth) / planes[] when a, b, c
+  // are drawn (same expressions, same bits), which halves the per-thread scratch.
+  short2* spv = strong_points;
+  float spd[64];
   int valid_count = 0;
   float X[3];
   get3d(camera, x, y, B.planes[center].w, X);
   const float cpz = X[2];
   for (int i = 0; i < 64; ++i) {
-    spv[i] = make_short2(-1, -1);
     if ((dir_valid >> i) & 1ull) {
       const short2 sp = strong_points[i];
-      const int spc = sp.x + sp.y * W;
       spv[valid_count] = sp;
-      const float4 pl = B.planes[spc];
-      get3d(camera, sp.x, sp.y, pl.w, X);
-      spv3[valid_count] = make_float3(X[0], X[1], X[2]);
-      const float4 n4 = transform_normal_ref(camera, pl);
-      spvn[valid_count] = make_float3(n4.x, n4.y, n4.z);
+      spd[valid_count] = B.planes[sp.x + sp.y * W].w;
       valid_count++;
     }
   }
+  for (int i = valid_count; i < 64; ++i) spv[i] = make_short2(-1, -1);
+  auto point3 = [&](int i) -> float3 {
+    float Y[3];
+    get3d(camera, spv[i].x, spv[i].y, spd[i], Y);
+    return make_float3(Y[0], Y[1], Y[2]);
+  };
+  auto normal3 = [&](int i) -> float3 {
+    const float4 n4 = transform_normal_ref(camera, B.planes[spv[i].x + spv[i].y * W]);
+    return make_float3(n4.x, n4.y, n4.z);
+  };
   float4 best_plane = make_float4(0, 0, 0, 0);
   bool has_valid_plane = false;
   {
@@ -252,7 +278,7 @@ __global__ void __launch_bounds__(256) k_gen_neighbours(const PassConst* __restr
       }
       bool normal_consistency = false;
       if (pc.P.geom_consistency && edge_limit) {
-        const float3 AN = spvn[a], BN = spvn[b], CN = spvn[c];
+        const float3 AN = normal3(a), BN = normal3(b), CN = normal3(c);
         normal_consistency = true;
         if ((double)(AN.x * BN.x + AN.y * BN.y + AN.z * BN.z) < 0.8660254 ||
             (double)(AN.x * CN.x + AN.y * CN.y + AN.z * CN.z) < 0.8660254 ||
@@ -261,7 +287,7 @@ __global__ void __launch_bounds__(256) k_gen_neighbours(const PassConst* __restr
         if (has_consist_normal_plane && !normal_consistency) continue;
       }
       iteration--;
-      const float3 A = spv3[a], Bq = spv3[b], C = spv3[c];
+      const float3 A = point3(a), Bq = point3(b), C = point3(c);
       const float ACx = A.x - C.x, ACy = A.y - C.y, ACz = A.z - C.z;
       const float BCx = Bq.x - C.x, BCy = Bq.y - C.y, BCz = Bq.z - C.z;
       float4 cv;
@@ -276,7 +302,7 @@ __global__ void __launch_bounds__(256) k_gen_neighbours(const PassConst* __restr
         const float fx = ((float)spv[si].x - camera.K[2]) / camera.K[0];
         const float fy = ((float)spv[si].y - camera.K[5]) / camera.K[4];
         const float fd = -cv.w / (cv.x * fx + cv.y * fy + cv.z);
-        const float dist = __builtin_fabsf(fd - spv3[si].z);
+        const float dist = __builtin_fabsf(fd - spd[si]);
         residuals[si] = dist;
         if (dist < temp_thr) temp_count++;
       }
@@ -317,12 +343,12 @@ __global__ void __launch_bounds__(256) k_gen_neighbours(const PassConst* __restr
     }
   }
   if (!has_valid_plane) { B.weak_rel[center] = 0; return; }
-  float weight[64];
+  float* weight = spd;          // in place: weight[i] is written after spd[i] is read
   for (int i = 0; i < valid_count; ++i) {
     const float fx = ((float)spv[i].x - camera.K[2]) / camera.K[0];
     const float fy = ((float)spv[i].y - camera.K[5]) / camera.K[4];
     const float fd = -best_plane.w / (best_plane.x * fx + best_plane.y * fy + best_plane.z);
-    const float dist = __builtin_fabsf(fd - spv3[i].z);
+    const float dist = __builtin_fabsf(fd - spd[i]);
     if (dist >= ransac_threshold) { spv[i] = make_short2(-1, -1); weight[i] = 3.40282347e+38f; continue; }
     weight[i] = dist;
   }
