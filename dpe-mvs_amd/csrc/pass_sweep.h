@@ -235,8 +235,11 @@ DEV int acmh_candidate(const PassConst& pc, const float* __restrict__ costs, int
 
 // ------------------------------------------------------------------------------ strong sweep
 // LDS floats per wave for P pixels, C candidate lanes each, nv source views (multiple of 4)
-__host__ __device__ inline int strong_lds_per_wave(int P, int C, int nv) {
+__host__ __device__ inline int strong_lds_base(int P, int C, int nv) {   // floats before the plane table
   return (P * (165 + 2 * C + (C + 8) * nv) + 3) & ~3;
+}
+__host__ __device__ inline int strong_lds_per_wave(int P, int C, int nv) {
+  return strong_lds_base(P, C, nv) + P * (C + 1) * 5;   // + planes [P][C+1] float4 + alias [P][C+1]
 }
 
 // Job pools of a wave: the NCCs of all its pixels are dealt round-robin over the 64 lanes, so a
@@ -290,6 +293,10 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_strong_coop(const PassCo
   int* misc = ib + C + 8;                                // [8] 0: nsel, 1: job slots (candidates + current)
   int* sel_list = ib + C + 16;                           // [nv]
   int* slots = ib + C + 16 + nv;                         // [C + 1] cost-vector jobs: candidate slots, then C
+  float4* cpl_all = (float4*)(wl + strong_lds_base(P, C, nv));   // [P][C + 1] candidate planes, slot C = current
+  int* alias_all = (int*)(wl + strong_lds_base(P, C, nv) + P * (C + 1) * 4);   // [P][C + 1]
+  float4* cpl = cpl_all + ps * (C + 1);
+  int* alias = alias_all + ps * (C + 1);
   float4* hyp = hyp_all + ps * 5;
   float* pw = pw_all + ps * 108;
   float* cost = cost_all + ps * (C + 1) * nv;
@@ -311,13 +318,31 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_strong_coop(const PassCo
       pos = acmh_candidate(pc, costs_s, x, y, center, c);
     }
     posl[c] = pos;
+    if (pos >= 0) cpl[c] = planes_s[pos];
+    if (c == 0) cpl[C] = planes_s[center];
+  }
+  wave_sync();
+  // ---- phase 1b: bitwise-identical planes among the candidates and the current plane (a third of
+  // the candidates in a converged map: propagation copies planes) share one cost vector
+  auto same = [](const float4& a, const float4& b) {
+    return __float_as_uint(a.x) == __float_as_uint(b.x) && __float_as_uint(a.y) == __float_as_uint(b.y) &&
+           __float_as_uint(a.z) == __float_as_uint(b.z) && __float_as_uint(a.w) == __float_as_uint(b.w);
+  };
+  if (active) {
+    for (int sl = c; sl <= C; sl += C) {
+      if (sl < C && posl[sl] < 0) { alias[sl] = -1; continue; }
+      const float4 me = cpl[sl];
+      int a = sl;
+      for (int t = 0; t < sl; ++t)
+        if (posl[t] >= 0 && same(cpl[t], me)) { a = t; break; }
+      alias[sl] = a;
+    }
   }
   wave_sync();
   if (c == 0) {
     int n = 0;
     if (active) {
-      for (int k = 0; k < C; ++k) if (posl[k] >= 0) slots[n++] = k;
-      slots[n++] = C;
+      for (int k = 0; k <= C; ++k) if (alias[k] == k) slots[n++] = k;
       if (fast) patch_lds_sums(pw, sums_all[ps * 4 + 0], sums_all[ps * 4 + 1], sums_all[ps * 4 + 2]);
     }
     misc[1] = n;
@@ -336,10 +361,18 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_strong_coop(const PassCo
       const int slot = iq[C + 16 + nv + r], v = j / S + 1;
       const int cq = list[wbase + q];
       const int qx = cq % W, qy = cq / W;
-      const float4 pl = slot < C ? planes_s[iq[slot]] : planes_s[cq];
+      const float4 pl = cpl_all[q * (C + 1) + slot];
       const float* sm = sums_all + q * 4;
       cost_all[(q * (C + 1) + slot) * nv + v - 1] =
           ncc_old_any<U8>(fast, pw_all + q * 108, sm[0], sm[1], sm[2], qx, qy, pc, B, v, pl);
+    }
+  }
+  wave_sync();
+  if (active) {                                          // duplicates take their original's vector
+    for (int sl = c; sl <= C; sl += C) {
+      const int a = alias[sl];
+      if (a >= 0 && a != sl)
+        for (int v = 0; v < nv; ++v) cost[sl * nv + v] = cost[a * nv + v];
     }
   }
   wave_sync();
