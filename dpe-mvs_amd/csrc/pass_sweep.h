@@ -679,7 +679,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassCons
   int* misc = (int*)(pb + 424);                          // 0 nsel, 1 ncand, 2 skip, 3 tsv, 4 wnorm, 8..15 flags
   short2* nbl = (short2*)(pb + 440);                     // [9]
   uint32_t* nsv = (uint32_t*)(pb + 452);                 // [9]
-  int* cand = (int*)(pb + 464);                          // [8] flagged candidate rows
+  int* alias = (int*)(pb + 464);                         // [8] earlier row with a bitwise-identical plane
   uint8_t* vwl = (uint8_t*)(pb + 472);                   // [32] view weights
   float* cost = pb + 480;                                // [8][nv]
   float* sp = cost + 8 * nv;                             // [nv]
@@ -753,22 +753,39 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassCons
       }
       sums[3 * k] = a_ref; sums[3 * k + 1] = a_rr; sums[3 * k + 2] = a_w;
     }
-    if (c == C - 1) {
-      if (fast_old) patch_lds_sums(pw, osum[0], osum[1], osum[2]);
-      int nc = 0;
-      for (int i = 0; i < 8; ++i) if (misc[8 + i]) cand[nc++] = i;
-      misc[1] = nc;
+    if (c == C - 1 && fast_old) patch_lds_sums(pw, osum[0], osum[1], osum[2]);
+    // bitwise-identical neighbour planes share one cost vector: alias = first earlier flagged row
+    // with the same plane (lanes 8..15; lanes 0..8 build the sums above)
+    for (int i = c - 8; i >= 0 && i < 8; i += C) {
+      int a = i;
+      if (misc[8 + i]) {
+        const float4 me = cpl[i];
+        for (int t = 0; t < i; ++t)
+          if (misc[8 + t] && __float_as_uint(cpl[t].x) == __float_as_uint(me.x) &&
+              __float_as_uint(cpl[t].y) == __float_as_uint(me.y) && __float_as_uint(cpl[t].z) == __float_as_uint(me.z) &&
+              __float_as_uint(cpl[t].w) == __float_as_uint(me.w)) { a = t; break; }
+      }
+      alias[i] = a;
     }
   }
   wave_sync();
-  // ---- phase 2: candidate cost vectors, jobs (flagged neighbour, view)
+  // ---- phase 2: candidate cost vectors, jobs (unique flagged neighbour plane, view)
   if (active) {
-    const int ncand = misc[1];
+    uint32_t um = 0;
+    for (int i = 0; i < 8; ++i) if (misc[8 + i] && alias[i] == i) um |= 1u << i;
+    const int ncand = __builtin_popcount(um);
     for (int j = c; j < ncand * nv; j += C) {
-      const int i = cand[j / nv], v = j % nv + 1;
+      uint32_t m = um;
+      for (int q = j / nv; q > 0; --q) m &= m - 1;
+      const int i = __builtin_ctz(m), v = j % nv + 1;
       cost[i * nv + v - 1] = ncc_new_tab<U8>(pc, B, T, x, y, v, cpl[i]);
     }
   }
+  wave_sync();
+  if (active)
+    for (int i = c; i < 8; i += C)
+      if (misc[8 + i] && alias[i] != i)
+        for (int v = 0; v < nv; ++v) cost[i * nv + v] = cost[alias[i] * nv + v];
   wave_sync();
   // ---- phase 3: per-view probabilities with the deformable-neighbour priors (DPE.cu:1768-1790)
   const float cost_threshold = (float)(0.8 * (double)d_expf((float)(iter * iter) / (-90.0f)));
