@@ -24,6 +24,22 @@ using namespace dpe;
 
 static const int kDefaultXcdRows = 1;
 static constexpr int kWeakLanes = 16;   // lanes per weak pixel in k_weak_coop
+// source-image layout of each kernel for 8-bit grey-level images (pass_common.h TEX_*): TEX_F16
+// issues fewer VALU ops per tap, TEX_U8 touches half the bytes (better for scattered gathers)
+#ifndef DPE_TEX_STRONG
+#define DPE_TEX_STRONG TEX_F16
+#endif
+#ifndef DPE_TEX_WEAK
+#define DPE_TEX_WEAK TEX_U8
+#endif
+#ifndef DPE_TEX_D2W
+#define DPE_TEX_D2W TEX_F16
+#endif
+#ifndef DPE_TEX_LR
+#define DPE_TEX_LR TEX_U8
+#endif
+static constexpr int kTexInit = TEX_U8, kTexStrong = DPE_TEX_STRONG, kTexWeak = DPE_TEX_WEAK;
+static constexpr int kTexD2W = DPE_TEX_D2W, kTexLR = DPE_TEX_LR;
 
 namespace {
 
@@ -70,7 +86,8 @@ struct DpeContext {
   // inputs
   DevArr<float> img_plain[DPE_MAX_IMAGES];  // plain f32 images (ref used directly)
   DevArr<float4> imgq[DPE_MAX_IMAGES];
-  DevArr<uint32_t> imgq8_all;        // all u8 quad images, one allocation (32-bit tap offsets)
+  DevArr<uint32_t> imgq8_all;        // all 8-bit quad images, TEX_U8 layout, one allocation
+  DevArr<uint2> imgq16_all;          //   and TEX_F16 layout (32-bit tap offsets)
   bool img8 = false;                 // all images are 8-bit grey levels -> u8 quad layout
   DevArr<float> depth[DPE_MAX_IMAGES];
   DevArr<uint8_t> edge, edge_low;
@@ -148,6 +165,7 @@ void dpe_destroy(DpeContext* c) {
   c->dc.release();
   for (int i = 0; i < DPE_MAX_IMAGES; ++i) { c->img_plain[i].release(); c->imgq[i].release(); c->depth[i].release(); }
   c->imgq8_all.release();
+  c->imgq16_all.release();
   c->edge.release(); c->edge_low.release(); c->label.release();
   c->planes0.release(); c->weak0.release(); c->sel0.release();
   c->planes.release(); c->planes_snap.release(); c->fit_plane.release();
@@ -263,6 +281,7 @@ extern "C" int dpe_pm_stage(DpeContext* c, const DpePassInput* in, const DpePass
       if (!(v >= 0.0f && v <= 255.0f) || v != (float)(int)v) { img8 = false; break; }
     }
   }
+  if ((size_t)(W + 2) * (H + 2) * 8 * N >= (1ull << 32)) img8 = false;   // 32-bit tap offsets
   c->img8 = img8;
   for (int i = 0; i < N; ++i) {
     HIPC(c->img_plain[i].ensure(L));
@@ -270,11 +289,13 @@ extern "C" int dpe_pm_stage(DpeContext* c, const DpePassInput* in, const DpePass
     if (img8) {
       const size_t plane = (size_t)(W + 2) * (H + 2);
       HIPC(c->imgq8_all.ensure(plane * N));
-      uint32_t* q8 = c->imgq8_all.p + plane * i;
-      k_build_quad8<<<qg, qb, 0, c->stream>>>(c->img_plain[i].p, q8, W, H);
-      B.imgq8[i] = q8;
+      HIPC(c->imgq16_all.ensure(plane * N));
+      k_build_quad8<<<qg, qb, 0, c->stream>>>(c->img_plain[i].p, c->imgq8_all.p + plane * i,
+                                              c->imgq16_all.p + plane * i, W, H);
       B.img8 = (const uint8_t*)c->imgq8_all.p;
       B.img8_view = (uint32_t)(plane * 4);
+      B.img16 = (const uint8_t*)c->imgq16_all.p;
+      B.img16_view = (uint32_t)(plane * 8);
     } else {
       HIPC(c->imgq[i].ensure((size_t)(W + 2) * (H + 2)));
       k_build_quad<<<qg, qb, 0, c->stream>>>(c->img_plain[i].p, c->imgq[i].p, W, H);
@@ -403,7 +424,7 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   k_list_fill<0><<<(pc.half_rows + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p, c->lists.p, list_stride);
   end();
   Bc = begin(DPE_CLASS_INIT);
-  if (c->img8) k_random_init<true><<<fg, fb, 0, s>>>(dpc, Bc); else k_random_init<false><<<fg, fb, 0, s>>>(dpc, Bc);
+  if (c->img8) k_random_init<kTexInit><<<fg, fb, 0, s>>>(dpc, Bc); else k_random_init<TEX_F32><<<fg, fb, 0, s>>>(dpc, Bc);
   end();
   HIPC(hipGetLastError());
   for (int it = 0; it < pc.P.max_iterations; ++it) {
@@ -420,11 +441,11 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
         const size_t lds = (size_t)4 * strong_lds_per_wave(P, C, nv) * sizeof(float);
         const unsigned grid = (unsigned)((L / 2 + 1 + 4 * P - 1) / (4 * P));
         if (edge) {
-          if (c->img8) k_strong_coop<true, true><<<grid, 256, lds, s>>>(dpc, Bc, it, lst, cnt);
-          else k_strong_coop<false, true><<<grid, 256, lds, s>>>(dpc, Bc, it, lst, cnt);
+          if (c->img8) k_strong_coop<kTexStrong, true><<<grid, 256, lds, s>>>(dpc, Bc, it, lst, cnt);
+          else k_strong_coop<TEX_F32, true><<<grid, 256, lds, s>>>(dpc, Bc, it, lst, cnt);
         } else {
-          if (c->img8) k_strong_coop<true, false><<<grid, 256, lds, s>>>(dpc, Bc, it, lst, cnt);
-          else k_strong_coop<false, false><<<grid, 256, lds, s>>>(dpc, Bc, it, lst, cnt);
+          if (c->img8) k_strong_coop<kTexStrong, false><<<grid, 256, lds, s>>>(dpc, Bc, it, lst, cnt);
+          else k_strong_coop<TEX_F32, false><<<grid, 256, lds, s>>>(dpc, Bc, it, lst, cnt);
         }
       }
       end();
@@ -442,8 +463,8 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
         const size_t per_wave = (size_t)P * weak_lds_per_pixel(nv) * sizeof(float);
         const int wpb = per_wave * 4 <= 64 * 1024 ? 4 : (per_wave * 2 <= 64 * 1024 ? 2 : 1);
         const unsigned grid = (unsigned)((L / 2 + 1 + wpb * P - 1) / (wpb * P));
-        if (c->img8) k_weak_coop<true, C><<<grid, 64 * wpb, per_wave * wpb, s>>>(dpc, Bc, it, lst, cnt);
-        else k_weak_coop<false, C><<<grid, 64 * wpb, per_wave * wpb, s>>>(dpc, Bc, it, lst, cnt);
+        if (c->img8) k_weak_coop<kTexWeak, C><<<grid, 64 * wpb, per_wave * wpb, s>>>(dpc, Bc, it, lst, cnt);
+        else k_weak_coop<TEX_F32, C><<<grid, 64 * wpb, per_wave * wpb, s>>>(dpc, Bc, it, lst, cnt);
       }
       end();
     }
@@ -454,15 +475,15 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   for (int colour = 0; colour < 2; ++colour) k_filter<<<hg, hb, 0, s>>>(dpc, Bc, colour);
   end();
   Bc = begin(DPE_CLASS_DEPTH_TO_WEAK);
-  if (c->img8) k_depth_to_weak<true><<<(unsigned)((L + 3) / 4), 256, 0, s>>>(dpc, Bc);
-  else k_depth_to_weak<false><<<(unsigned)((L + 3) / 4), 256, 0, s>>>(dpc, Bc);
+  if (c->img8) k_depth_to_weak<kTexD2W><<<(unsigned)((L + 3) / 4), 256, 0, s>>>(dpc, Bc);
+  else k_depth_to_weak<TEX_F32><<<(unsigned)((L + 3) / 4), 256, 0, s>>>(dpc, Bc);
   end();
   Bc = begin(DPE_CLASS_LOCAL_REFINE);
   {
     const unsigned g = (unsigned)((L + 4 * kLrPix - 1) / (4 * kLrPix));
     const size_t lds = (size_t)4 * kLrPix * 12 * nv * 2 * sizeof(float);
-    if (c->img8) k_local_refine_jobs<true><<<g, 256, lds, s>>>(dpc, Bc);
-    else k_local_refine_jobs<false><<<g, 256, lds, s>>>(dpc, Bc);
+    if (c->img8) k_local_refine_jobs<kTexLR><<<g, 256, lds, s>>>(dpc, Bc);
+    else k_local_refine_jobs<TEX_F32><<<g, 256, lds, s>>>(dpc, Bc);
   }
   end();
   HIPC(hipGetLastError());

@@ -36,9 +36,10 @@ struct PassConst {
 
 struct DevBufs {
   const float4* imgq[DPE_MAX_IMAGES];     // f32 quad-texel images (any grey levels)
-  const uint32_t* imgq8[DPE_MAX_IMAGES];  // u8 quad-texel images (8-bit grey levels: same values, 4 B/tap)
-  const uint8_t* img8;                    // == imgq8[0]: all u8 quad images in one allocation,
-  uint32_t img8_view;                     //   view v at byte offset v * img8_view (< 4 GiB: 32-bit offsets)
+  // 8-bit grey-level images as quad texels in the two layouts below (TEX_U8, TEX_F16), each with
+  // all views in one allocation, view v at byte offset v * view bytes (< 4 GiB: 32-bit offsets)
+  const uint8_t* img8; uint32_t img8_view;
+  const uint8_t* img16; uint32_t img16_view;
   const float* depth[DPE_MAX_IMAGES];
   const float* ref;
   float4* planes; float4* planes_snap; float4* fit_plane;
@@ -236,20 +237,48 @@ DEV float sample_quad(const float4* __restrict__ q, int W, int H, float sx, floa
   const float r1 = __builtin_fmaf(ax, t.w - t.z, t.z);
   return __builtin_fmaf(ay, r1 - r0, r0);
 }
-// Same sampler on the u8 quad image: the four grey levels are exact small integers, so the floats
-// fed to the interpolation are identical to the f32 layout's.
-DEV float sample_quad8(const uint32_t* __restrict__ q, int W, int H, float sx, float sy) {
+// Source-image layouts, the kernels' `U8` template argument: TEX_F32 is the f32 quad image (any
+// grey levels); the other two hold 8-bit grey levels.  A quad texel holds the 2x2 neighbourhood
+// a=(x0,y0), b=(x1,y0), c=(x0,y1), d=(x1,y1) of its bilinear footprint:
+//   TEX_U8:  4 B, bytes (a, b, c, d)
+//   TEX_F16: 8 B, f16 (a, c, (b-a)/256, (d-c)/256): all exact (integers <= 255 and their
+//     differences scaled by a power of two), so fma(fx, (b-a)/256, a) with the raw 8-bit fraction
+//     fx equals the reference's fma(fx/256, b-a, a) bit for bit (the products are the same real
+//     number), and each row interpolation is one v_fma_mix_f32 on the loaded halves: 7 fewer
+//     VALU ops per tap than TEX_U8 for twice the bytes.
+enum { TEX_F32 = 0, TEX_U8 = 1, TEX_F16 = 2 };
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+template <int T> DEV const uint8_t* tex_base(const DevBufs& B) { return T == TEX_F16 ? B.img16 : B.img8; }
+template <int T> DEV uint32_t tex_view(const DevBufs& B) { return T == TEX_F16 ? B.img16_view : B.img8_view; }
+template <int T> constexpr uint32_t tex_bytes() { return T == TEX_F16 ? 8u : 4u; }
+// the two row interpolations (r0 at y0, r1 at y1) of the texel at `p` for the raw x fraction fx
+template <int T>
+DEV void texel_rows(const uint8_t* p, float fx, float& r0, float& r1) {
+  if constexpr (T == TEX_F16) {
+    // v_fma_mix_f32 is fma(fx, (float)half, (float)half) with one rounding; the compiler only forms
+    // it under f32 denormal flushing, which cannot matter here (|fx*d| >= 2^-8 or 0, a integer)
+    const uint2 t = *(const uint2*)p;
+    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(r0) : "v"(fx), "v"(t.y), "v"(t.x));
+    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[0,1,1] op_sel_hi:[0,1,1]" : "=v"(r1) : "v"(fx), "v"(t.y), "v"(t.x));
+  } else {
+    const uint32_t t = *(const uint32_t*)p;
+    const float ax = fx * 0.00390625f;
+    const float t00 = (float)(t & 255u), t10 = (float)((t >> 8) & 255u);
+    const float t01 = (float)((t >> 16) & 255u), t11 = (float)(t >> 24);
+    r0 = __builtin_fmaf(ax, t10 - t00, t00);
+    r1 = __builtin_fmaf(ax, t11 - t01, t01);
+  }
+}
+// Same sampler on the 8-bit quad texels of one view: identical values to the f32 layout's.
+template <int T>
+DEV float sample_quad8(const uint8_t* __restrict__ q, int W, int H, float sx, float sy) {
   const float xb = __builtin_fminf(__builtin_fmaxf(sx, -1.0f), (float)W);
   const float yb = __builtin_fminf(__builtin_fmaxf(sy, -1.0f), (float)H);
   const int ux = (int)__builtin_fmaf(xb, 256.0f, 256.5f);
   const int uy = (int)__builtin_fmaf(yb, 256.0f, 256.5f);
-  const float ax = (float)(ux & 255) * 0.00390625f;
   const float ay = (float)(uy & 255) * 0.00390625f;
-  const uint32_t t = q[(uy >> 8) * (W + 2) + (ux >> 8)];
-  const float t00 = (float)(t & 255u), t10 = (float)((t >> 8) & 255u);
-  const float t01 = (float)((t >> 16) & 255u), t11 = (float)(t >> 24);
-  const float r0 = __builtin_fmaf(ax, t10 - t00, t00);
-  const float r1 = __builtin_fmaf(ax, t11 - t01, t01);
+  float r0, r1;
+  texel_rows<T>(q + (size_t)((uy >> 8) * (W + 2) + (ux >> 8)) * tex_bytes<T>(), (float)(ux & 255), r0, r1);
   return __builtin_fmaf(ay, r1 - r0, r0);
 }
 // Minimum waves per SIMD the tap-heavy kernels are compiled for (register cap 512 / waves).
@@ -269,10 +298,11 @@ typedef float f2v __attribute__((ext_vector_type(2)));
 DEV f2v f2s(float a) { return (f2v){a, a}; }
 DEV f2v fma2(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
 
-// One bilinear tap of the u8 quad image whose byte offset is `vofs`, at the projection of the tap
-// (row terms bxy = (h0 x + h2, h3 x + h5), bz = h6 x + h8; column yf).  Bit-identical to
-// sample_quad8(project) when the tap's qz is in d_rcp_fast's exact range (rcp_range_ok), with
-// packed FP32 ops, one med3 per clamp and a 32-bit offset from one uniform base.
+// One bilinear tap of the 8-bit quad image (layout T) whose byte offset is `vofs`, at the
+// projection of the tap (row terms bxy = (h0 x + h2, h3 x + h5), bz = h6 x + h8; column yf).
+// Bit-identical to sample_quad8(project) when the tap's qz is in d_rcp_fast's exact range
+// (rcp_range_ok), with packed FP32 ops, one med3 per clamp and a 32-bit offset from one base.
+template <int T>
 DEV float tap_u8_fast(const DevBufs& B, uint32_t vofs, uint32_t stride, f2v lim, const float* h, f2v bxy, float bz,
                       float yf) {
   const f2v q = fma2((f2v){h[1], h[4]}, f2s(yf), bxy);
@@ -282,17 +312,24 @@ DEV float tap_u8_fast(const DevBufs& B, uint32_t vofs, uint32_t stride, f2v lim,
   const float yb = __builtin_amdgcn_fmed3f(sxy.y, -1.0f, lim.y);
   const f2v u = fma2((f2v){xb, yb}, f2s(256.0f), f2s(256.5f));
   const uint32_t ux = (uint32_t)(int)u.x, uy = (uint32_t)(int)u.y;       // >= 0 after the clamp
-  const uint32_t t = *(const uint32_t*)(B.img8 + (vofs + (__umul24(uy >> 8, stride) + (ux >> 8)) * 4u));
-  const float ax = (float)(ux & 255u) * 0.00390625f;
+  const uint8_t* p = tex_base<T>(B) + (vofs + (__umul24(uy >> 8, stride) + (ux >> 8)) * tex_bytes<T>());
   const float ay = (float)(uy & 255u) * 0.00390625f;
-  const f2v lo = (f2v){(float)(t & 255u), (float)((t >> 16) & 255u)};
-  const f2v hi = (f2v){(float)((t >> 8) & 255u), (float)(t >> 24)};
-  const f2v r = fma2(f2s(ax), hi - lo, lo);
-  return __builtin_fmaf(ay, r.y - r.x, r.x);
+  if constexpr (T == TEX_F16) {
+    float r0, r1;
+    texel_rows<T>(p, (float)(ux & 255u), r0, r1);
+    return __builtin_fmaf(ay, r1 - r0, r0);
+  } else {
+    const uint32_t t = *(const uint32_t*)p;
+    const float ax = (float)(ux & 255u) * 0.00390625f;
+    const f2v lo = (f2v){(float)(t & 255u), (float)((t >> 16) & 255u)};
+    const f2v hi = (f2v){(float)((t >> 8) & 255u), (float)(t >> 24)};
+    const f2v r = fma2(f2s(ax), hi - lo, lo);
+    return __builtin_fmaf(ay, r.y - r.x, r.x);
+  }
 }
 
-template <bool U8> DEV float sample_src(const DevBufs& B, int v, int W, int H, float sx, float sy) {
-  if constexpr (U8) return sample_quad8(B.imgq8[v], W, H, sx, sy);
+template <int U8> DEV float sample_src(const DevBufs& B, int v, int W, int H, float sx, float sy) {
+  if constexpr (U8 != TEX_F32) return sample_quad8<U8>(tex_base<U8>(B) + (size_t)v * tex_view<U8>(B), W, H, sx, sy);
   else return sample_quad(B.imgq[v], W, H, sx, sy);
 }
 
@@ -321,7 +358,7 @@ DEV float ncc_finalize(float s_ref, float s_rr, float s_w, float s_src, float s_
 
 // Generic bilateral NCC of one patch, weights computed per tap (NCC-New neighbour patches and
 // non-default radius/increment).  Same arithmetic order as the oracle's PatchNCC.
-template <bool U8, bool FAST>
+template <int U8, bool FAST>
 DEV void generic_taps(const PassConst& pc, const DevBufs& B, int v, const Homog& H, int cx, int cy, float rcp,
                       int radius, int increment, float* acc) {
   const int W = pc.W, Hh = pc.H;
@@ -359,7 +396,7 @@ DEV void generic_taps(const PassConst& pc, const DevBufs& B, int v, const Homog&
 
 // Generic bilateral NCC of one patch, weights computed per tap (NCC-New neighbour patches and
 // non-default radius/increment).  Same arithmetic order as the oracle's PatchNCC.
-template <bool U8>
+template <int U8>
 DEV float patch_ncc_generic(const PassConst& pc, const DevBufs& B, int v, const Homog& H,
                             int cx, int cy, float rcp, int radius, int increment) {
   float a[6];
@@ -378,7 +415,7 @@ DEV bool center_outside(const PassConst& pc, int v, const Homog& H, int px, int 
 }
 
 // ComputeBilateralNCCOld (DPE.cu:692-778), weights per tap.
-template <bool U8>
+template <int U8>
 DEV float ncc_old_generic(const PassConst& pc, const DevBufs& B, int px, int py, int v, const float4& pl) {
   const Homog H = make_homography(pc, v, pl);
   count_work(B, 1, 0);
@@ -420,7 +457,7 @@ DEV void make_patch36(Patch36& P, const PassConst& pc, const DevBufs& B, int px,
   }
   P.s_ref = s_ref; P.s_rr = s_rr; P.s_w = s_w;
 }
-template <bool U8, bool FAST>
+template <int U8, bool FAST>
 DEV void patch36_taps(const Patch36& P, const PassConst& pc, const DevBufs& B, int v, const Homog& H, float* acc) {
   const int W = pc.W, Hh = pc.H;
   float s_src = 0, s_ss = 0, s_rs = 0;
@@ -448,7 +485,7 @@ DEV void patch36_taps(const Patch36& P, const PassConst& pc, const DevBufs& B, i
   }
   acc[0] = s_src; acc[1] = s_ss; acc[2] = s_rs;
 }
-template <bool U8>
+template <int U8>
 DEV float ncc_old_patch36(const Patch36& P, const PassConst& pc, const DevBufs& B, int v, const float4& pl) {
   const Homog H = make_homography(pc, v, pl);
   if (center_outside(pc, v, H, P.px, P.py)) { count_work(B, 1, 0); return 2.0f; }
@@ -462,14 +499,14 @@ DEV float ncc_old_patch36(const Patch36& P, const PassConst& pc, const DevBufs& 
 }
 
 // Old NCC through the cached patch when the pass uses the default 5/2 patch, else generic.
-template <bool U8>
+template <int U8>
 DEV float ncc_old(const Patch36& P, bool fast, const PassConst& pc, const DevBufs& B, int v, const float4& pl) {
   if (fast) return ncc_old_patch36<U8>(P, pc, B, v, pl);
   return ncc_old_generic<U8>(pc, B, P.px, P.py, v, pl);
 }
 
 // ComputeBilateralNCCNew (DPE.cu:557-690)
-template <bool U8>
+template <int U8>
 DEV float ncc_new(const PassConst& pc, const DevBufs& B, int px, int py, int v, const float4& pl) {
   const int W = pc.W, Hh = pc.H;
   const int center = px + py * W;

@@ -372,7 +372,7 @@ __global__ void k_neighbour_update(const PassConst* __restrict__ pcp, DevBufs B)
 }
 
 // ------------------------------------------------------------------------------ RandomInitialization
-template <bool U8>
+template <int U8>
 __global__ void __launch_bounds__(256) k_random_init(const PassConst* __restrict__ pcp, DevBufs B) {   // DPE.cu:1035-1063
   const PassConst& pc = *pcp;
   PIX2D_FULL();
@@ -625,16 +625,20 @@ __global__ void k_filter(const PassConst* __restrict__ pcp, DevBufs B, int colou
 }
 
 // ------------------------------------------------------------------------------ staging kernels
-// u8 padded quad-texel image (images that are 8-bit grey levels)
-__global__ void k_build_quad8(const float* __restrict__ img, uint32_t* __restrict__ q, int W, int H) {
+// padded quad-texel images of 8-bit grey levels, both layouts (pass_common.h: TEX_U8, TEX_F16)
+__global__ void k_build_quad8(const float* __restrict__ img, uint32_t* __restrict__ q8, uint2* __restrict__ q16,
+                              int W, int H) {
   const int X = blockIdx.x * blockDim.x + threadIdx.x;
   const int Y = blockIdx.y * blockDim.y + threadIdx.y;
   if (X > W + 1 || Y > H + 1) return;
   auto cl = [](int v, int n) { return v < 0 ? 0 : (v > n - 1 ? n - 1 : v); };
   const int x0 = cl(X - 1, W), x1 = cl(X, W), y0 = cl(Y - 1, H), y1 = cl(Y, H);
-  const uint32_t a = (uint32_t)img[y0 * W + x0], b = (uint32_t)img[y0 * W + x1];
-  const uint32_t c = (uint32_t)img[y1 * W + x0], d = (uint32_t)img[y1 * W + x1];
-  q[Y * (W + 2) + X] = a | (b << 8) | (c << 16) | (d << 24);
+  const float a = img[y0 * W + x0], b = img[y0 * W + x1], c = img[y1 * W + x0], d = img[y1 * W + x1];
+  const size_t o = (size_t)Y * (W + 2) + X;
+  q8[o] = (uint32_t)a | ((uint32_t)b << 8) | ((uint32_t)c << 16) | ((uint32_t)d << 24);
+  const h2v lo = (h2v){(_Float16)a, (_Float16)c};
+  const h2v df = (h2v){(_Float16)((b - a) * 0.00390625f), (_Float16)((d - c) * 0.00390625f)};
+  q16[o] = make_uint2(__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, df));
 }
 // padded quad-texel image (see pass_common.h)
 __global__ void k_build_quad(const float* __restrict__ img, float4* __restrict__ q, int W, int H) {

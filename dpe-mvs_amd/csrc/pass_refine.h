@@ -50,13 +50,13 @@ DEV void patch_lds_sums(const float* pw, float& s_ref, float& s_rr, float& s_w) 
   s_ref = a_ref; s_rr = a_rr; s_w = a_w;
 }
 // Old NCC with the patch read from LDS (same arithmetic as ncc_old_patch36)
-template <bool U8, bool FAST>
+template <int U8, bool FAST>
 DEV void lds_taps(const float* pw, int px, int py, const PassConst& pc, const DevBufs& B, int v, const Homog& H,
                   float* acc) {
   const int W = pc.W, Hh = pc.H;
-  if constexpr (U8 && FAST && DPE_PACKED_TAP) {
+  if constexpr (U8 != TEX_F32 && FAST && DPE_PACKED_TAP) {
     // packed form: (r_src, r_rs) accumulate as one pair; weights are (w, w*grey) pairs in LDS
-    const uint32_t vofs = (uint32_t)v * B.img8_view, stride = (uint32_t)(W + 2);
+    const uint32_t vofs = (uint32_t)v * tex_view<U8>(B), stride = (uint32_t)(W + 2);
     const f2v lim = (f2v){(float)W, (float)Hh};
     const f2v* wp = (const f2v*)pw;
     f2v s_sr = f2s(0.0f);
@@ -74,7 +74,7 @@ DEV void lds_taps(const float* pw, int px, int py, const PassConst& pc, const De
       float r_ss = 0;
 #pragma unroll
       for (int b = 0; b < 6; ++b) {
-        const float sp = tap_u8_fast(B, vofs, stride, lim, H.h, bxy, bz, (float)(py - 5 + 2 * b));
+        const float sp = tap_u8_fast<U8>(B, vofs, stride, lim, H.h, bxy, bz, (float)(py - 5 + 2 * b));
         const f2v w = wp[a * 6 + b];
         r_sr = fma2(w, f2s(sp), r_sr);
         const float ws = w.x * sp;
@@ -110,7 +110,7 @@ DEV void lds_taps(const float* pw, int px, int py, const PassConst& pc, const De
     acc[0] = s_src; acc[1] = s_ss; acc[2] = s_rs;
   }
 }
-template <bool U8>
+template <int U8>
 DEV float ncc_old_lds(const float* pw, float s_ref, float s_rr, float s_w, int px, int py, const PassConst& pc,
                       const DevBufs& B, int v, const float4& pl) {
   const Homog H = make_homography(pc, v, pl);
@@ -124,7 +124,7 @@ DEV float ncc_old_lds(const float* pw, float s_ref, float s_rr, float s_w, int p
   return ncc_finalize(s_ref, s_rr, s_w, a[0], a[1], a[2]);
 }
 
-template <bool U8>
+template <int U8>
 DEV float ncc_old_any(bool fast, const float* pw, float s_ref, float s_rr, float s_w, int px, int py,
                       const PassConst& pc, const DevBufs& B, int v, const float4& pl) {
   if (fast) return ncc_old_lds<U8>(pw, s_ref, s_rr, s_w, px, py, pc, B, v, pl);
@@ -151,7 +151,7 @@ DEV void baseline_and_weights(const PassConst& pc, uint32_t sel, const uint8_t* 
 
 // ------------------------------------------------------------------------------ DepthToWeak
 // grid: one wave per pixel, 4 waves per 256-thread workgroup.
-template <bool U8>
+template <int U8>
 __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_depth_to_weak(const PassConst* __restrict__ pcp, DevBufs B) {   // DPE.cu:2593-2747
   __shared__ float s_patch[4][108];
   __shared__ float s_pc[4][64];
@@ -240,7 +240,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_depth_to_weak(const Pass
 // view counts are.  Per-hypothesis sums over views then run on one lane each, in ascending view
 // order (the reference's si loop), and the arg-min on the pixel's first lane.
 constexpr int kLrPix = 4;
-template <bool U8>
+template <int U8>
 __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_local_refine_jobs(const PassConst* __restrict__ pcp, DevBufs B) {   // DPE.cu:2749-2835
   __shared__ float s_patch[4][kLrPix][108];
   __shared__ float s_sum[4][kLrPix][3];

@@ -256,7 +256,7 @@ DEV bool job_decode(const int* cnt, int j, int& p, int& r) {
   return false;
 }
 
-template <bool U8, bool EDGE>
+template <int U8, bool EDGE>
 __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_strong_coop(const PassConst* __restrict__ pcp, DevBufs B, int iter,
                                                      const int* __restrict__ list, const int* __restrict__ nlist_p) {
   extern __shared__ float4 lds4[];
@@ -541,13 +541,13 @@ struct WeakTab {
 };
 
 // patch NCC with tabulated weights; the same tap order and arithmetic as patch_ncc_generic
-template <bool U8, bool FAST>
+template <int U8, bool FAST>
 DEV void tab_taps(const PassConst& pc, const DevBufs& B, int v, const Homog& H, int cx, int cy, int rad, int inc,
                   int n, const float* __restrict__ tw, float* acc) {
   const int W = pc.W, Hh = pc.H;
   const f2v* wp = (const f2v*)tw;            // (w, w*grey) pairs
-  if constexpr (U8 && FAST && DPE_PACKED_TAP) {
-    const uint32_t vofs = (uint32_t)v * B.img8_view, stride = (uint32_t)(W + 2);
+  if constexpr (U8 != TEX_F32 && FAST && DPE_PACKED_TAP) {
+    const uint32_t vofs = (uint32_t)v * tex_view<U8>(B), stride = (uint32_t)(W + 2);
     const f2v lim = (f2v){(float)W, (float)Hh};
     f2v s_sr = f2s(0.0f);
     float s_ss = 0;
@@ -558,7 +558,7 @@ DEV void tab_taps(const PassConst& pc, const DevBufs& B, int v, const Homog& H, 
       f2v r_sr = f2s(0.0f);
       float r_ss = 0;
       for (int b = 0; b < n; ++b) {
-        const float sp = tap_u8_fast(B, vofs, stride, lim, H.h, bxy, bz, (float)(cy - rad + b * inc));
+        const float sp = tap_u8_fast<U8>(B, vofs, stride, lim, H.h, bxy, bz, (float)(cy - rad + b * inc));
         const f2v w = wp[a * n + b];
         r_sr = fma2(w, f2s(sp), r_sr);
         const float ws = w.x * sp;
@@ -592,7 +592,7 @@ DEV void tab_taps(const PassConst& pc, const DevBufs& B, int v, const Homog& H, 
     acc[0] = s_src; acc[1] = s_ss; acc[2] = s_rs;
   }
 }
-template <bool U8>
+template <int U8>
 DEV float patch_ncc_tab(const PassConst& pc, const DevBufs& B, int v, const Homog& H, int cx, int cy, int rad, int inc,
                         int n, const float* __restrict__ tw, const float* sm) {
   float a[3];
@@ -605,7 +605,7 @@ DEV float patch_ncc_tab(const PassConst& pc, const DevBufs& B, int v, const Homo
 }
 
 // ComputeBilateralNCCNew (DPE.cu:557-690) of the tabulated weak pixel (px, py)
-template <bool U8>
+template <int U8>
 DEV float ncc_new_tab(const PassConst& pc, const DevBufs& B, const WeakTab& T, int px, int py, int v, const float4& pl) {
   const int W = pc.W, Hh = pc.H;
   const Homog H = make_homography(pc, v, pl);
@@ -647,7 +647,7 @@ __host__ __device__ inline int weak_lds_per_pixel(int nv) { return (480 + 17 * n
 
 // CheckerboardPropagationWeak (DPE.cu:1668-1862) + PlaneHypothesisRefinementWeak (:1120-1212).
 // C lanes per pixel, 64/C pixels per wave, blockDim.x/64 waves per workgroup.
-template <bool U8, int C>
+template <int U8, int C>
 __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassConst* __restrict__ pcp, DevBufs B, int iter,
                                                    const int* __restrict__ list, const int* __restrict__ nlist_p) {
   extern __shared__ float4 lds4[];
