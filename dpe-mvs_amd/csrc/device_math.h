@@ -155,9 +155,19 @@ DEV uint32_t rng_u32(Rng& s) {
   const int i = s.idx++;
   return i == 0 ? s.b0 : (i == 1 ? s.b1 : (i == 2 ? s.b2 : s.b3));
 }
-DEV float rng_uniform(Rng& s) {
-  const uint32_t u = rng_u32(s);
-  return (float)u * 2.32830644e-10f + 1.16415322e-10f;
+DEV float u32_to_uniform(uint32_t u) { return (float)u * 2.32830644e-10f + 1.16415322e-10f; }
+DEV float rng_uniform(Rng& s) { return u32_to_uniform(rng_u32(s)); }
+// word n of the stream (draws are position-addressable: word n = word n%4 of Philox block n/4)
+DEV uint32_t rng_word(const Rng& s, uint32_t n) {
+  uint32_t c0 = n >> 2, c1 = s.stream, c2 = s.salt, c3 = 0u;
+  philox10(c0, c1, c2, c3, s.k0, s.k1);
+  const uint32_t i = n & 3u;
+  return i == 0 ? c0 : (i == 1 ? c1 : (i == 2 ? c2 : c3));
+}
+// position the stream so that the next draw is word n
+DEV void rng_seek(Rng& s, uint32_t n) {
+  s.ctr = n >> 2; s.idx = 4;
+  if (n & 3u) { (void)rng_u32(s); s.idx = (int)(n & 3u); }
 }
 
 enum { STREAM_GEN_NEIGHBOURS = 1, STREAM_RANDOM_INIT = 2, STREAM_ITER_BASE = 16 };

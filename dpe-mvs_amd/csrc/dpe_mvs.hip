@@ -81,6 +81,7 @@ struct DpeContext {
   unsigned long long counts[DPE_NUM_CLASSES * 4] = {0};
   hipEvent_t ev[2 * 64] = {};
   DevArr<unsigned long long> cnt;
+  DevArr<unsigned long long> phase;  // DPE_PHASE_PROF builds: per-phase cycle sums
   PassConst hc;                  // host copy of the pass constants
   DevArr<PassConst> dc;
   // inputs
@@ -365,6 +366,11 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
     const char* e = getenv("DPE_XCD_ROWS");
     B.xcd_rows = e ? atoi(e) : kDefaultXcdRows;
   }
+#if DPE_PHASE_PROF
+  HIPC(c->phase.ensure(32 * 64));
+  HIPC(hipMemsetAsync(c->phase.p, 0, 32 * 64 * sizeof(unsigned long long), s));
+  B.phase = c->phase.p;
+#endif
   if (c->counting) {
     HIPC(c->cnt.ensure(DPE_NUM_CLASSES * 4));
     HIPC(hipMemsetAsync(c->cnt.p, 0, DPE_NUM_CLASSES * 4 * sizeof(unsigned long long), s));
@@ -498,6 +504,18 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
       c->timings[1 + ev_class[e]] += ms;
     }
   }
+#if DPE_PHASE_PROF
+  {
+    unsigned long long ph32[32 * 64], ph[64] = {};
+    HIPC(hipMemcpyAsync(ph32, c->phase.p, sizeof(ph32), hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    for (int k = 0; k < 32 * 64; ++k) ph[k % 64] += ph32[k];
+    unsigned long long tot[4] = {0, 0, 0, 0};
+    for (int k = 0; k < 64; ++k) tot[k / 16] += ph[k];
+    for (int k = 0; k < 64; ++k)
+      if (ph[k]) fprintf(stderr, "PHASE %d.%d %.4e cycles %.1f%%\n", k / 16, k % 16, (double)ph[k], 100.0 * ph[k] / tot[k / 16]);
+  }
+#endif
   if (c->counting) {
     HIPC(hipMemcpyAsync(c->counts, c->cnt.p, sizeof(c->counts), hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));

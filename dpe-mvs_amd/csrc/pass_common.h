@@ -52,9 +52,35 @@ struct DevBufs {
   // algorithmic work counters of the launch class (nullptr unless counting):
   // [0] homographies (NCC set-ups), [1] bilinear taps, [2] geometric-consistency evaluations
   unsigned long long* cnt;
+  unsigned long long* phase;              // DPE_PHASE_PROF builds only
   int xcd_rows;   // block rows per XCD chunk (0 = dispatcher order)
 };
 
+// Phase profiling (build with -DDPE_PHASE_PROF=1; tools/phase_prof.sh): shader-clock cycles of
+// each phase of a cooperative kernel, summed over waves into B.phase[k].
+#ifndef DPE_PHASE_PROF
+#define DPE_PHASE_PROF 0
+#endif
+#if DPE_PHASE_PROF
+#define PHASE_BEGIN() uint64_t ph_t_ = __builtin_readcyclecounter(), ph_acc_[16] = {}
+#define PHASE(k)                                                                    \
+  do {                                                                              \
+    const uint64_t n_ = __builtin_readcyclecounter();                               \
+    ph_acc_[k] += n_ - ph_t_;                                                       \
+    ph_t_ = n_;                                                                     \
+  } while (0)
+// per-wave sums go to one of 32 copies of the counters (the host adds them up)
+#define PHASE_END(kernel)                                                           \
+  do {                                                                              \
+    if ((threadIdx.x & 63) == 0 && B.phase)                                         \
+      for (int k_ = 0; k_ < 16; ++k_)                                               \
+        if (ph_acc_[k_]) atomicAdd(B.phase + ((blockIdx.x & 31) * 4 + (kernel)) * 16 + k_, (unsigned long long)ph_acc_[k_]); \
+  } while (0)
+#else
+#define PHASE_BEGIN() do {} while (0)
+#define PHASE(k) do {} while (0)
+#define PHASE_END(kernel) do {} while (0)
+#endif
 DEV void count_work(const DevBufs& B, unsigned long long ncc, unsigned long long taps) {
   if (B.cnt) { atomicAdd(B.cnt + 0, ncc); atomicAdd(B.cnt + 1, taps); }
 }

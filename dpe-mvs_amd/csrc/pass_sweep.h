@@ -127,6 +127,41 @@ DEV void view_sample(const float* sp, int nv, Rng& rs, uint8_t* vw, uint32_t& ts
   tsv = t; wnorm = wn;
 }
 
+// The same sampling on the C lanes of one pixel: the CDF is built in the reference's order on lane
+// 0 (in place of sp), the 15 draws (stream words 0..14) and their CDF searches run one per lane,
+// and the per-view counts are LDS integer atomics (order-free).  cnt: nv ints of scratch.
+// Leaves vwl[0..31] and the global copy vwg[0..31]; the caller's lane-0 stream is then positioned
+// with rng_seek(rs, 15).  Every lane of the wave calls it (wave_sync inside).
+DEV void view_sample_coop(float* sp, int* cnt, int nv, int c, int C, bool active, const Rng& rs, uint8_t* vwl,
+                          uint8_t* vwg) {
+  if (active) {
+    if (c == 0) {
+      float psum = 0.0f;
+      for (int i = 0; i < nv; ++i) psum += sp[i];
+      const float inv = 1.0f / psum;
+      float cum = 0.0f;
+      for (int i = 0; i < nv; ++i) { const float q = sp[i] * inv; cum += q; sp[i] = cum; }
+    }
+    for (int v = c; v < nv; v += C) cnt[v] = 0;
+  }
+  wave_sync();
+  if (active) {
+    for (int s = c; s < 15; s += C) {
+      const float rp = u32_to_uniform(rng_word(rs, (uint32_t)s)) - 1.1920929e-07f;
+      for (int id = 0; id < nv; ++id)
+        if (sp[id] > rp) { atomicAdd(&cnt[id], 1); break; }
+    }
+  }
+  wave_sync();
+  if (active)
+    for (int j = c; j < DPE_MAX_IMAGES; j += C) {
+      const uint8_t w = j < nv ? (uint8_t)cnt[j] : (uint8_t)0;
+      vwl[j] = w;
+      vwg[j] = w;
+    }
+  wave_sync();
+}
+
 // ------------------------------------------------------------------------------ candidate scans
 // Edge-adaptive (kind 0) and fixed 11-step (kind 1) scans of direction d (DPE.cu:1250-1292, 1297-1322).
 DEV int edge_candidate(const PassConst& pc, const DevBufs& B, const float* __restrict__ costs, int x, int y, int center,
@@ -154,12 +189,20 @@ DEV int edge_candidate(const PassConst& pc, const DevBufs& B, const float* __res
   int fx = 0, fy = 0;
   if (d > 4) { if (d % 2) fx = dx; else fy = dy; }
   int mpos = -1; float mc = 3.40282347e+38f;
-  for (int step = 0; step < step_num; ++step) {
-    const int tx = x + s0 * dx + step * step_len * dx + fx, ty = y + s0 * dy + step * step_len * dy + fy;
-    if (!(tx >= 0 && ty >= 0 && tx < W && ty < H)) continue;
-    const int ptc = tx + ty * W;
-    const float c = costs[ptc];
-    if (mc > c) { mpos = ptc; mc = c; }
+  // the loads of 8 steps are issued together, then scanned in step order (same first minimum)
+  for (int s = 0; s < step_num; s += 8) {
+    float cv[8]; int pv[8]; bool ok[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int step = s + u;
+      const int tx = x + s0 * dx + step * step_len * dx + fx, ty = y + s0 * dy + step * step_len * dy + fy;
+      ok[u] = step < step_num && tx >= 0 && ty >= 0 && tx < W && ty < H;
+      pv[u] = tx + ty * W;
+      cv[u] = ok[u] ? costs[pv[u]] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (ok[u] && mc > cv[u]) { mpos = pv[u]; mc = cv[u]; }
   }
   return mc < 3.40282347e+38f ? mpos : -1;
 }
@@ -306,6 +349,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_strong_coop(const PassCo
   const float4* __restrict__ planes_s = B.planes_snap;
   const bool fast = pc.P.strong_radius == 5 && pc.P.strong_increment == 2;
   bool on_edge = false;
+  PHASE_BEGIN();
   // ---- phase 1: reference patch + candidate scans
   if (active) {
     if (fast) patch_lds_build(pw, pc, B, x, y, c, C);
@@ -318,27 +362,54 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_strong_coop(const PassCo
       pos = acmh_candidate(pc, costs_s, x, y, center, c);
     }
     posl[c] = pos;
-    if (pos >= 0) cpl[c] = planes_s[pos];
-    if (c == 0) cpl[C] = planes_s[center];
+    auto phash = [](const float4& p) -> int {
+      uint32_t h = __float_as_uint(p.x) * 0x9E3779B1u;
+      h = (h ^ (h >> 15) ^ __float_as_uint(p.y)) * 0x85EBCA77u;
+      h = (h ^ (h >> 13) ^ __float_as_uint(p.z)) * 0xC2B2AE3Du;
+      h = (h ^ (h >> 16) ^ __float_as_uint(p.w)) * 0x27D4EB2Fu;
+      return (int)((h ^ (h >> 15)) & 0x7FFFFFFFu);
+    };
+    if (pos >= 0) { const float4 pl = planes_s[pos]; cpl[c] = pl; alias[c] = phash(pl); }
+    else alias[c] = (int)(0x80000000u | (uint32_t)c);
+    if (c == 0) { const float4 pl = planes_s[center]; cpl[C] = pl; alias[C] = phash(pl); }
   }
   wave_sync();
+  PHASE(0);
   // ---- phase 1b: bitwise-identical planes among the candidates and the current plane (a third of
-  // the candidates in a converged map: propagation copies planes) share one cost vector
+  // the candidates in a converged map: propagation copies planes) share one cost vector.  alias[]
+  // first holds a 31-bit hash of each valid slot's plane (absent slots: a unique value with the top
+  // bit set); the earliest equal-hash slot is then confirmed bit by bit.
   auto same = [](const float4& a, const float4& b) {
     return __float_as_uint(a.x) == __float_as_uint(b.x) && __float_as_uint(a.y) == __float_as_uint(b.y) &&
            __float_as_uint(a.z) == __float_as_uint(b.z) && __float_as_uint(a.w) == __float_as_uint(b.w);
   };
+  int al[2] = {-1, -1};
   if (active) {
-    for (int sl = c; sl <= C; sl += C) {
-      if (sl < C && posl[sl] < 0) { alias[sl] = -1; continue; }
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int sl = c + r * C;
+      if (sl > C || (sl < C && posl[sl] < 0)) continue;
       const float4 me = cpl[sl];
+      const uint32_t h = (uint32_t)alias[sl];
+      uint32_t m = 0;
+#pragma unroll
+      for (int t = 0; t < C; ++t) m |= ((uint32_t)alias[t] == h && t < sl) ? (1u << t) : 0u;
       int a = sl;
-      for (int t = 0; t < sl; ++t)
-        if (posl[t] >= 0 && same(cpl[t], me)) { a = t; break; }
-      alias[sl] = a;
+      while (m) {
+        const int t = __builtin_ctz(m);
+        if (same(cpl[t], me)) { a = t; break; }
+        m &= m - 1;
+      }
+      al[r] = a;
     }
   }
   wave_sync();
+  if (active) {
+    alias[c] = al[0];
+    if (c == 0) alias[C] = al[1];
+  }
+  wave_sync();
+  PHASE(1);
   if (c == 0) {
     int n = 0;
     if (active) {
@@ -348,6 +419,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_strong_coop(const PassCo
     misc[1] = n;
   }
   wave_sync();
+  PHASE(2);
   // ---- phase 2: cost vectors of every candidate and of the current plane, one flat pool
   {
     // view-major order: the lanes of one round gather from the same source image (cache locality)
@@ -368,6 +440,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_strong_coop(const PassCo
     }
   }
   wave_sync();
+  PHASE(3);
   if (active) {                                          // duplicates take their original's vector
     for (int sl = c; sl <= C; sl += C) {
       const int a = alias[sl];
@@ -376,6 +449,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_strong_coop(const PassCo
     }
   }
   wave_sync();
+  PHASE(4);
   // ---- phase 3: arbitration of the two candidates of each direction (edge mode, DPE.cu:1323-1342)
   if (active && c < 8) {
     if constexpr (EDGE) {
@@ -402,6 +476,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_strong_coop(const PassCo
     }
   }
   wave_sync();
+  PHASE(5);
   // cost of (direction j, view i) as the reference's cost_array holds it
   auto cst = [&](int j, int i) -> float {
     const int f = fin[j];
@@ -427,21 +502,24 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_strong_coop(const PassCo
     }
   }
   wave_sync();
-  // ---- serial: samples + view weights (pixel lane 0)
+  PHASE(6);
+  // ---- samples + view weights (cooperative), then the selected-view list on lane 0
   Rng rs;
+  rng_init(rs, (uint32_t)center, pc.seed32, STREAM_ITER_BASE + 4 * iter + 0, pc.salt);
+  view_sample_coop(sp, (int*)ref, nv, c, C, active, rs, vwl, B.vw + (size_t)center * DPE_MAX_IMAGES);
+  PHASE(12);
   uint32_t tsv = 0; float wnorm = 0.0f;
   if (c == 0) {
     int ns = 0;
     if (active) {
-      rng_init(rs, (uint32_t)center, pc.seed32, STREAM_ITER_BASE + 4 * iter + 0, pc.salt);
-      view_sample(sp, nv, rs, vwl, tsv, wnorm);
-      for (int i = 0; i < nv; ++i) if (vwl[i] > 0) sel_list[ns++] = i;
-      uint8_t* vwg = B.vw + (size_t)center * DPE_MAX_IMAGES;
-      for (int j = 0; j < DPE_MAX_IMAGES; ++j) vwg[j] = vwl[j];
+      rng_seek(rs, 15);
+      for (int i = 0; i < nv; ++i) if (vwl[i] > 0) { setBit(tsv, i); wnorm += vwl[i]; sel_list[ns++] = i; }
+      sums_all[ps * 4 + 3] = wnorm;
     }
     misc[0] = ns;
   }
   wave_sync();
+  PHASE(7);
   const int nsel = active ? misc[0] : 0;
   // ---- phase 5: final costs of the 8 directions
   if (active && c < 8) {
@@ -452,6 +530,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_strong_coop(const PassCo
     fc[c] = f / wn;
   }
   wave_sync();
+  PHASE(8);
   // ---- serial: propagation acceptance + refinement hypotheses (DPE.cu:1617-1654, 1065-1095)
   float cost_now = 0.0f, cost_written = 0.0f, depth_now = 0.0f;
   float4 pnow = make_float4(0, 0, 0, 0);
@@ -488,6 +567,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_strong_coop(const PassCo
     hyp[0] = h0; hyp[1] = h1; hyp[2] = h2; hyp[3] = h3; hyp[4] = h4;
   }
   wave_sync();
+  PHASE(9);
   // ---- phase 6: refinement NCCs, one flat pool of (pixel, hypothesis, selected view)
   {
     int cnt[P];
@@ -504,16 +584,24 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_strong_coop(const PassCo
     }
   }
   wave_sync();
-  // ---- serial: sequential acceptance + write-back (DPE.cu:1097-1117, 1656-1665)
+  PHASE(10);
+  // ---- hypothesis costs and depths (one lane each), then sequential acceptance + write-back on
+  // lane 0 (DPE.cu:1097-1117, 1656-1665)
+  if (active && c < 5) {
+    const int h = c;
+    float tc = 0.0f;
+    for (int k = 0; k < nsel; ++k) tc += vwl[sel_list[k]] * ref[h * nv + k];
+    tc /= sums_all[ps * 4 + 3];
+    fc[h] = tc;
+    misc[2 + h] = __float_as_int(depth_from_plane(c0, hyp[h], x, y));
+  }
+  wave_sync();
+  PHASE(13);
   if (active && c == 0) {
     const float dmin = pc.P.depth_min, dmax = pc.P.depth_max;
     for (int h = 0; h < 5; ++h) {
-      const float4 tp = hyp[h];
-      float tc = 0.0f;
-      for (int k = 0; k < nsel; ++k) tc += vwl[sel_list[k]] * ref[h * nv + k];
-      tc /= wnorm;
-      const float db = depth_from_plane(c0, tp, x, y);
-      if (db >= dmin && db <= dmax && tc < cost_now) { depth_now = db; pnow = tp; cost_now = tc; }
+      const float tc = fc[h], db = __int_as_float(misc[2 + h]);
+      if (db >= dmin && db <= dmax && tc < cost_now) { depth_now = db; pnow = hyp[h]; cost_now = tc; }
     }
     if (pc.P.state == DPE_REFINE_INIT) {
       if ((double)cost_now < (double)cost_written - 0.1) { B.costs[center] = cost_now; B.planes[center] = pnow; }
@@ -522,6 +610,8 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_strong_coop(const PassCo
       B.planes[center] = pnow;
     }
   }
+  PHASE(11);
+  PHASE_END(0);
 }
 
 // ------------------------------------------------------------------------------ weak sweep
@@ -803,16 +893,15 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassCons
   }
   wave_sync();
   Rng rs;
+  rng_init(rs, (uint32_t)center, pc.seed32, STREAM_ITER_BASE + 4 * iter + 2, pc.salt);
+  view_sample_coop(sp, (int*)hv, nv, c, C, active, rs, vwl, B.vw + (size_t)center * DPE_MAX_IMAGES);
   uint32_t tsv = 0; float wnorm = 0.0f;
   if (active && c == 0) {
-    rng_init(rs, (uint32_t)center, pc.seed32, STREAM_ITER_BASE + 4 * iter + 2, pc.salt);
-    view_sample(sp, nv, rs, vwl, tsv, wnorm);
+    rng_seek(rs, 15);
     int ns = 0;
-    for (int i = 0; i < nv; ++i) if (vwl[i] > 0) sel_list[ns++] = i;
+    for (int i = 0; i < nv; ++i) if (vwl[i] > 0) { setBit(tsv, i); wnorm += vwl[i]; sel_list[ns++] = i; }
     misc[0] = ns;
     misc[4] = __float_as_int(wnorm);
-    uint8_t* vwg = B.vw + (size_t)center * DPE_MAX_IMAGES;
-    for (int j = 0; j < DPE_MAX_IMAGES; ++j) vwg[j] = vwl[j];
   }
   wave_sync();
   const int nsel = active ? misc[0] : 0;
