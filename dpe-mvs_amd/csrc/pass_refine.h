@@ -21,15 +21,26 @@ DEV void wave_sync() {
 
 // 36-tap reference patch in LDS: (w, w*grey) pairs [36][2], then rp[36] (grey level), pixel (px, py).
 // Lane `t` of the group computes taps t, t+stride, ...
-DEV void patch_lds_build(float* pw, const PassConst& pc, const DevBufs& B, int px, int py, int t, int stride) {
+// (lane t of S lanes; all of a lane's texel loads are issued before the weights are computed)
+template <int S>
+DEV void patch_lds_build(float* pw, const PassConst& pc, const DevBufs& B, int px, int py, int t) {
+  constexpr int R = (36 + S - 1) / S;
   const float rc = ref_texel(B.ref, pc.W, pc.H, px, py);
-  for (int k = t; k < 36; k += stride) {
+  float rp[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int k = t + r * S < 36 ? t + r * S : 35;
+    rp[r] = ref_texel(B.ref, pc.W, pc.H, px - 5 + 2 * (k / 6), py - 5 + 2 * (k % 6));
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int k = t + r * S;
+    if (k >= 36) break;
     const int i = -5 + 2 * (k / 6), j = -5 + 2 * (k % 6);
-    const float rp = ref_texel(B.ref, pc.W, pc.H, px + i, py + j);
-    const float w = bilateral_weight(i, j, rp, rc, pc.P.sigma_spatial, pc.P.sigma_color);
+    const float w = bilateral_weight(i, j, rp[r], rc, pc.P.sigma_spatial, pc.P.sigma_color);
     pw[2 * k] = w;
-    pw[2 * k + 1] = w * rp;
-    pw[72 + k] = rp;
+    pw[2 * k + 1] = w * rp[r];
+    pw[72 + k] = rp[r];
   }
 }
 // reference sums in the row order of make_patch36 (bit-identical)
@@ -180,7 +191,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_depth_to_weak(const Pass
   const float disp = c0.K[0] * base_line / od;
   const bool fast = pc.P.strong_radius == 5 && pc.P.strong_increment == 2;
   float* pw = s_patch[wave];
-  if (fast) patch_lds_build(pw, pc, B, x, y, lane, 64);
+  if (fast) patch_lds_build<64>(pw, pc, B, x, y, lane);
   wave_sync();
   float s_ref = 0, s_rr = 0, s_w = 0;
   if (fast) patch_lds_sums(pw, s_ref, s_rr, s_w);
@@ -209,24 +220,28 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_depth_to_weak(const Pass
     s_pc[wave][lane] = val;
   }
   wave_sync();
-  if (lane != 0) return;
+  // local minima of the cost curve: one lane per sample, then the reference's in-order scan over
+  // the (few) peaks only, which is the same scan since non-peaks never update it
   const float* pcs = s_pc[wave];
-  int peak_count = 0, min_peak = 0;
+  const bool pk = lane >= 2 && lane < 59 && pcs[lane - 1] > pcs[lane] && pcs[lane + 1] > pcs[lane];
+  const uint64_t is_peak = __ballot(pk);
+  if (lane != 0) return;
+  const int peak_count = __popcll(is_peak);
+  int min_peak = 0;
   float min_cost = 2.0f;
-  uint64_t is_peak = 0;
-  for (int i = 2; i < 59; ++i) {
-    const float c = pcs[i];
-    if (pcs[i - 1] > c && pcs[i + 1] > c) {
-      is_peak |= 1ull << i; peak_count++;
-      if (c < min_cost) { min_peak = i; min_cost = c; }
-    }
+  for (uint64_t m = is_peak; m; m &= m - 1) {
+    const int i = __builtin_ctzll(m);
+    if (pcs[i] < min_cost) { min_peak = i; min_cost = pcs[i]; }
   }
   uint8_t cls;
   if (abs(min_peak - radius) > pc.P.weak_peak_radius || pcs[min_peak] > 0.5f) cls = DPE_WEAK;
   else if (peak_count == 1) cls = pcs[min_peak] <= 0.15f ? DPE_STRONG : DPE_WEAK;
   else {
     float var = 0.0f;
-    for (int i = 2; i < 59; ++i) if (((is_peak >> i) & 1ull) && i != min_peak) { const float d = pcs[i] - min_cost; var += d * d; }
+    for (uint64_t m = is_peak; m; m &= m - 1) {
+      const int i = __builtin_ctzll(m);
+      if (i != min_peak) { const float d = pcs[i] - min_cost; var += d * d; }
+    }
     var = __builtin_sqrtf(var);
     var /= (peak_count - 1);
     cls = var > 0.2f ? DPE_STRONG : DPE_WEAK;
@@ -278,7 +293,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_local_refine_jobs(const 
     if (weight_normal == 0 || valid == 0) go = false;
   }
   float* pw = s_patch[wave][gp];
-  if (go && fast) patch_lds_build(pw, pc, B, x, y, gl, 16);
+  if (go && fast) patch_lds_build<16>(pw, pc, B, x, y, gl);
   float disp = 0.0f;
   if (go) { base_line /= valid; disp = c0.K[0] * base_line / od; }
   if (go && gl < 12) {                             // hypothesis gl (11 = the current depth)

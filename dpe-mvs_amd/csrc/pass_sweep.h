@@ -352,7 +352,8 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_strong_coop(const PassCo
   PHASE_BEGIN();
   // ---- phase 1: reference patch + candidate scans
   if (active) {
-    if (fast) patch_lds_build(pw, pc, B, x, y, c, C);
+    if (fast) patch_lds_build<C>(pw, pc, B, x, y, c);
+    PHASE(14);
     int pos;
     if constexpr (EDGE) {
       on_edge = B.edge[center] != 0;
@@ -791,9 +792,10 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassCons
   T.tc = tcp; T.tn = tnp; T.sums = sums; T.nbl = nbl; T.nsv = nsv;
   const short2* nbg = B.nb + (size_t)center * 9;
 
+  PHASE_BEGIN();
   // ---- phase 1: neighbours, weight tables, Old-NCC patch, candidate rows
   if (active) {
-    if (fast_old) patch_lds_build(pw, pc, B, x, y, c, C);
+    if (fast_old) patch_lds_build<C>(pw, pc, B, x, y, c);
     for (int k = c; k < 9; k += C) {
       const short2 np = nbg[k];
       nbl[k] = np;
@@ -822,6 +824,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassCons
     }
   }
   wave_sync();
+  PHASE(0);
   // ---- phase 1b: reference sums of every tabulated patch (tap order of patch_ncc_generic)
   if (active) {
     for (int k = c; k < 9; k += C) {
@@ -859,6 +862,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassCons
     }
   }
   wave_sync();
+  PHASE(1);
   // ---- phase 2: candidate cost vectors, jobs (unique flagged neighbour plane, view)
   if (active) {
     uint32_t um = 0;
@@ -872,11 +876,13 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassCons
     }
   }
   wave_sync();
+  PHASE(2);
   if (active)
     for (int i = c; i < 8; i += C)
       if (misc[8 + i] && alias[i] != i)
         for (int v = 0; v < nv; ++v) cost[i * nv + v] = cost[alias[i] * nv + v];
   wave_sync();
+  PHASE(3);
   // ---- phase 3: per-view probabilities with the deformable-neighbour priors (DPE.cu:1768-1790)
   const float cost_threshold = (float)(0.8 * (double)d_expf((float)(iter * iter) / (-90.0f)));
   if (active) {
@@ -892,6 +898,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassCons
     }
   }
   wave_sync();
+  PHASE(4);
   Rng rs;
   rng_init(rs, (uint32_t)center, pc.seed32, STREAM_ITER_BASE + 4 * iter + 2, pc.salt);
   view_sample_coop(sp, (int*)hv, nv, c, C, active, rs, vwl, B.vw + (size_t)center * DPE_MAX_IMAGES);
@@ -904,6 +911,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassCons
     misc[4] = __float_as_int(wnorm);
   }
   wave_sync();
+  PHASE(5);
   const int nsel = active ? misc[0] : 0;
   const float wn = active ? __int_as_float(misc[4]) : 1.0f;
   const float4 cur = active ? B.planes[center] : make_float4(0, 0, 0, 1);
@@ -938,6 +946,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassCons
     }
   }
   wave_sync();
+  PHASE(6);
   // ---- serial: propagation acceptance, fit plane, refinement hypotheses (DPE.cu:1792-1843, 1120-1170)
   float cost_now = 0.0f, cost_written = 0.0f, depth_now = 0.0f;
   float4 pnow = cur;
@@ -977,6 +986,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassCons
     }
   }
   wave_sync();
+  PHASE(7);
   // ---- phase 5: refinement NCCs, jobs (hypothesis, selected view)
   if (active && has_fit) {
     for (int j = c; j < 5 * nsel; j += C) {
@@ -985,6 +995,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassCons
     }
   }
   wave_sync();
+  PHASE(8);
   // ---- serial: sequential acceptance + write-back (DPE.cu:1190-1207, 1831-1843)
   if (active && c == 0) {
     if (has_fit) {
@@ -1007,6 +1018,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassCons
     hyp[5] = fin;
   }
   wave_sync();
+  PHASE(9);
   // ---- phase 6: the stored cost is the Old NCC of the final plane (DPE.cu:1845-1861)
   if (active) {
     const float4 fin = hyp[5];
@@ -1014,11 +1026,14 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassCons
       hv[k] = ncc_old_any<U8>(fast_old, pw, osum[0], osum[1], osum[2], x, y, pc, B, sel_list[k] + 1, fin);
   }
   wave_sync();
+  PHASE(10);
   if (active && c == 0) {
     float c2 = 0.0f;
     for (int k = 0; k < nsel; ++k) c2 += vwl[sel_list[k]] * hv[k];
     B.costs[center] = c2 / wnorm;
   }
+  PHASE(11);
+  PHASE_END(1);
 }
 
 }  // namespace dpe
