@@ -354,6 +354,36 @@ DEV float tap_u8_fast(const DevBufs& B, uint32_t vofs, uint32_t stride, f2v lim,
   }
 }
 
+// Two taps of one patch row (columns yf.x, yf.y) with the projection, reciprocal refinement and
+// the vertical interpolation packed across the two taps; per element the same operations as
+// tap_u8_fast, so each result is bit-identical to it.
+#ifndef DPE_TAP_PAIR
+#define DPE_TAP_PAIR 1
+#endif
+template <int T>
+DEV f2v tap2_fast(const DevBufs& B, uint32_t vofs, uint32_t stride, f2v lim, const float* h, f2v bxy, float bz, f2v yf) {
+  const f2v qx = fma2(f2s(h[1]), yf, f2s(bxy.x));
+  const f2v qy = fma2(f2s(h[4]), yf, f2s(bxy.y));
+  const f2v qz = fma2(f2s(h[7]), yf, f2s(bz));
+  const f2v r = (f2v){__builtin_amdgcn_rcpf(qz.x), __builtin_amdgcn_rcpf(qz.y)};
+  const f2v iz = fma2(fma2(-qz, r, f2s(1.0f)), r, r);
+  const f2v sx = qx * iz, sy = qy * iz;
+  const f2v xb = (f2v){__builtin_amdgcn_fmed3f(sx.x, -1.0f, lim.x), __builtin_amdgcn_fmed3f(sx.y, -1.0f, lim.x)};
+  const f2v yb = (f2v){__builtin_amdgcn_fmed3f(sy.x, -1.0f, lim.y), __builtin_amdgcn_fmed3f(sy.y, -1.0f, lim.y)};
+  const f2v ux = fma2(xb, f2s(256.0f), f2s(256.5f)), uy = fma2(yb, f2s(256.0f), f2s(256.5f));
+  const uint32_t ux0 = (uint32_t)(int)ux.x, ux1 = (uint32_t)(int)ux.y;   // >= 0 after the clamp
+  const uint32_t uy0 = (uint32_t)(int)uy.x, uy1 = (uint32_t)(int)uy.y;
+  const uint8_t* base = tex_base<T>(B);
+  const uint8_t* p0 = base + (vofs + (__umul24(uy0 >> 8, stride) + (ux0 >> 8)) * tex_bytes<T>());
+  const uint8_t* p1 = base + (vofs + (__umul24(uy1 >> 8, stride) + (ux1 >> 8)) * tex_bytes<T>());
+  const f2v ay = (f2v){(float)(uy0 & 255u), (float)(uy1 & 255u)} * f2s(0.00390625f);
+  float a0, a1, b0, b1;
+  texel_rows<T>(p0, (float)(ux0 & 255u), a0, a1);
+  texel_rows<T>(p1, (float)(ux1 & 255u), b0, b1);
+  const f2v r0 = (f2v){a0, b0}, r1 = (f2v){a1, b1};
+  return fma2(ay, r1 - r0, r0);
+}
+
 template <int U8> DEV float sample_src(const DevBufs& B, int v, int W, int H, float sx, float sy) {
   if constexpr (U8 != TEX_F32) return sample_quad8<U8>(tex_base<U8>(B) + (size_t)v * tex_view<U8>(B), W, H, sx, sy);
   else return sample_quad(B.imgq[v], W, H, sx, sy);

@@ -99,7 +99,10 @@ __global__ void k_gen_edge_inform(const PassConst* __restrict__ pcp, DevBufs B) 
 
 // ------------------------------------------------------------------------------ GenNeighbours
 // One thread per WEAK pixel of `list` (the reference's full-grid launch with most threads idle).
-__global__ void __launch_bounds__(256) k_gen_neighbours(const PassConst* __restrict__ pcp, DevBufs B,
+#ifndef DPE_GN_WAVES
+#define DPE_GN_WAVES 1
+#endif
+__global__ void __launch_bounds__(256, DPE_GN_WAVES) k_gen_neighbours(const PassConst* __restrict__ pcp, DevBufs B,
                                                         const int* __restrict__ list, const int* __restrict__ nlist_p) {   // DPE.cu:2103-2463
   const PassConst& pc = *pcp;
   const int gi = xcd_remap(blockIdx.x, gridDim.x, B.xcd_rows * 16) * blockDim.x + threadIdx.x;

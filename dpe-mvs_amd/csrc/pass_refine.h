@@ -83,6 +83,19 @@ DEV void lds_taps(const float* pw, int px, int py, const PassConst& pc, const De
       const float bz = __builtin_fmaf(H.h[6], x, H.h[8]);
       f2v r_sr = f2s(0.0f);
       float r_ss = 0;
+#if DPE_TAP_PAIR
+#pragma unroll
+      for (int b = 0; b < 6; b += 2) {
+        const f2v sp = tap2_fast<U8>(B, vofs, stride, lim, H.h, bxy, bz,
+                                     (f2v){(float)(py - 5 + 2 * b), (float)(py - 3 + 2 * b)});
+        const f2v w0 = wp[a * 6 + b], w1 = wp[a * 6 + b + 1];
+        const f2v ws = (f2v){w0.x, w1.x} * sp;
+        r_sr = fma2(w0, f2s(sp.x), r_sr);
+        r_ss = __builtin_fmaf(ws.x, sp.x, r_ss);
+        r_sr = fma2(w1, f2s(sp.y), r_sr);
+        r_ss = __builtin_fmaf(ws.y, sp.y, r_ss);
+      }
+#else
 #pragma unroll
       for (int b = 0; b < 6; ++b) {
         const float sp = tap_u8_fast<U8>(B, vofs, stride, lim, H.h, bxy, bz, (float)(py - 5 + 2 * b));
@@ -91,6 +104,7 @@ DEV void lds_taps(const float* pw, int px, int py, const PassConst& pc, const De
         const float ws = w.x * sp;
         r_ss = __builtin_fmaf(ws, sp, r_ss);
       }
+#endif
       s_sr += r_sr; s_ss += r_ss;
     }
     acc[0] = s_sr.x; acc[1] = s_ss; acc[2] = s_sr.y;
