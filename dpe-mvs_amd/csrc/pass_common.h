@@ -76,10 +76,18 @@ struct DevBufs {
       for (int k_ = 0; k_ < 16; ++k_)                                               \
         if (ph_acc_[k_]) atomicAdd(B.phase + ((blockIdx.x & 31) * 4 + (kernel)) * 16 + k_, (unsigned long long)ph_acc_[k_]); \
   } while (0)
+// every lane adds its own sums (thread-per-item kernels whose lanes diverge)
+#define PHASE_END_ALL(kernel)                                                       \
+  do {                                                                              \
+    if (B.phase)                                                                    \
+      for (int k_ = 0; k_ < 16; ++k_)                                               \
+        if (ph_acc_[k_]) atomicAdd(B.phase + ((blockIdx.x & 31) * 4 + (kernel)) * 16 + k_, (unsigned long long)ph_acc_[k_]); \
+  } while (0)
 #else
 #define PHASE_BEGIN() do {} while (0)
 #define PHASE(k) do {} while (0)
 #define PHASE_END(kernel) do {} while (0)
+#define PHASE_END_ALL(kernel) do {} while (0)
 #endif
 DEV void count_work(const DevBufs& B, unsigned long long ncc, unsigned long long taps) {
   if (B.cnt) { atomicAdd(B.cnt + 0, ncc); atomicAdd(B.cnt + 1, taps); }

@@ -109,6 +109,7 @@ __global__ void __launch_bounds__(256, DPE_GN_WAVES) k_gen_neighbours(const Pass
   if (gi >= *nlist_p) return;
   const int W = pc.W, H = pc.H;
   const int center = list[gi];
+  PHASE_BEGIN();
   const int x = center % W, y = center / W;
   const int min_margin = 6;
   const float depth_diff = pc.P.depth_max - pc.P.depth_min;
@@ -180,6 +181,7 @@ __global__ void __launch_bounds__(256, DPE_GN_WAVES) k_gen_neighbours(const Pass
       }
     }
   }
+  PHASE(0);
   int extend_index = 31;
   if (pc.P.use_label && B.label[center] > 0) {
     const short2* lb = B.lab_bound + (size_t)center * 8;
@@ -217,7 +219,8 @@ __global__ void __launch_bounds__(256, DPE_GN_WAVES) k_gen_neighbours(const Pass
       }
     }
   }
-  if (strong_point_size <= 3) { B.weak_rel[center] = 0; return; }
+  PHASE(1);
+  if (strong_point_size <= 3) { B.weak_rel[center] = 0; PHASE_END_ALL(2); return; }
 
   // support points compacted in place (strong_points doubles as spv[]); per point only the depth
   // is kept: its 3-D point and normal are recomputed from (pixel, depth) / planes[] when a, b, c
@@ -237,6 +240,11 @@ __global__ void __launch_bounds__(256, DPE_GN_WAVES) k_gen_neighbours(const Pass
     }
   }
   for (int i = valid_count; i < 64; ++i) spv[i] = make_short2(-1, -1);
+  // normalised image coordinates of each support point: loop-invariant in the RANSAC iterations
+  // below (same expression, same bits as evaluating it per iteration)
+  float2 spf[64];
+  for (int i = 0; i < valid_count; ++i)
+    spf[i] = make_float2(((float)spv[i].x - camera.K[2]) / camera.K[0], ((float)spv[i].y - camera.K[5]) / camera.K[4]);
   auto point3 = [&](int i) -> float3 {
     float Y[3];
     get3d(camera, spv[i].x, spv[i].y, spd[i], Y);
@@ -246,6 +254,7 @@ __global__ void __launch_bounds__(256, DPE_GN_WAVES) k_gen_neighbours(const Pass
     const float4 n4 = transform_normal_ref(camera, B.planes[spv[i].x + spv[i].y * W]);
     return make_float3(n4.x, n4.y, n4.z);
   };
+  PHASE(2);
   float4 best_plane = make_float4(0, 0, 0, 0);
   bool has_valid_plane = false;
   {
@@ -300,15 +309,15 @@ __global__ void __launch_bounds__(256, DPE_GN_WAVES) k_gen_neighbours(const Pass
       if ((cv.x == 0 && cv.y == 0 && cv.z == 0) || cv.x != cv.x || cv.y != cv.y || cv.z != cv.z) continue;
       normalize3(cv);
       cv.w = -(cv.x * A.x + cv.y * A.y + cv.z * A.z);
+      // residual of support point si under cv (stored only when a new best plane needs the sort)
+      auto resid = [&](int si) -> float {
+        const float2 f = spf[si];
+        const float fd = -cv.w / (cv.x * f.x + cv.y * f.y + cv.z);
+        return __builtin_fabsf(fd - spd[si]);
+      };
       int temp_count = 0;
-      for (int si = 0; si < valid_count; ++si) {
-        const float fx = ((float)spv[si].x - camera.K[2]) / camera.K[0];
-        const float fy = ((float)spv[si].y - camera.K[5]) / camera.K[4];
-        const float fd = -cv.w / (cv.x * fx + cv.y * fy + cv.z);
-        const float dist = __builtin_fabsf(fd - spd[si]);
-        residuals[si] = dist;
-        if (dist < temp_thr) temp_count++;
-      }
+      for (int si = 0; si < valid_count; ++si)
+        if (resid(si) < temp_thr) temp_count++;
       if (temp_count < 6) continue;
       if (temp_count > max_count) {
         if (!must_in_triangle && point_in_triangle(spv[a], spv[b], spv[c], x, y)) must_in_triangle = true;
@@ -319,6 +328,7 @@ __global__ void __launch_bounds__(256, DPE_GN_WAVES) k_gen_neighbours(const Pass
         const float cd = __builtin_fabsf(fd - cpz);
         best_plane = cv; max_count = temp_count; min_cost = cd; has_valid_plane = true;
         if ((double)temp_thr > (pc.P.high_res_img ? 0.05 : 0.005)) {
+          for (int si = 0; si < valid_count; ++si) residuals[si] = resid(si);
           // sort_small(residuals, valid_count) (DPE.cu:5-14)
           for (int i = 1; i < valid_count; i++) {
             const float tmp = residuals[i];
@@ -345,11 +355,11 @@ __global__ void __launch_bounds__(256, DPE_GN_WAVES) k_gen_neighbours(const Pass
       }
     }
   }
-  if (!has_valid_plane) { B.weak_rel[center] = 0; return; }
+  PHASE(3);
+  if (!has_valid_plane) { B.weak_rel[center] = 0; PHASE_END_ALL(2); return; }
   float* weight = spd;          // in place: weight[i] is written after spd[i] is read
   for (int i = 0; i < valid_count; ++i) {
-    const float fx = ((float)spv[i].x - camera.K[2]) / camera.K[0];
-    const float fy = ((float)spv[i].y - camera.K[5]) / camera.K[4];
+    const float fx = spf[i].x, fy = spf[i].y;
     const float fd = -best_plane.w / (best_plane.x * fx + best_plane.y * fy + best_plane.z);
     const float dist = __builtin_fabsf(fd - spd[i]);
     if (dist >= ransac_threshold) { spv[i] = make_short2(-1, -1); weight[i] = 3.40282347e+38f; continue; }
@@ -364,6 +374,8 @@ __global__ void __launch_bounds__(256, DPE_GN_WAVES) k_gen_neighbours(const Pass
   }
   for (int i = 1; i < DPE_NEIGHBOUR_NUM; ++i) nb[i] = spv[i - 1];
   B.weak_rel[center] = 1;
+  PHASE(4);
+  PHASE_END_ALL(2);
 }
 
 // ------------------------------------------------------------------------------ NeigbourUpdate
