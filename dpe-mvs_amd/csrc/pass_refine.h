@@ -196,6 +196,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_depth_to_weak(const Pass
   const float4 op = transform_normal_ref(c0, B.planes[center]);
   const float od = op.w;
   if (od == 0) { if (lane == 0) B.weak[center] = DPE_UNKNOWN; return; }
+  PHASE_BEGIN();
   const uint32_t sel = B.sel[center];
   const uint8_t* vw = B.vw + (size_t)DPE_MAX_IMAGES * center;
   float base_line, weight_normal; int valid;
@@ -209,6 +210,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_depth_to_weak(const Pass
   wave_sync();
   float s_ref = 0, s_rr = 0, s_w = 0;
   if (fast) patch_lds_sums(pw, s_ref, s_rr, s_w);
+  PHASE(0);
   const int radius = 30;
   if (lane < 2 * radius + 1) {
     const int pd = lane - radius;
@@ -224,7 +226,9 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_depth_to_weak(const Pass
         if (isSet(sel, vi)) {
           float tcst = 0.0f;
           tcst += ncc_old_any<U8>(fast, pw, s_ref, s_rr, s_w, x, y, pc, B, si, tp);
+          PHASE(1);
           if (pc.P.geom_consistency) tcst += pc.P.geom_factor * geom_cost(pc, B, x, y, si, tp);
+          PHASE(2);
           p_cost += (tcst * vw[vi]);
         }
       }
@@ -234,11 +238,14 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_depth_to_weak(const Pass
     s_pc[wave][lane] = val;
   }
   wave_sync();
+  PHASE(3);
   // local minima of the cost curve: one lane per sample, then the reference's in-order scan over
   // the (few) peaks only, which is the same scan since non-peaks never update it
   const float* pcs = s_pc[wave];
   const bool pk = lane >= 2 && lane < 59 && pcs[lane - 1] > pcs[lane] && pcs[lane + 1] > pcs[lane];
   const uint64_t is_peak = __ballot(pk);
+  PHASE(4);
+  PHASE_END(3);
   if (lane != 0) return;
   const int peak_count = __popcll(is_peak);
   int min_peak = 0;
