@@ -39,7 +39,7 @@ FLOP_PER_GEOM = 60
 # per-dispatch HBM bytes from the committed PMC passes (tools/pmc.sh + tools/prof_summary.py)
 PMC_JSON = os.path.join(ROOT, "profiles", "r01_pmc.json")
 CLASS_KERNEL = {"strong": "k_strong_coop", "weak": "k_weak_coop", "depth_to_weak": "k_depth_to_weak",
-                "local_refine": "k_local_refine", "init": "k_random_init", "ransac": "k_ransac_fit",
+                "local_refine": "k_local_refine_jobs", "init": "k_random_init", "ransac": "k_ransac_fit",
                 "setup": "k_gen_neighbours"}
 
 
