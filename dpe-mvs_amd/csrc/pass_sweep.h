@@ -631,24 +631,29 @@ struct WeakTab {
   float rc;                               // grey level of the pixel
 };
 
-// patch NCC with tabulated weights; the same tap order and arithmetic as patch_ncc_generic
-template <int U8, bool FAST>
+// patch NCC with tabulated weights; the same tap order and arithmetic as patch_ncc_generic.
+// NN > 0: the patch side n is the compile-time NN, so the tap loop unrolls and the gathers of a
+// patch are in flight together (the weak sweep's patches are 3x3 and 4..6 square).
+template <int U8, bool FAST, int NN = 0>
 DEV void tab_taps(const PassConst& pc, const DevBufs& B, int v, const Homog& H, int cx, int cy, int rad, int inc,
-                  int n, const float* __restrict__ tw, float* acc) {
+                  int n_rt, const float* __restrict__ tw, float* acc) {
   const int W = pc.W, Hh = pc.H;
+  const int n = NN > 0 ? NN : n_rt;
   const f2v* wp = (const f2v*)tw;            // (w, w*grey) pairs
   if constexpr (U8 != TEX_F32 && FAST && DPE_PACKED_TAP) {
     const uint32_t vofs = (uint32_t)v * tex_view<U8>(B), stride = (uint32_t)(W + 2);
     const f2v lim = (f2v){(float)W, (float)Hh};
     f2v s_sr = f2s(0.0f);
     float s_ss = 0;
-    for (int a = 0; a < n; ++a) {
+#pragma unroll
+    for (int a = 0; a < (NN > 0 ? NN : n); ++a) {
       const float xf = (float)(cx - rad + a * inc);
       const f2v bxy = fma2((f2v){H.h[0], H.h[3]}, f2s(xf), (f2v){H.h[2], H.h[5]});
       const float bz = __builtin_fmaf(H.h[6], xf, H.h[8]);
       f2v r_sr = f2s(0.0f);
       float r_ss = 0;
-      for (int b = 0; b < n; ++b) {
+#pragma unroll
+      for (int b = 0; b < (NN > 0 ? NN : n); ++b) {
         const float sp = tap_u8_fast<U8>(B, vofs, stride, lim, H.h, bxy, bz, (float)(cy - rad + b * inc));
         const f2v w = wp[a * n + b];
         r_sr = fma2(w, f2s(sp), r_sr);
@@ -687,10 +692,17 @@ template <int U8>
 DEV float patch_ncc_tab(const PassConst& pc, const DevBufs& B, int v, const Homog& H, int cx, int cy, int rad, int inc,
                         int n, const float* __restrict__ tw, const float* sm) {
   float a[3];
-  if (rcp_range_ok(H, (float)(cx - rad), (float)(cx + rad), (float)(cy - rad), (float)(cy + rad)))
-    tab_taps<U8, true>(pc, B, v, H, cx, cy, rad, inc, n, tw, a);
-  else
+  if (rcp_range_ok(H, (float)(cx - rad), (float)(cx + rad), (float)(cy - rad), (float)(cy + rad))) {
+    switch (n) {
+      case 3: tab_taps<U8, true, 3>(pc, B, v, H, cx, cy, rad, inc, n, tw, a); break;
+      case 4: tab_taps<U8, true, 4>(pc, B, v, H, cx, cy, rad, inc, n, tw, a); break;
+      case 5: tab_taps<U8, true, 5>(pc, B, v, H, cx, cy, rad, inc, n, tw, a); break;
+      case 6: tab_taps<U8, true, 6>(pc, B, v, H, cx, cy, rad, inc, n, tw, a); break;
+      default: tab_taps<U8, true>(pc, B, v, H, cx, cy, rad, inc, n, tw, a); break;
+    }
+  } else {
     tab_taps<U8, false>(pc, B, v, H, cx, cy, rad, inc, n, tw, a);
+  }
   count_work(B, 0, (unsigned long long)(n * n));
   return ncc_finalize(sm[0], sm[1], sm[2], a[0], a[1], a[2]);
 }
