@@ -629,6 +629,8 @@ struct WeakTab {
   int rad_c, inc_c, n_c, rad_n, inc_n, n_n;
   bool tab_c, tab_n;
   float rc;                               // grey level of the pixel
+  bool nb3;                               // neighbour patches are tabulated 3x3 and nbox is set
+  float nbox[4];                          // x0, x1, y0, y1 of the union of the neighbour patches
 };
 
 // patch NCC with tabulated weights; the same tap order and arithmetic as patch_ncc_generic.
@@ -716,28 +718,40 @@ DEV float ncc_new_tab(const PassConst& pc, const DevBufs& B, const WeakTab& T, i
   if (center_outside(pc, v, H, px, py)) return 2.0f;
   float center_cost = 0.0f, strong_cost = 0.0f;
   int strong_count = 0;
-  for (int k = 0; k < DPE_NEIGHBOUR_NUM; ++k) {
+  {   // k = 0: the pixel's own patch
+    const short2 np = T.nbl[0];
+    if (!(np.x == -1 || np.y == -1)) {
+      const float2 nsp = project_h(H, (float)np.x, (float)np.y);
+      if (nsp.x < 0 || nsp.y < 0 || nsp.x >= (float)W || nsp.y >= (float)Hh) return 2.0f;
+      center_cost = T.tab_c ? patch_ncc_tab<U8>(pc, B, v, H, np.x, np.y, T.rad_c, T.inc_c, T.n_c, T.tc, T.sums)
+                            : patch_ncc_generic<U8>(pc, B, v, H, np.x, np.y, T.rc, T.rad_c, T.inc_c);
+    }
+  }
+  // k = 1..8; one range check over the union of the 3x3 neighbour patches selects the fast
+  // reciprocal for all of them (it is exact on every tap inside that box)
+  const bool nfast = T.nb3 && rcp_range_ok(H, T.nbox[0], T.nbox[1], T.nbox[2], T.nbox[3]);
+#pragma unroll 1
+  for (int k = 1; k < DPE_NEIGHBOUR_NUM; ++k) {
     const short2 np = T.nbl[k];
     if (np.x == -1 || np.y == -1) continue;
     const float2 nsp = project_h(H, (float)np.x, (float)np.y);
     if (nsp.x < 0 || nsp.y < 0 || nsp.x >= (float)W || nsp.y >= (float)Hh) {
-      if (k != 0) {
-        if (isSet(T.nsv[k], v - 1)) { strong_cost += 2.0f; strong_count++; }
-        continue;
-      }
-      return 2.0f;
+      if (isSet(T.nsv[k], v - 1)) { strong_cost += 2.0f; strong_count++; }
+      continue;
     }
     float tc;
-    if (k == 0) {
-      tc = T.tab_c ? patch_ncc_tab<U8>(pc, B, v, H, np.x, np.y, T.rad_c, T.inc_c, T.n_c, T.tc, T.sums)
-                   : patch_ncc_generic<U8>(pc, B, v, H, np.x, np.y, T.rc, T.rad_c, T.inc_c);
-      center_cost = tc;
+    if (nfast) {
+      float a[3];
+      tab_taps<U8, true, 3>(pc, B, v, H, np.x, np.y, T.rad_n, T.inc_n, 3, T.tn + (k - 1) * 18, a);
+      count_work(B, 0, 9ull);
+      const float* sm = T.sums + 3 * k;
+      tc = ncc_finalize(sm[0], sm[1], sm[2], a[0], a[1], a[2]);
     } else {
       tc = T.tab_n ? patch_ncc_tab<U8>(pc, B, v, H, np.x, np.y, T.rad_n, T.inc_n, T.n_n, T.tn + (k - 1) * 18,
                                        T.sums + 3 * k)
                    : patch_ncc_generic<U8>(pc, B, v, H, np.x, np.y, T.rc, T.rad_n, T.inc_n);
-      strong_cost += tc; strong_count++;
     }
+    strong_cost += tc; strong_count++;
   }
   if (strong_count == 0) return center_cost;
   strong_cost /= (float)strong_count;
@@ -837,6 +851,21 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassCons
   }
   wave_sync();
   PHASE(0);
+  // union box of the neighbour patches (k = 1..8) for the one-check fast path of ncc_new_tab
+  T.nb3 = false;
+  if (active && T.tab_n && T.n_n == 3) {
+    int x0 = 0x7FFFFFFF, x1 = -0x7FFFFFFF, y0 = 0x7FFFFFFF, y1 = -0x7FFFFFFF;
+    for (int k = 1; k < DPE_NEIGHBOUR_NUM; ++k) {
+      const short2 np = nbl[k];
+      if (np.x == -1 || np.y == -1) continue;
+      x0 = min(x0, (int)np.x); x1 = max(x1, (int)np.x); y0 = min(y0, (int)np.y); y1 = max(y1, (int)np.y);
+    }
+    if (x0 <= x1) {
+      T.nb3 = true;
+      T.nbox[0] = (float)(x0 - T.rad_n); T.nbox[1] = (float)(x1 + T.rad_n);
+      T.nbox[2] = (float)(y0 - T.rad_n); T.nbox[3] = (float)(y1 + T.rad_n);
+    }
+  }
   // ---- phase 1b: reference sums of every tabulated patch (tap order of patch_ncc_generic)
   if (active) {
     for (int k = c; k < 9; k += C) {
@@ -929,7 +958,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassCons
   const float4 cur = active ? B.planes[center] : make_float4(0, 0, 0, 1);
   const float4 fp = active ? B.fit_plane[center] : make_float4(0, 0, 0, 0);
   const bool has_fit = !(fp.x == 0 && fp.y == 0 && fp.z == 0);
-  auto hyp_val = [&](int v, const float4& pl) -> float {   // one term of hyp_cost (DPE.cu:1140-1150)
+  auto hyp_val = [&](int v, const float4& pl) __attribute__((always_inline)) -> float {   // one term of hyp_cost (DPE.cu:1140-1150)
     const float cn = ncc_new_tab<U8>(pc, B, T, x, y, v, pl);
     return geom ? cn + gf * geom_cost(pc, B, x, y, v, pl) : cn;
   };
