@@ -409,6 +409,22 @@ DEV float bilateral_weight(int i, int j, float pix, float cpix, float ss, float 
   return d_expf(-sd / (2.0f * ss * ss) - cd / (2.0f * sc * sc));
 }
 
+// The reference-patch half of ncc_finalize, computed once per patch: (1/s_w, s_ref/s_w, var_ref)
+// with the same operations, so ncc_finalize_pre(pre..., src sums) == ncc_finalize(ref sums, src sums).
+DEV void ncc_pre(float s_ref, float s_rr, float s_w, float& inv, float& mref, float& var_ref) {
+  inv = 1.0f / s_w;
+  mref = s_ref * inv;
+  const float mrr = s_rr * inv;
+  var_ref = mrr - mref * mref;
+}
+DEV float ncc_finalize_pre(float inv, float mref, float var_ref, float s_src, float s_ss, float s_rs) {
+  s_src *= inv; s_ss *= inv; s_rs *= inv;
+  const float var_src = s_ss - s_src * s_src;
+  if (var_ref < 1e-5f || var_src < 1e-5f) return 2.0f;
+  const float cov = s_rs - mref * s_src;
+  const float vrs = __builtin_sqrtf(var_ref * var_src);
+  return __builtin_fmaxf(0.0f, __builtin_fminf(2.0f, 1.0f - cov / vrs));
+}
 DEV float ncc_finalize(float s_ref, float s_rr, float s_w, float s_src, float s_ss, float s_rs) {
   const float inv = 1.0f / s_w;
   s_ref *= inv; s_rr *= inv; s_src *= inv; s_ss *= inv; s_rs *= inv;
@@ -472,8 +488,17 @@ DEV float patch_ncc_generic(const PassConst& pc, const DevBufs& B, int v, const 
   return ncc_finalize(a[0], a[1], a[5], a[2], a[3], a[4]);
 }
 
+// project_h with the exact 3-op reciprocal (callers guarantee rcp_range_ok over a box holding (x, y))
+DEV float2 project_h_fast(const Homog& H, float x, float y) {
+  const float px = __builtin_fmaf(H.h[1], y, __builtin_fmaf(H.h[0], x, H.h[2]));
+  const float py = __builtin_fmaf(H.h[4], y, __builtin_fmaf(H.h[3], x, H.h[5]));
+  const float pz = __builtin_fmaf(H.h[7], y, __builtin_fmaf(H.h[6], x, H.h[8]));
+  const float iz = d_rcp_fast(pz);
+  return make_float2(px * iz, py * iz);
+}
+template <bool FAST = false>
 DEV bool center_outside(const PassConst& pc, int v, const Homog& H, int px, int py) {
-  const float2 pt = project_h(H, (float)px, (float)py);
+  const float2 pt = FAST ? project_h_fast(H, (float)px, (float)py) : project_h(H, (float)px, (float)py);
   const DpeCamera& sc = pc.cams[v];
   return pt.x >= (float)sc.width || pt.x < 0.0f || pt.y >= (float)sc.height || pt.y < 0.0f;
 }

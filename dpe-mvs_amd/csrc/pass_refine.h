@@ -43,8 +43,9 @@ DEV void patch_lds_build(float* pw, const PassConst& pc, const DevBufs& B, int p
     pw[72 + k] = rp[r];
   }
 }
-// reference sums in the row order of make_patch36 (bit-identical)
-DEV void patch_lds_sums(const float* pw, float& s_ref, float& s_rr, float& s_w) {
+// reference sums in the row order of make_patch36 (bit-identical), returned as ncc_pre's
+// (1/s_w, s_ref/s_w, var_ref), which is what every NCC of the patch needs
+DEV void patch_lds_pre(const float* pw, float& p_inv, float& p_mref, float& p_var) {
   float a_ref = 0, a_rr = 0, a_w = 0;
 #pragma unroll
   for (int a = 0; a < 6; ++a) {
@@ -58,7 +59,7 @@ DEV void patch_lds_sums(const float* pw, float& s_ref, float& s_rr, float& s_w) 
     }
     a_ref += r_ref; a_rr += r_rr; a_w += r_w;
   }
-  s_ref = a_ref; s_rr = a_rr; s_w = a_w;
+  ncc_pre(a_ref, a_rr, a_w, p_inv, p_mref, p_var);
 }
 // Old NCC with the patch read from LDS (same arithmetic as ncc_old_patch36)
 template <int U8, bool FAST>
@@ -146,7 +147,7 @@ DEV float ncc_old_lds(const float* pw, float s_ref, float s_rr, float s_w, int p
     lds_taps<U8, true>(pw, px, py, pc, B, v, H, a);
   else
     lds_taps<U8, false>(pw, px, py, pc, B, v, H, a);
-  return ncc_finalize(s_ref, s_rr, s_w, a[0], a[1], a[2]);
+  return ncc_finalize_pre(s_ref, s_rr, s_w, a[0], a[1], a[2]);   // (inv, mref, var_ref) of patch_lds_pre
 }
 
 template <int U8>
@@ -209,7 +210,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_depth_to_weak(const Pass
   if (fast) patch_lds_build<64>(pw, pc, B, x, y, lane);
   wave_sync();
   float s_ref = 0, s_rr = 0, s_w = 0;
-  if (fast) patch_lds_sums(pw, s_ref, s_rr, s_w);
+  if (fast) patch_lds_pre(pw, s_ref, s_rr, s_w);
   PHASE(0);
   const int radius = 30;
   if (lane < 2 * radius + 1) {
@@ -338,7 +339,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_local_refine_jobs(const 
     if (!go) s_cnt[wave][gp][1] = 0;
   }
   wave_sync();
-  if (go && fast && gl == 0) patch_lds_sums(pw, s_sum[wave][gp][0], s_sum[wave][gp][1], s_sum[wave][gp][2]);
+  if (go && fast && gl == 0) patch_lds_pre(pw, s_sum[wave][gp][0], s_sum[wave][gp][1], s_sum[wave][gp][2]);
   wave_sync();
   // ---- flat job pool: (pixel, valid hypothesis, selected view)
   int total = 0;

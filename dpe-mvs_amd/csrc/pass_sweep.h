@@ -415,7 +415,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_strong_coop(const PassCo
     int n = 0;
     if (active) {
       for (int k = 0; k <= C; ++k) if (alias[k] == k) slots[n++] = k;
-      if (fast) patch_lds_sums(pw, sums_all[ps * 4 + 0], sums_all[ps * 4 + 1], sums_all[ps * 4 + 2]);
+      if (fast) patch_lds_pre(pw, sums_all[ps * 4 + 0], sums_all[ps * 4 + 1], sums_all[ps * 4 + 2]);
     }
     misc[1] = n;
   }
@@ -623,7 +623,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_strong_coop(const PassCo
 struct WeakTab {
   const float* tc;                        // centre patch (w, w*grey) pairs [n_c^2][2]
   const float* tn;                        // neighbour k=1..8: pairs at [((k-1)*9 + t)*2]
-  const float* sums;                      // [9][3]: s_ref, s_rr, s_w of each tabulated patch
+  const float* sums;                      // [9][3]: ncc_pre (1/s_w, s_ref/s_w, var_ref) of each tabulated patch
   const short2* nbl;                      // [9] neighbour pixels (nb[0] = the pixel itself)
   const uint32_t* nsv;                    // [9] selected_views of the neighbours
   int rad_c, inc_c, n_c, rad_n, inc_n, n_n;
@@ -706,7 +706,7 @@ DEV float patch_ncc_tab(const PassConst& pc, const DevBufs& B, int v, const Homo
     tab_taps<U8, false>(pc, B, v, H, cx, cy, rad, inc, n, tw, a);
   }
   count_work(B, 0, (unsigned long long)(n * n));
-  return ncc_finalize(sm[0], sm[1], sm[2], a[0], a[1], a[2]);
+  return ncc_finalize_pre(sm[0], sm[1], sm[2], a[0], a[1], a[2]);
 }
 
 // ComputeBilateralNCCNew (DPE.cu:557-690) of the tabulated weak pixel (px, py)
@@ -734,7 +734,7 @@ DEV float ncc_new_tab(const PassConst& pc, const DevBufs& B, const WeakTab& T, i
   for (int k = 1; k < DPE_NEIGHBOUR_NUM; ++k) {
     const short2 np = T.nbl[k];
     if (np.x == -1 || np.y == -1) continue;
-    const float2 nsp = project_h(H, (float)np.x, (float)np.y);
+    const float2 nsp = nfast ? project_h_fast(H, (float)np.x, (float)np.y) : project_h(H, (float)np.x, (float)np.y);
     if (nsp.x < 0 || nsp.y < 0 || nsp.x >= (float)W || nsp.y >= (float)Hh) {
       if (isSet(T.nsv[k], v - 1)) { strong_cost += 2.0f; strong_count++; }
       continue;
@@ -745,7 +745,7 @@ DEV float ncc_new_tab(const PassConst& pc, const DevBufs& B, const WeakTab& T, i
       tab_taps<U8, true, 3>(pc, B, v, H, np.x, np.y, T.rad_n, T.inc_n, 3, T.tn + (k - 1) * 18, a);
       count_work(B, 0, 9ull);
       const float* sm = T.sums + 3 * k;
-      tc = ncc_finalize(sm[0], sm[1], sm[2], a[0], a[1], a[2]);
+      tc = ncc_finalize_pre(sm[0], sm[1], sm[2], a[0], a[1], a[2]);
     } else {
       tc = T.tab_n ? patch_ncc_tab<U8>(pc, B, v, H, np.x, np.y, T.rad_n, T.inc_n, T.n_n, T.tn + (k - 1) * 18,
                                        T.sums + 3 * k)
@@ -885,9 +885,9 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassCons
         }
         a_ref += r_ref; a_rr += r_rr; a_w += r_w;
       }
-      sums[3 * k] = a_ref; sums[3 * k + 1] = a_rr; sums[3 * k + 2] = a_w;
+      ncc_pre(a_ref, a_rr, a_w, sums[3 * k], sums[3 * k + 1], sums[3 * k + 2]);
     }
-    if (c == C - 1 && fast_old) patch_lds_sums(pw, osum[0], osum[1], osum[2]);
+    if (c == C - 1 && fast_old) patch_lds_pre(pw, osum[0], osum[1], osum[2]);
     // bitwise-identical neighbour planes share one cost vector: alias = first earlier flagged row
     // with the same plane (lanes 8..15; lanes 0..8 build the sums above)
     for (int i = c - 8; i >= 0 && i < 8; i += C) {
