@@ -336,16 +336,39 @@ DEV f2v fma2(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
 // projection of the tap (row terms bxy = (h0 x + h2, h3 x + h5), bz = h6 x + h8; column yf).
 // Bit-identical to sample_quad8(project) when the tap's qz is in d_rcp_fast's exact range
 // (rcp_range_ok), with packed FP32 ops, one med3 per clamp and a 32-bit offset from one base.
+// Fixed-point coordinate of the clamped sample: trunc(fma(clamp(s, -1, lim), 256, 256.5)) computed
+// as min(cvt_u32_sat(fma(s, 256, 256.5)), 256 lim + 256).  Below -1 both give 0 (the saturating
+// conversion maps every u < 1 to 0; u(-1) = 0.5); above lim both give 256 lim + 256; in between
+// the operations are identical.  One VOP2 min replaces the med3 + signed conversion pair.
+#ifndef DPE_SAT_CLAMP
+#define DPE_SAT_CLAMP 1
+#endif
+DEV uint32_t fixed_coord(float s, uint32_t umax) {
+#if DPE_SAT_CLAMP
+  const float u = __builtin_fmaf(s, 256.0f, 256.5f);
+  uint32_t r;
+  asm("v_cvt_u32_f32 %0, %1" : "=v"(r) : "v"(u));
+  return min(r, umax);
+#else
+  const float lim = (float)((umax - 256u) >> 8);
+  return (uint32_t)(int)__builtin_fmaf(__builtin_amdgcn_fmed3f(s, -1.0f, lim), 256.0f, 256.5f);
+#endif
+}
 template <int T>
 DEV float tap_u8_fast(const DevBufs& B, uint32_t vofs, uint32_t stride, f2v lim, const float* h, f2v bxy, float bz,
                       float yf) {
   const f2v q = fma2((f2v){h[1], h[4]}, f2s(yf), bxy);
   const float iz = d_rcp_fast(__builtin_fmaf(h[7], yf, bz));
   const f2v sxy = q * f2s(iz);
+#if DPE_SAT_CLAMP
+  const uint32_t ux = fixed_coord(sxy.x, (uint32_t)lim.x * 256u + 256u);
+  const uint32_t uy = fixed_coord(sxy.y, (uint32_t)lim.y * 256u + 256u);
+#else
   const float xb = __builtin_amdgcn_fmed3f(sxy.x, -1.0f, lim.x);
   const float yb = __builtin_amdgcn_fmed3f(sxy.y, -1.0f, lim.y);
   const f2v u = fma2((f2v){xb, yb}, f2s(256.0f), f2s(256.5f));
   const uint32_t ux = (uint32_t)(int)u.x, uy = (uint32_t)(int)u.y;       // >= 0 after the clamp
+#endif
   const uint8_t* p = tex_base<T>(B) + (vofs + (__umul24(uy >> 8, stride) + (ux >> 8)) * tex_bytes<T>());
   const float ay = (float)(uy & 255u) * 0.00390625f;
   if constexpr (T == TEX_F16) {
@@ -376,11 +399,9 @@ DEV f2v tap2_fast(const DevBufs& B, uint32_t vofs, uint32_t stride, f2v lim, con
   const f2v r = (f2v){__builtin_amdgcn_rcpf(qz.x), __builtin_amdgcn_rcpf(qz.y)};
   const f2v iz = fma2(fma2(-qz, r, f2s(1.0f)), r, r);
   const f2v sx = qx * iz, sy = qy * iz;
-  const f2v xb = (f2v){__builtin_amdgcn_fmed3f(sx.x, -1.0f, lim.x), __builtin_amdgcn_fmed3f(sx.y, -1.0f, lim.x)};
-  const f2v yb = (f2v){__builtin_amdgcn_fmed3f(sy.x, -1.0f, lim.y), __builtin_amdgcn_fmed3f(sy.y, -1.0f, lim.y)};
-  const f2v ux = fma2(xb, f2s(256.0f), f2s(256.5f)), uy = fma2(yb, f2s(256.0f), f2s(256.5f));
-  const uint32_t ux0 = (uint32_t)(int)ux.x, ux1 = (uint32_t)(int)ux.y;   // >= 0 after the clamp
-  const uint32_t uy0 = (uint32_t)(int)uy.x, uy1 = (uint32_t)(int)uy.y;
+  const uint32_t mx = (uint32_t)lim.x * 256u + 256u, my = (uint32_t)lim.y * 256u + 256u;
+  const uint32_t ux0 = fixed_coord(sx.x, mx), ux1 = fixed_coord(sx.y, mx);
+  const uint32_t uy0 = fixed_coord(sy.x, my), uy1 = fixed_coord(sy.y, my);
   const uint8_t* base = tex_base<T>(B);
   const uint8_t* p0 = base + (vofs + (__umul24(uy0 >> 8, stride) + (ux0 >> 8)) * tex_bytes<T>());
   const uint8_t* p1 = base + (vofs + (__umul24(uy1 >> 8, stride) + (ux1 >> 8)) * tex_bytes<T>());
