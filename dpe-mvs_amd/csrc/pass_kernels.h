@@ -259,15 +259,19 @@ __global__ void __launch_bounds__(256, DPE_GN_WAVES) k_gen_neighbours(const Pass
   bool has_valid_plane = false;
   {
     int iteration = 50, max_iter = pc.P.high_res_img ? 200 : 125, max_count = 3;
+    // residuals[i < valid_count] are written before every read; of the rest only index
+    // DPE_NEIGHBOUR_NUM is ever read (as the reference's zero-initialised entry)
     float min_cost = 3.40282347e+38f, residuals[64];
-    for (int i = 0; i < 64; ++i) residuals[i] = 0.0f;
+    for (int i = valid_count; i <= DPE_NEIGHBOUR_NUM; ++i) residuals[i] = 0.0f;
     float temp_thr = ransac_threshold;
     // edge_test[64][64] (DPE.cu:2307) as two bit matrices: tested / crosses-an-edge
-    uint64_t tested[64], crosses[64];
-    for (int i = 0; i < 64; ++i) { tested[i] = 0; crosses[i] = 0; }
+    // rows are zeroed on first use (row_live), not up front: a thread touches a few of the 64
+    uint64_t tested[64], crosses[64], row_live = 0;
     bool has_consist_normal_plane = false;
     bool must_in_triangle = (pc.P.use_label && B.label[center] > 0 && edge_limit) ? false : true;
     auto edge_pair = [&](int a, int b) -> bool {   // returns edge_test[a][b] == 1
+      if (!((row_live >> a) & 1ull)) { tested[a] = 0; crosses[a] = 0; row_live |= 1ull << a; }
+      if (!((row_live >> b) & 1ull)) { tested[b] = 0; crosses[b] = 0; row_live |= 1ull << b; }
       if (!((tested[a] >> b) & 1ull)) {
         const bool c = bresenham(pc, B, spv[a].x, spv[a].y, spv[b].x, spv[b].y);
         tested[a] |= 1ull << b; tested[b] |= 1ull << a;
