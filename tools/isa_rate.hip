@@ -34,6 +34,14 @@ KERNEL(k_fma_mix, asm volatile("v_fma_mix_f32 %0, %0, %1, %2 op_sel_hi:[0,1,1]" 
 KERNEL(k_rcp, asm volatile("v_rcp_f32 %0, %0" : "+v"(a[i])))
 KERNEL(k_and, asm volatile("v_and_b32 %0, 0xff, %0" : "+v"(a[i])))
 KERNEL(k_cndmask, asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a[i]) : "v"(b)))
+KERNEL(k_mul_hi, asm volatile("v_mul_hi_u32 %0, %0, %1" : "+v"(a[i]) : "v"(b)))
+KERNEL(k_mul_lo, asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(a[i]) : "v"(b)))
+KERNEL(k_mul_u24, asm volatile("v_mul_u32_u24 %0, %0, %1" : "+v"(a[i]) : "v"(b)))
+KERNEL(k_xor, asm volatile("v_xor_b32 %0, %0, %1" : "+v"(a[i]) : "v"(b)))
+KERNEL(k_xad, asm volatile("v_xad_u32 %0, %0, %1, %2" : "+v"(a[i]) : "v"(b), "v"(c)))
+KERNEL(k_sqrt, asm volatile("v_sqrt_f32 %0, %0" : "+v"(a[i])))
+KERNEL(k_cvt_u32, asm volatile("v_cvt_u32_f32 %0, %0" : "+v"(a[i])))
+KERNEL(k_min_u32, asm volatile("v_min_u32 %0, %0, %1" : "+v"(a[i]) : "v"(b)))
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 #define KERNEL2(name, body)                                                          \
@@ -65,6 +73,8 @@ int main() {
       {"v_cvt_i32_f32", k_cvt_i32}, {"v_cvt_f32_ubyte0", k_cvt_ubyte}, {"v_lshrrev_b32", k_lshr},
       {"v_mad_u32_u24", k_mad24}, {"v_lshl_add_u32", k_lshl_add}, {"v_fma_mix_f32", k_fma_mix},
       {"v_rcp_f32", k_rcp}, {"v_and_b32", k_and}, {"v_cndmask_b32", k_cndmask},
+      {"v_mul_hi_u32", k_mul_hi}, {"v_mul_lo_u32", k_mul_lo}, {"v_mul_u32_u24", k_mul_u24}, {"v_xor_b32", k_xor},
+      {"v_xad_u32", k_xad}, {"v_sqrt_f32", k_sqrt}, {"v_cvt_u32_f32", k_cvt_u32}, {"v_min_u32", k_min_u32},
       {"v_pk_fma_f32", k_pk_fma}, {"v_pk_mul_f32", k_pk_mul}, {"v_pk_add_f32", k_pk_add}};
   hipEvent_t e0, e1;
   hipEventCreate(&e0); hipEventCreate(&e1);
