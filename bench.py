@@ -88,11 +88,33 @@ def cpu_baseline(abi, synthetic, seconds_hint: float = 20.0) -> dict:
         cores = os.cpu_count() or 1
     cores = max(1, min(cores, 16))
     t0 = time.perf_counter()
-    oracle.run_pass(inp, st, threads=cores)
+    ref = oracle.run_pass(inp, st, threads=cores)
     dt = time.perf_counter() - t0
-    return {"value": round(w * h / dt / 1e6, 6), "unit": "Mpix/s", "cores": cores, "kind": "port",
+    base = {"value": round(w * h / dt / 1e6, 6), "unit": "Mpix/s", "cores": cores, "kind": "port",
             "sample": f"one full REFINE_ITER+geom pass, {w}x{h}, 9 source views, oracle/ scalar C++ "
                       f"restatement, {cores} threads, {dt:.1f} s"}
+    return base, (inp, st, ref, f"{w}x{h}")
+
+
+def parity_on_sample(native, local_rank: int, sample) -> dict:
+    """The metric's "L1 vs ref": the HIP pass on the cpu_baseline sample against the oracle's output
+    of the same run (depth = plane .w; weak/selected-view maps compared exactly)."""
+    import numpy as np
+    inp, st, ref, size = sample
+    c = native.PatchMatchContext(local_rank)
+    try:
+        out = c.run(inp, st)
+    finally:
+        c.close()
+    dg, do = out["planes"][..., 3].astype(np.float64), ref["planes"][..., 3].astype(np.float64)
+    ok = np.abs(do) > 0
+    rel = np.abs(dg - do)[ok] / np.abs(do)[ok]
+    bits = {k: bool(np.array_equal(out[k].view(np.uint8), ref[k].view(np.uint8))) for k in ("planes", "weak", "sel", "costs")}
+    return {"sample": f"{size} REFINE_ITER+geom pass (the cpu_baseline sample), HIP vs oracle",
+            "depth_l1_rel": float(rel.mean()) if rel.size else 0.0,
+            "depth_max_rel": float(rel.max()) if rel.size else 0.0,
+            "weak_mismatch_px": int((out["weak"] != ref["weak"]).sum()),
+            "bit_exact": bits}
 
 
 def main():
@@ -182,6 +204,31 @@ def main():
     cnt = ctx.counts()
     ctx.set_counting(False)
 
+    # the other pass types of the schedule at the same size (reported per pass type)
+    per_type = {"refine_iter": round(value / world, 4)}
+    for kind in ("first_init", "refine_init"):
+        pk = workload_params(_abi, NV_)
+        if kind == "first_init":
+            pk.state = _abi.FIRST_INIT; pk.use_APD = False; pk.use_edge = False; pk.geom_consistency = False
+            stk = synthetic.first_init_state(sc)
+        else:
+            pk.state = _abi.REFINE_INIT; pk.geom_consistency = False; pk.rotate_time = 4
+            pk.ransac_threshold = 0.0075; pk.max_scale_size = 4; pk.weak_peak_radius = 6
+            stk = st
+        ik = synthetic.pass_input(sc, pk, depths=None)
+        ck = native.PatchMatchContext(local_rank)
+        ck.stage(ik, stk)
+        ck.execute(sp)                                   # warm-up
+        exec_s = 0.0
+        for _ in range(2):                               # each pass starts from the staged state
+            ck.stage(ik, stk)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            ck.execute(sp)
+            torch.cuda.synchronize()
+            exec_s += time.perf_counter() - t1
+        ck.close()
+        per_type[kind] = round(2 * Wd * Hd / exec_s / 1e6, 4)
     dom = max(("strong", "weak", "depth_to_weak", "local_refine", "init", "ransac", "setup"), key=lambda k: tim.get(k, 0.0))
     launches = max(1, cnt[dom]["launches"])
     flop_per_launch = algorithmic_flops(cnt[dom]) / launches
@@ -228,11 +275,13 @@ def main():
         "pass_tflops": round(pass_flops / (ms_per_step * 1e-3) / 1e12, 3),
         "stage_ms": round(stage_ms, 3),
         "pcie_inclusive_mpix_s": round(Wd * Hd / ((stage_ms + ms_per_step) * 1e-3) / 1e6, 4),
+        "pass_types_mpix_s": per_type,
         "kernel_ms": {k: round(v, 3) for k, v in tim.items()},
         "work": {k: v for k, v in cnt.items() if v["launches"]},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(_abi, synthetic)
+        result["cpu_baseline"], sample = cpu_baseline(_abi, synthetic)
+        result["parity"] = parity_on_sample(native, local_rank, sample)
     if rank == 0:
         print(json.dumps(result), flush=True)
     ctx.close()
