@@ -65,6 +65,13 @@ def lib() -> C.CDLL:
         L.dpe_host_read_camera.argtypes = [C.c_char_p, C.POINTER(_abi.DpeCamera)]
         L.dpe_host_resize_linear.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int]
         L.dpe_host_rescale_nearest.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int]
+        L.dpe_host_edge_segment.argtypes = [C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                            C.c_size_t, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        L.dpe_host_canny.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_double, C.c_void_p]
+        L.dpe_host_resize_u8.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int]
+        L.dpe_host_connect.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_int]
+        L.dpe_host_hough_lines_p.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_double, C.c_int, C.c_double,
+                                             C.c_double, C.c_void_p, C.c_int]
         _lib = L
     return _lib
 
@@ -99,6 +106,64 @@ def rescale_to(src: np.ndarray, W: int, H: int) -> np.ndarray:
     elem = s.itemsize * int(np.prod(s.shape[2:], dtype=np.int64))
     lib().dpe_host_rescale_nearest(s.ctypes.data, s.shape[1], s.shape[0], dst.ctypes.data, W, H, elem)
     return dst
+
+
+# ------------------------------------------------------------------------------ EdgeSegment (C++, edges.cpp)
+def _u8(img: np.ndarray) -> np.ndarray:
+    a = np.ascontiguousarray(img)
+    if a.dtype != np.uint8 or a.ndim != 2:
+        raise ValueError("expected a 2-D uint8 image")
+    return a
+
+
+def edge_segment(scale: int, img: np.ndarray, mode: int, use_canny: bool, high_res: bool = True) -> np.ndarray:
+    """EdgeSegment (DPE.cpp:129-291): mode 0 -> uint8 0/255 edges, mode 1 -> int32 labels."""
+    a = _u8(img)
+    ow, oh = C.c_int(), C.c_int()
+    args = (scale, a.ctypes.data, a.shape[1], a.shape[0], mode, int(use_canny), int(high_res))
+    if lib().dpe_host_edge_segment(*args, None, 0, C.byref(ow), C.byref(oh)) != 0:
+        raise PipelineError("EdgeSegment failed")
+    out = np.empty((oh.value, ow.value), np.uint8 if mode == 0 else np.int32)
+    if lib().dpe_host_edge_segment(*args, out.ctypes.data, out.nbytes, C.byref(ow), C.byref(oh)) != 0:
+        raise PipelineError("EdgeSegment failed")
+    return out
+
+
+def canny(img: np.ndarray, low: float, high: float) -> np.ndarray:
+    """cv::Canny(img, low, high, 3, L2gradient=true) -> uint8 0/255."""
+    a = _u8(img)
+    out = np.empty_like(a)
+    lib().dpe_host_canny(a.ctypes.data, a.shape[1], a.shape[0], low, high, out.ctypes.data)
+    return out
+
+
+def resize_u8(img: np.ndarray, new_w: int, new_h: int) -> np.ndarray:
+    """cv::resize(INTER_LINEAR) of an 8-bit image."""
+    a = _u8(img)
+    out = np.empty((new_h, new_w), np.uint8)
+    lib().dpe_host_resize_u8(a.ctypes.data, a.shape[1], a.shape[0], out.ctypes.data, new_w, new_h)
+    return out
+
+
+def connect(img: np.ndarray):
+    """Connect (DPE.cpp:27-127) -> (labels int32, counts per label)."""
+    a = _u8(img)
+    lab = np.empty(a.shape, np.int32)
+    n = lib().dpe_host_connect(a.ctypes.data, a.shape[1], a.shape[0], lab.ctypes.data, None, 0)
+    cnt = np.empty(max(n, 1), np.int32)
+    lib().dpe_host_connect(a.ctypes.data, a.shape[1], a.shape[0], lab.ctypes.data, cnt.ctypes.data, n)
+    return lab, cnt[:n]
+
+
+def hough_lines_p(img: np.ndarray, rho: float, theta: float, threshold: int, min_len: float, max_gap: float) -> np.ndarray:
+    """cv::HoughLinesP -> int32 [n, 4] segments (x0, y0, x1, y1)."""
+    a = _u8(img)
+    n = lib().dpe_host_hough_lines_p(a.ctypes.data, a.shape[1], a.shape[0], rho, theta, threshold, min_len, max_gap, None, 0)
+    out = np.empty((max(n, 0), 4), np.int32)
+    if n > 0:
+        lib().dpe_host_hough_lines_p(a.ctypes.data, a.shape[1], a.shape[0], rho, theta, threshold, min_len, max_gap,
+                                     out.ctypes.data, n)
+    return out
 
 
 # ------------------------------------------------------------------------------ dataset writers

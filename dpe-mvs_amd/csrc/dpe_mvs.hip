@@ -23,7 +23,10 @@
 using namespace dpe;
 
 static const int kDefaultXcdRows = 1;
-static constexpr int kWeakLanes = 16;   // lanes per weak pixel in k_weak_coop
+#ifndef DPE_WEAK_LANES
+#define DPE_WEAK_LANES 16
+#endif
+static constexpr int kWeakLanes = DPE_WEAK_LANES;   // lanes per weak pixel in k_weak_coop (16 or 32)
 // source-image layout of each kernel for 8-bit grey-level images (pass_common.h TEX_*): TEX_F16
 // issues fewer VALU ops per tap, TEX_U8 touches half the bytes (better for scattered gathers)
 #ifndef DPE_TEX_STRONG

@@ -73,8 +73,12 @@ DEV void lds_taps(const float* pw, int px, int py, const PassConst& pc, const De
     const f2v* wp = (const f2v*)pw;
     f2v s_sr = f2s(0.0f);
     float s_ss = 0;
-#if DPE_UNROLL_ROWS
+#if DPE_UNROLL_ROWS == 1
 #pragma unroll
+#elif DPE_UNROLL_ROWS == 2
+#pragma unroll 2
+#elif DPE_UNROLL_ROWS == 3
+#pragma unroll 3
 #else
 #pragma unroll 1
 #endif

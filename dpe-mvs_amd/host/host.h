@@ -1,6 +1,7 @@
 // host.h — internal interfaces of the host pipeline (libdpe_host.so).  Plain C++17, no HIP: the
 // device work goes through the C-ABI of dpe_mvs.h.
 #pragma once
+#include <array>
 #include <cstdint>
 #include <string>
 #include <vector>
@@ -39,5 +40,19 @@ void resize_linear(const float* src, int w, int h, float* dst, int nw, int nh);
 void rescale_nearest(const void* src, int w, int h, void* dst, int nw, int nh, int elem);
 
 std::string fmt_index(int i);   // ToFormatIndex: %08d
+
+// edges.cpp: EdgeSegment and the OpenCV operations it uses (DPE.cpp:9-291, main.cpp:331-388)
+void resize_u8(const uint8_t* src, int w, int h, uint8_t* dst, int nw, int nh);
+void threshold_binary(uint8_t* img, size_t n, int thr);
+void canny_l2(const uint8_t* src, int w, int h, double low, double high, uint8_t* dst);
+void roberts(const uint8_t* src, int w, int h, uint8_t* dst);
+void connect(const uint8_t* img, int w, int h, int* label, std::vector<int>& label_cnt);
+void draw_line(uint8_t* img, int w, int h, int x0, int y0, int x1, int y1, uint8_t value);
+void hough_lines_p(const uint8_t* img, int w, int h, double rho, double theta, int threshold, double min_len,
+                   double max_gap, std::vector<std::array<int, 4>>& lines);
+bool edge_segment(int scale, const uint8_t* src, int cols, int rows, int mode, bool use_canny, bool high_res, Mat& out,
+                  std::string& err);
+bool get_problem_edges(const GrayImage& full, int scale_size, const std::string& result_folder, bool use_edge,
+                       bool use_label, bool high_res, std::string& err);
 
 }  // namespace dpe_host

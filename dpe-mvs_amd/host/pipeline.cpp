@@ -12,8 +12,10 @@
 // maps are all-gathered after every pass; "reference" schedule = the reference's serial order,
 // "jacobi" = each pass reads the previous pass's depths (forced when world_size > 1).
 //
-// Not part of this build: EdgeSegment (the edge/label maps must exist), RunFusion
-// (fusion=true fails), the viz medium results (ignored).
+// GetProblemEdges (main.cpp:331-388) runs before the first pass as in the reference: edges_<s>.dmb /
+// labels_<s>.dmb that are missing are computed by EdgeSegment (edges.cpp) and written.
+// Not part of this build: RunFusion (fusion=true fails), the viz medium results
+// (ignored).
 #include "host.h"
 
 #include <cmath>
@@ -159,8 +161,7 @@ std::vector<T> rescaled(const std::vector<T>& src, int w, int h, int nw, int nh,
 bool read_support(const Problem& p, const std::string& name, Mat& m, std::string& err) {
   const std::string path = (fs::path(p.result_folder) / name).string();
   if (!fs::exists(path)) {
-    err = path + " missing: the EdgeSegment edge/label precompute (DPE.cpp:9-291) is not part of this build "
-                 "(SURVEY.md §8f); provide edges_<s>.dmb / labels_<s>.dmb";
+    err = path + " missing (GetProblemEdges writes it before the first pass)";
     return false;
   }
   return read_bin_mat(path, m, err);
@@ -367,6 +368,20 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
     std::printf("There are %d images to be processed!\n", n);
     std::printf("There are %d resolution stages for coarse-to-fine processing!\n", round_num);
     std::printf("Iteration nums: %d\n", round_num * 4);
+  }
+  for (int pi : blocks[rank]) {   // GetProblemEdges for every scale of the schedule (main.cpp:494-501)
+    const Problem& p = problems[pi];
+    int fw, fh;
+    const std::vector<float>* f = cache.full(p.ref_image_id, fw, fh, err);
+    if (!f) return 1;
+    GrayImage g;
+    g.w = fw; g.h = fh;
+    g.px.resize(f->size());
+    for (size_t k = 0; k < f->size(); ++k) g.px[k] = (uint8_t)(*f)[k];
+    for (int i = 0; i < round_num; ++i)
+      if (!get_problem_edges(g, (int)std::pow(2, round_num - 1 - i), p.result_folder, p.params.use_edge,
+                             p.params.use_label, p.params.high_res_img, err))
+        return 1;
   }
   for (auto& p : problems) p.params.max_scale_size = std::max(1, (int)std::pow(2, round_num - 1));
   std::map<int, ImageState> states;

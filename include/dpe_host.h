@@ -11,6 +11,12 @@
  *   cv::imread(IMREAD_GRAYSCALE)                 dpe_host_read_gray (JPEG islow luma / PGM)
  *   cv::resize(INTER_LINEAR)  DPE.cpp:808        dpe_host_resize_linear
  *   RescaleMatToTargetSize    DPE.cpp:1146       dpe_host_rescale_nearest
+ *   EdgeSegment               DPE.cpp:129-291    dpe_host_edge_segment (GetProblemEdges, main.cpp:331,
+ *                                                runs inside dpe_run_pipeline for missing maps)
+ *   cv::Canny(L2, aperture 3) DPE.cpp:226        dpe_host_canny
+ *   cv::resize INTER_LINEAR 8U DPE.cpp:145,230   dpe_host_resize_u8
+ *   Connect                   DPE.cpp:27-127     dpe_host_connect
+ *   cv::HoughLinesP           DPE.cpp:186        dpe_host_hough_lines_p
  *
  * Additions for the one-process-per-GPU deployment: a pass runner hook (default: the HIP library
  * on `gpu_index`) and an all-gather hook for the depth maps (RCCL in the CLI, torch.distributed
@@ -65,6 +71,23 @@ void dpe_host_resize_linear(const float* src, int w, int h, float* dst, int nw, 
 /* RescaleMatToTargetSize: nearest with the reference's swapped factors; `elem` bytes per pixel;
  * destination pixels whose source falls outside keep their (caller-initialised) value. */
 void dpe_host_rescale_nearest(const void* src, int w, int h, void* dst, int nw, int nh, int elem);
+
+/* EdgeSegment (DPE.cpp:129-291): mode 0 = edges (uint8 0/255, same size as src, use_canny = 1 in the
+ * reference's call), mode 1 = labels (int32: -1 small region, 0 boundary, > 0 region; size
+ * round(src / 2^scale), use_canny = 0).  Writes up to `cap` bytes into `out` (NULL: size query via
+ * *ow, *oh).  0 on success. */
+int dpe_host_edge_segment(int scale, const uint8_t* src, int w, int h, int mode, int use_canny, int high_res, void* out,
+                          size_t cap, int* ow, int* oh);
+/* cv::Canny(src, dst, low, high, 3, L2gradient = true): dst uint8 0/255.  0 on success. */
+int dpe_host_canny(const uint8_t* src, int w, int h, double low, double high, uint8_t* dst);
+/* cv::resize(INTER_LINEAR) of a CV_8UC1 image (exact 1/2: INTER_AREA fast path).  0 on success. */
+int dpe_host_resize_u8(const uint8_t* src, int w, int h, uint8_t* dst, int nw, int nh);
+/* Connect (DPE.cpp:27-127): labels of the 4-connected zero regions (255 -> 0); returns the label
+ * count (label_cnt entries, written up to cnt_cap) or -1. */
+int dpe_host_connect(const uint8_t* img, int w, int h, int* label, int* cnt, int cnt_cap);
+/* cv::HoughLinesP: writes up to `cap` segments (x0, y0, x1, y1) into `lines`; returns the count or -1. */
+int dpe_host_hough_lines_p(const uint8_t* img, int w, int h, double rho, double theta, int threshold, double min_len,
+                           double max_gap, int* lines, int cap);
 
 #ifdef __cplusplus
 }

@@ -147,11 +147,16 @@ def test_rescale_swapped_factors_quirk():
 
 
 # ------------------------------------------------------------------------------ pipeline
-def test_missing_edges_is_a_clear_error(tmp_path, dense4):
+def test_missing_edge_map_is_regenerated(tmp_path, dense4):
+    # GetProblemEdges (main.cpp:331-388): a missing edges_<s>.dmb is computed by EdgeSegment
     d = _copy(dense4, tmp_path, "noedge")
-    os.remove(os.path.join(d, "DPE", "00000000", "edges_1.dmb"))
-    with pytest.raises(pipeline.PipelineError, match="EdgeSegment"):
-        pipeline.run_dpe_pipeline(d, runner=oracle_runner(), verbose=False)
+    p = os.path.join(d, "DPE", "00000000", "edges_1.dmb")
+    os.remove(p)
+    assert pipeline.run_dpe_pipeline(d, runner=oracle_runner(), verbose=False, keep_intermediate=True) == 0
+    img = pipeline.read_gray(os.path.join(d, "images", "00000000.jpg"))
+    half = pipeline.resize_linear(img, 32, 24)
+    e = pipeline.read_bin_mat(p)
+    assert np.array_equal(e, pipeline.edge_segment(1, np.rint(half).astype(np.uint8), 0, True, True))
 
 
 def test_fusion_not_built(dense4):
