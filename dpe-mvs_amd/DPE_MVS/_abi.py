@@ -31,6 +31,11 @@ class DpeCamera(C.Structure):
     ]
 
 
+class DpeFusionView(C.Structure):   # include/dpe_mvs.h (RunFusion's projection tests)
+    _fields_ = [("width", C.c_int), ("height", C.c_int), ("cam", DpeCamera),
+                ("depth", C.c_void_p), ("normal", C.c_void_p)]
+
+
 class DpePatchMatchParams(C.Structure):
     _fields_ = [
         ("max_iterations", C.c_int),

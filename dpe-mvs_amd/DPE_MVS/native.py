@@ -19,6 +19,7 @@ EXPORTED = [
     "dpe_params_default", "dpe_create", "dpe_destroy", "dpe_last_error", "dpe_pm_stage",
     "dpe_pm_execute", "dpe_pm_fetch", "dpe_pm_run", "dpe_pm_device_planes", "dpe_pm_export_depth",
     "dpe_pm_last_timings", "dpe_set_timing", "dpe_set_counting", "dpe_pm_last_counts",
+    "dpe_fusion_stage", "dpe_fusion_candidates",
 ]
 
 CLASSES = ["setup", "init", "strong", "ransac", "weak", "filter", "depth_to_weak", "local_refine"]

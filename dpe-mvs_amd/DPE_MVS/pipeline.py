@@ -41,6 +41,7 @@ class DpePipelineOptions(C.Structure):
         ("runner", C.c_void_p), ("runner_user", C.c_void_p),
         ("base_seed", C.c_uint64),
         ("keep_intermediate", C.c_bool),
+        ("fusion_runner", C.c_void_p), ("fusion_user", C.c_void_p),
     ]
 
 
@@ -65,6 +66,7 @@ def lib() -> C.CDLL:
         L.dpe_host_read_camera.argtypes = [C.c_char_p, C.POINTER(_abi.DpeCamera)]
         L.dpe_host_resize_linear.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int]
         L.dpe_host_rescale_nearest.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int]
+        L.dpe_host_read_bgr.argtypes = [C.c_char_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_int), C.POINTER(C.c_int)]
         L.dpe_host_edge_segment.argtypes = [C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
                                             C.c_size_t, C.POINTER(C.c_int), C.POINTER(C.c_int)]
         L.dpe_host_canny.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_double, C.c_void_p]
@@ -83,6 +85,16 @@ def read_gray(path: str) -> np.ndarray:
         raise PipelineError(f"cannot decode {path}")
     out = np.empty((h.value, w.value), np.uint8)
     lib().dpe_host_read_gray(path.encode(), out.ctypes.data, out.nbytes, C.byref(w), C.byref(h))
+    return out
+
+
+def read_bgr(path: str) -> np.ndarray:
+    """cv::imread(path, IMREAD_COLOR): uint8 [H, W, 3] BGR."""
+    w, h = C.c_int(), C.c_int()
+    if lib().dpe_host_read_bgr(path.encode(), None, 0, C.byref(w), C.byref(h)) != 0:
+        raise PipelineError(f"cannot decode {path}")
+    out = np.empty((h.value, w.value, 3), np.uint8)
+    lib().dpe_host_read_bgr(path.encode(), out.ctypes.data, out.nbytes, C.byref(w), C.byref(h))
     return out
 
 
@@ -234,10 +246,11 @@ def _torch_allgather(dist):
 def run_dpe_pipeline(dense_folder: str, gpu_index: int = 0, verbose: bool = True, fusion: bool = False,
                      viz: bool = False, depth: bool = True, normal: bool = False, weak: bool = False,
                      edge: bool = False, schedule: str = "reference", dist=None, runner=None,
-                     base_seed: int = 0x5EED, keep_intermediate: bool = False) -> int:
+                     base_seed: int = 0x5EED, keep_intermediate: bool = False, fusion_runner=None) -> int:
     """RunDPEPipeline (main.cpp:474) through libdpe_host.  `dist`: an initialised torch.distributed
     (one process per GPU; problems split in contiguous blocks, depth maps all-gathered per pass).
-    `runner`: (C function pointer, user pointer) of a dpe_pass_runner_fn; default the HIP library."""
+    `runner`: (C function pointer, user pointer) of a dpe_pass_runner_fn; default the HIP library.
+    `fusion_runner`: (C function pointer, user pointer) of a dpe_fusion_fn; default the HIP kernel."""
     o = DpePipelineOptions()
     lib().dpe_pipeline_default_options(C.byref(o))
     o.gpu_index = gpu_index
@@ -254,6 +267,9 @@ def run_dpe_pipeline(dense_folder: str, gpu_index: int = 0, verbose: bool = True
     if runner is not None:
         o.runner = C.cast(runner[0], C.c_void_p)
         o.runner_user = C.cast(runner[1], C.c_void_p) if runner[1] is not None else None
+    if fusion_runner is not None:
+        o.fusion_runner = C.cast(fusion_runner[0], C.c_void_p)
+        o.fusion_user = C.cast(fusion_runner[1], C.c_void_p) if fusion_runner[1] is not None else None
     rc = lib().dpe_run_pipeline(dense_folder.encode(), C.byref(o))
     if rc != 0:
         raise PipelineError(lib().dpe_pipeline_last_error().decode(errors="replace"))

@@ -18,6 +18,7 @@
 
 #include "pass_kernels.h"
 #include "pass_refine.h"
+#include "pass_fusion.h"
 #include "pass_sweep.h"
 
 using namespace dpe;
@@ -110,6 +111,15 @@ struct DpeContext {
   DevArr<int> tab_right, tab_down;   // FindNearestStrongPoint tables
   DevArr<int> lists, row_counts, list_totals;   // per-colour pixel lists for the sweeps
   DevBufs bufs;
+  // fusion (dpe_fusion_stage / dpe_fusion_candidates)
+  std::vector<DevArr<float>> fz_depth, fz_normal;
+  std::vector<FusionViewDev> fz_host;
+  DevArr<FusionViewDev> fz_views;
+  DevArr<DpeCamera> fz_cams;
+  DevArr<int> fz_src;
+  DevArr<int32_t> fz_idx;
+  DevArr<float> fz_val;
+  int fz_n = 0;
 };
 
 extern "C" {
@@ -165,6 +175,9 @@ void dpe_destroy(DpeContext* c) {
   if (!c) return;
   hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
+  for (auto& a : c->fz_depth) a.release();
+  for (auto& a : c->fz_normal) a.release();
+  c->fz_views.release(); c->fz_cams.release(); c->fz_src.release(); c->fz_idx.release(); c->fz_val.release();
   for (auto& e : c->ev) hipEventDestroy(e);
   c->dc.release();
   for (int i = 0; i < DPE_MAX_IMAGES; ++i) { c->img_plain[i].release(); c->imgq[i].release(); c->depth[i].release(); }
@@ -566,6 +579,55 @@ extern "C" int dpe_pm_export_depth(DpeContext* c, float* dev_dst, void* stream_)
   const size_t L = (size_t)c->hc.W * c->hc.H;
   k_export_depth<<<(unsigned)((L + 255) / 256), 256, 0, s>>>(c->bufs.planes, dev_dst, L);
   HIPC(hipGetLastError());
+  return DPE_OK;
+}
+
+extern "C" int dpe_fusion_stage(DpeContext* c, const DpeFusionView* views, int n) {
+  g_err.clear();
+  if (!c || !views || n < 1) { g_err = "dpe_fusion_stage: bad argument"; return DPE_ERR_ARG; }
+  HIPC(hipSetDevice(c->device));
+  c->fz_depth.resize(n); c->fz_normal.resize(n); c->fz_host.assign(n, FusionViewDev{});
+  std::vector<DpeCamera> cams(n);
+  for (int i = 0; i < n; ++i) {
+    const DpeFusionView& v = views[i];
+    if (v.width < 1 || v.height < 1 || !v.depth || !v.normal) { g_err = "dpe_fusion_stage: bad view"; return DPE_ERR_ARG; }
+    const size_t L = (size_t)v.width * v.height;
+    HIPC(c->fz_depth[i].ensure(L));
+    HIPC(c->fz_normal[i].ensure(3 * L));
+    HIPC(hipMemcpyAsync(c->fz_depth[i].p, v.depth, L * 4, hipMemcpyHostToDevice, c->stream));
+    HIPC(hipMemcpyAsync(c->fz_normal[i].p, v.normal, 3 * L * 4, hipMemcpyHostToDevice, c->stream));
+    c->fz_host[i] = FusionViewDev{c->fz_depth[i].p, c->fz_normal[i].p, v.width, v.height};
+    cams[i] = v.cam;
+  }
+  HIPC(c->fz_views.ensure(n));
+  HIPC(c->fz_cams.ensure(n));
+  HIPC(hipMemcpyAsync(c->fz_views.p, c->fz_host.data(), n * sizeof(FusionViewDev), hipMemcpyHostToDevice, c->stream));
+  HIPC(hipMemcpyAsync(c->fz_cams.p, cams.data(), n * sizeof(DpeCamera), hipMemcpyHostToDevice, c->stream));
+  HIPC(hipStreamSynchronize(c->stream));
+  c->fz_n = n;
+  return DPE_OK;
+}
+
+extern "C" int dpe_fusion_candidates(DpeContext* c, int ref, const int* src, int ns, int32_t* idx, float* val) {
+  g_err.clear();
+  if (!c || !src || !idx || !val || ns < 0) { g_err = "dpe_fusion_candidates: bad argument"; return DPE_ERR_ARG; }
+  if (c->fz_n < 1) { g_err = "dpe_fusion_candidates: nothing staged"; return DPE_ERR_STATE; }
+  if (ref < 0 || ref >= c->fz_n) { g_err = "dpe_fusion_candidates: bad reference view"; return DPE_ERR_ARG; }
+  for (int j = 0; j < ns; ++j)
+    if (src[j] < 0 || src[j] >= c->fz_n) { g_err = "dpe_fusion_candidates: bad source view"; return DPE_ERR_ARG; }
+  if (ns == 0) return DPE_OK;
+  HIPC(hipSetDevice(c->device));
+  const size_t L = (size_t)c->fz_host[ref].w * c->fz_host[ref].h;
+  HIPC(c->fz_src.ensure(ns));
+  HIPC(c->fz_idx.ensure(L * ns));
+  HIPC(c->fz_val.ensure(L * ns * 3));
+  HIPC(hipMemcpyAsync(c->fz_src.p, src, ns * sizeof(int), hipMemcpyHostToDevice, c->stream));
+  k_fusion_candidates<<<(unsigned)((L + 255) / 256), 256, 0, c->stream>>>(c->fz_cams.p, c->fz_views.p, ref, c->fz_src.p, ns,
+                                                                         c->fz_idx.p, c->fz_val.p);
+  HIPC(hipGetLastError());
+  HIPC(hipMemcpyAsync(idx, c->fz_idx.p, L * ns * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  HIPC(hipMemcpyAsync(val, c->fz_val.p, L * ns * 3 * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+  HIPC(hipStreamSynchronize(c->stream));
   return DPE_OK;
 }
 

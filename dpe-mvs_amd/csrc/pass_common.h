@@ -660,13 +660,18 @@ DEV float ncc_new(const PassConst& pc, const DevBufs& B, int px, int py, int v, 
   return cost;
 }
 
-// ComputeGeomConsistencyCost (DPE.cu:915-953)
-DEV float geom_cost(const PassConst& pc, const DevBufs& B, int px, int py, int v, const float4& pl) {
+// ComputeGeomConsistencyCost (DPE.cu:915-953), split where the view enters: the pixel's world point
+// under the plane (depth_from_plane + Get3DPointonWorld) is the same for every source view, so a
+// caller that scores one plane against several views computes it once (same operations, same bits).
+DEV float3 geom_point(const PassConst& pc, int px, int py, const float4& pl) {
+  const DpeCamera& rc = pc.cams[0];
+  const float depth = depth_from_plane(rc, pl, px, py);
+  return world_point((float)px, (float)py, depth, rc);
+}
+DEV float geom_cost_at(const PassConst& pc, const DevBufs& B, int px, int py, int v, const float3& fw) {
   if (B.cnt) atomicAdd(B.cnt + 2, 1ull);
   const DpeCamera& rc = pc.cams[0];
   const DpeCamera& sc = pc.cams[v];
-  const float depth = depth_from_plane(rc, pl, px, py);
-  const float3 fw = world_point((float)px, (float)py, depth, rc);
   const float2 sp = project_cam(fw, sc);
   const float src_depth = depth_texel(B.depth[v], pc.W, pc.H, sp.x, sp.y);
   if (src_depth == 0.0f) return 3.0f;
@@ -675,6 +680,9 @@ DEV float geom_cost(const PassConst& pc, const DevBufs& B, int px, int py, int v
   const float dc = (float)px - bp.x, dr = (float)py - bp.y;
   const float cc = __builtin_sqrtf(dc * dc + dr * dr);
   return __builtin_fminf(3.0f, cc);
+}
+DEV float geom_cost(const PassConst& pc, const DevBufs& B, int px, int py, int v, const float4& pl) {
+  return geom_cost_at(pc, B, px, py, v, geom_point(pc, px, py, pl));
 }
 
 // ------------------------------------------------------------------------------ edges / triangles

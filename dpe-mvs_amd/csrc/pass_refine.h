@@ -225,6 +225,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_depth_to_weak(const Pass
     else {
       float4 tp = op;
       tp.w = dist2origin(c0, x, y, p_depth, tp);
+      const float3 fw = pc.P.geom_consistency ? geom_point(pc, x, y, tp) : make_float3(0.0f, 0.0f, 0.0f);
       float p_cost = 0.0f;
       for (int si = 1; si < pc.N; ++si) {
         const int vi = si - 1;
@@ -232,7 +233,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_depth_to_weak(const Pass
           float tcst = 0.0f;
           tcst += ncc_old_any<U8>(fast, pw, s_ref, s_rr, s_w, x, y, pc, B, si, tp);
           PHASE(1);
-          if (pc.P.geom_consistency) tcst += pc.P.geom_factor * geom_cost(pc, B, x, y, si, tp);
+          if (pc.P.geom_consistency) tcst += pc.P.geom_factor * geom_cost_at(pc, B, x, y, si, fw);
           PHASE(2);
           p_cost += (tcst * vw[vi]);
         }
@@ -288,6 +289,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_local_refine_jobs(const 
   __shared__ float4 s_hyp[4][kLrPix][12];
   extern __shared__ float s_dyn[];                // [4 waves][kLrPix][12][nv][2] job results
   __shared__ float s_tc[4][kLrPix][12];
+  __shared__ float3 s_fw[4][kLrPix][12];          // geometric-consistency world point of each hypothesis
   __shared__ uint8_t s_sel[4][kLrPix][DPE_MAX_IMAGES];
   __shared__ int s_cnt[4][kLrPix][2];           // [0] selected views, [1] hypothesis mask (bit 11 = current)
   const PassConst& pc = *pcp;
@@ -333,6 +335,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_local_refine_jobs(const 
       tp.w = dist2origin(c0, x, y, od, tp);
     }
     s_hyp[wave][gp][gl] = tp;
+    if (pc.P.geom_consistency) s_fw[wave][gp][gl] = geom_point(pc, x, y, tp);
     const uint64_t m = __ballot(ok) >> (gp * 16);
     if (gl == 0) s_cnt[wave][gp][1] = (int)(m & 0xFFFu);
   }
@@ -367,7 +370,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_local_refine_jobs(const 
     const float* sm = s_sum[wave][p];
     float* rr = res + ((p * 12 + h) * nv + k) * 2;
     rr[0] = ncc_old_any<U8>(fast, s_patch[wave][p], sm[0], sm[1], sm[2], jx, jy, pc, B, si, tp);
-    if (pc.P.geom_consistency) rr[1] = geom_cost(pc, B, jx, jy, si, tp);
+    if (pc.P.geom_consistency) rr[1] = geom_cost_at(pc, B, jx, jy, si, s_fw[wave][p][h]);
   }
   wave_sync();
   // ---- per-hypothesis sums over views in ascending order (DPE.cu:2776-2795, 2805-2818)

@@ -971,12 +971,13 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassCons
     }
     for (int i = c; i < 8; i += C) {
       const bool fl = misc[8 + i] != 0;
+      const float3 fwi = (geom && fl) ? geom_point(pc, x, y, cpl[i]) : make_float3(0.0f, 0.0f, 0.0f);
       float f = 0.0f;
       for (int j = 0; j < nv; ++j) {
         const int w = vwl[j];
         if (w > 0) {
           if (geom) {
-            if (fl) f += w * (cost[i * nv + j] + gf * geom_cost(pc, B, x, y, j + 1, cpl[i]));
+            if (fl) f += w * (cost[i * nv + j] + gf * geom_cost_at(pc, B, x, y, j + 1, fwi));
             else f += w * (cost[i * nv + j] + gf * 3.0f);
           } else {
             f += w * cost[i * nv + j];

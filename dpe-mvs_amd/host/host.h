@@ -14,8 +14,15 @@ struct GrayImage {
   int w = 0, h = 0;
   std::vector<uint8_t> px;
 };
+struct ColorImage {                 // cv::imread(IMREAD_COLOR): 8-bit BGR, row-major
+  int w = 0, h = 0;
+  std::vector<uint8_t> bgr;
+};
+bool decode_jpeg(const uint8_t* data, size_t size, bool color, GrayImage* gray, ColorImage* bgr, std::string& err);
 bool decode_jpeg_luma(const uint8_t* data, size_t size, GrayImage& img, std::string& err);
+bool decode_jpeg_bgr(const uint8_t* data, size_t size, ColorImage& img, std::string& err);
 bool read_gray(const std::string& path, GrayImage& img, std::string& err);
+bool read_bgr(const std::string& path, ColorImage& img, std::string& err);
 
 // cv::Mat as the .dmb files carry it: OpenCV type code + raw rows (DPE.cpp:293-339)
 enum { CV_8UC1 = 0, CV_8SC1 = 1, CV_32SC1 = 4, CV_32FC1 = 5, CV_32FC3 = 21 };
@@ -54,5 +61,21 @@ bool edge_segment(int scale, const uint8_t* src, int cols, int rows, int mode, b
                   std::string& err);
 bool get_problem_edges(const GrayImage& full, int scale_size, const std::string& result_folder, bool use_edge,
                        bool use_label, bool high_res, std::string& err);
+
+// fusion.cpp: RunFusion (DPE.cpp:1220-1370) / ExportPointCloud (DPE.cpp:532-572)
+struct FusionView {
+  int image_id = 0;
+  std::vector<int> src_ids;          // pair.txt order
+  DpeFusionView view{};              // size, camera, depth, normal (borrowed pointers)
+  const uint8_t* weak = nullptr;     // PixelState [H][W]
+  std::vector<uint8_t> bgr;          // colour image at the map size
+  std::vector<uint8_t> block;        // blocks/mask_<id>.jpg at the map size, or empty
+  std::vector<uint8_t> mask;         // fusion masks (set by run_fusion)
+};
+struct FusedPoint { float x, y, z, b, g, r; };
+bool run_fusion(std::vector<FusionView>& views, dpe_fusion_fn fn, void* user, std::vector<FusedPoint>& cloud,
+                std::string& err);
+FusedPoint fusion_point(int x, int y, float depth, const DpeCamera& cam, const float* bgr);
+bool export_point_cloud(const std::string& path, const std::vector<FusedPoint>& cloud, std::string& err);
 
 }  // namespace dpe_host

@@ -125,6 +125,22 @@ bool read_gray(const std::string& path, GrayImage& img, std::string& err) {
   return false;
 }
 
+bool read_bgr(const std::string& path, ColorImage& img, std::string& err) {   // cv::imread(IMREAD_COLOR)
+  std::ifstream in(path, std::ios::binary);
+  if (!in) { err = "cannot read image: " + path; return false; }
+  std::vector<uint8_t> buf((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
+  if (buf.size() >= 2 && buf[0] == 0xFF && buf[1] == 0xD8) {
+    if (!decode_jpeg_bgr(buf.data(), buf.size(), img, err)) { err = path + ": " + err; return false; }
+    return true;
+  }
+  GrayImage g;
+  if (!read_gray(path, g, err)) return false;
+  img.w = g.w; img.h = g.h;
+  img.bgr.resize(g.px.size() * 3);
+  for (size_t i = 0; i < g.px.size(); ++i) img.bgr[3 * i] = img.bgr[3 * i + 1] = img.bgr[3 * i + 2] = g.px[i];
+  return true;
+}
+
 namespace {
 struct Taps { std::vector<int> s0, s1; std::vector<float> a0, a1; };
 Taps linear_taps(int n_src, int n_dst) {
@@ -186,6 +202,19 @@ int dpe_host_read_gray(const char* path, uint8_t* out, size_t cap, int* w, int* 
   if (w) *w = img.w;
   if (h) *h = img.h;
   if (out && cap) std::memcpy(out, img.px.data(), std::min(cap, img.px.size()));
+  return 0;
+}
+
+int dpe_host_read_bgr(const char* path, uint8_t* out, size_t cap, int* w, int* h) {
+  dpe_host::ColorImage img;
+  std::string err;
+  if (!path || !dpe_host::read_bgr(path, img, err)) return 1;
+  if (w) *w = img.w;
+  if (h) *h = img.h;
+  if (out) {
+    if (cap < img.bgr.size()) return 2;
+    std::memcpy(out, img.bgr.data(), img.bgr.size());
+  }
   return 0;
 }
 

@@ -1,7 +1,10 @@
-// jpeg.cpp — baseline / extended-sequential JPEG decoder producing the luma plane.
+// jpeg.cpp — baseline / extended-sequential JPEG decoder: the luma plane, or BGR colour.
 //
 // Stands in for cv::imread(path, IMREAD_GRAYSCALE) (DPE.cpp:745, 755; main.cpp:316, 337), which
-// asks libjpeg for JCS_GRAYSCALE output: the decoded Y component, no colour conversion.  The
+// asks libjpeg for JCS_GRAYSCALE output: the decoded Y component, no colour conversion; and for
+// cv::imread(path, IMREAD_COLOR) (RunFusion, DPE.cpp:1253): libjpeg's default "fancy" triangular
+// chroma upsampling (h2v1 / h2v2, edge rows and columns replicated) and its fixed-point YCbCr->RGB
+// tables (16-bit scale, round half up), delivered as BGR.  The
 // inverse DCT is the IJG "islow" integer algorithm (the libjpeg / libjpeg-turbo default), written
 // from its published description: Loeffler-Ligtenberg-Moschytz 8-point IDCT, 13-bit constants,
 // 2 extra bits of precision between the column and row passes, descale with rounding, +128 and
@@ -160,7 +163,66 @@ void idct_islow(const int* coef /* dequantised, natural order */, uint8_t* out, 
 
 }  // namespace
 
-bool decode_jpeg_luma(const uint8_t* data, size_t size, GrayImage& img, std::string& err) {
+namespace {
+// fancy upsampling of one chroma plane (jdsample.c h2v1 / h2v2), replication for other ratios
+void upsample_plane(const std::vector<uint8_t>& P, int st, int dw, int dh, int fx, int fy, int W, int H,
+                    std::vector<uint8_t>& out) {
+  out.assign((size_t)W * H, 0);
+  auto at = [&](int x, int y) { return (int)P[(size_t)y * st + x]; };
+  if (fx == 1 && fy == 1) {
+    for (int y = 0; y < H; ++y) for (int x = 0; x < W; ++x) out[(size_t)y * W + x] = (uint8_t)at(x, y);
+    return;
+  }
+  std::vector<int> row((size_t)2 * dw + 2);
+  if (fx == 2 && fy == 1) {
+    for (int y = 0; y < H && y < dh; ++y) {
+      int* o = row.data();
+      int v = at(0, y);
+      *o++ = v;
+      *o++ = (v * 3 + at(1, y) + 2) >> 2;
+      for (int i = 1; i <= dw - 2; ++i) {
+        v = at(i, y) * 3;
+        *o++ = (v + at(i - 1, y) + 1) >> 2;
+        *o++ = (v + at(i + 1, y) + 2) >> 2;
+      }
+      const int i = dw - 1;
+      v = at(i, y);
+      *o++ = (v * 3 + at(i > 0 ? i - 1 : 0, y) + 1) >> 2;
+      *o++ = v;
+      for (int x = 0; x < W; ++x) out[(size_t)y * W + x] = (uint8_t)row[x];
+    }
+    return;
+  }
+  if (fx == 2 && fy == 2) {
+    for (int yi = 0; yi < dh; ++yi)
+      for (int v = 0; v < 2; ++v) {
+        const int oy = 2 * yi + v;
+        if (oy >= H) break;
+        const int y1 = v == 0 ? (yi > 0 ? yi - 1 : 0) : (yi + 1 < dh ? yi + 1 : dh - 1);   // context rows replicated
+        auto cs = [&](int x) { return at(x, yi) * 3 + at(x, y1); };
+        int* o = row.data();
+        int thiscs = cs(0), nextcs = cs(1);
+        *o++ = (thiscs * 4 + 8) >> 4;
+        *o++ = (thiscs * 3 + nextcs + 7) >> 4;
+        int lastcs = thiscs; thiscs = nextcs;
+        for (int i = 2; i <= dw - 1; ++i) {
+          nextcs = cs(i);
+          *o++ = (thiscs * 3 + lastcs + 8) >> 4;
+          *o++ = (thiscs * 3 + nextcs + 7) >> 4;
+          lastcs = thiscs; thiscs = nextcs;
+        }
+        *o++ = (thiscs * 3 + lastcs + 8) >> 4;
+        *o++ = (thiscs * 4 + 7) >> 4;
+        for (int x = 0; x < W; ++x) out[(size_t)oy * W + x] = (uint8_t)row[x];
+      }
+    return;
+  }
+  for (int y = 0; y < H; ++y)
+    for (int x = 0; x < W; ++x) out[(size_t)y * W + x] = (uint8_t)at(std::min(x / fx, dw - 1), std::min(y / fy, dh - 1));
+}
+}  // namespace
+
+bool decode_jpeg(const uint8_t* data, size_t size, bool color, GrayImage* gray, ColorImage* bgr, std::string& err) {
   Reader r{data, size};
   if (r.u16() != 0xFFD8) { err = "not a JPEG file"; return false; }
   uint16_t qt[4][64];
@@ -240,6 +302,14 @@ bool decode_jpeg_luma(const uint8_t* data, size_t size, GrayImage& img, std::str
       const int mcux = (W + 8 * hmax - 1) / (8 * hmax), mcuy = (H + 8 * vmax - 1) / (8 * vmax);
       const int lw = mcux * hmax * 8, lh = mcuy * vmax * 8;   // padded luma plane
       std::vector<uint8_t> plane((size_t)lw * lh);
+      const bool chroma = color && comps.size() == 3;
+      std::vector<std::vector<uint8_t>> cplane(comps.size());
+      std::vector<int> cst(comps.size(), 0);
+      if (chroma)
+        for (size_t k = 1; k < comps.size(); ++k) {
+          cst[k] = mcux * comps[k].h * 8;
+          cplane[k].assign((size_t)cst[k] * mcuy * comps[k].v * 8, 0);
+        }
       for (auto& c : comps) {
         c.dc_pred = 0;
         if (!qt_ok[c.tq] || !hdc[c.td].present || !hac[c.ta].present) { err = "missing JPEG table"; return false; }
@@ -274,23 +344,75 @@ bool decode_jpeg_luma(const uint8_t* data, size_t size, GrayImage& img, std::str
                   if (k > 63) { err = "corrupt JPEG data"; return false; }
                   zz[k++] = extend(r.getbits(ss), ss);
                 }
-                if (ci != 0) continue;                 // chroma: entropy-decoded and dropped
+                if (ci != 0 && !chroma) continue;      // grey output: chroma entropy-decoded and dropped
                 for (int k = 0; k < 64; ++k) coef[kZigzag[k]] = zz[k] * (int)qt[c.tq][kZigzag[k]];
-                const int ox = (mx * hmax + bx) * 8, oy = (my * vmax + by) * 8;
-                idct_islow(coef, plane.data() + (size_t)oy * lw + ox, lw);
+                const int ox = (mx * c.h + bx) * 8, oy = (my * c.v + by) * 8;
+                if (ci == 0) idct_islow(coef, plane.data() + (size_t)oy * lw + ox, lw);
+                else idct_islow(coef, cplane[ci].data() + (size_t)oy * cst[ci] + ox, cst[ci]);
               }
             }
           }
           if (restart) mcus_left--;
         }
       }
-      img.w = W; img.h = H;
-      img.px.resize((size_t)W * H);
-      for (int y = 0; y < H; ++y) std::memcpy(img.px.data() + (size_t)y * W, plane.data() + (size_t)y * lw, W);
+      if (!color) {
+        gray->w = W; gray->h = H;
+        gray->px.resize((size_t)W * H);
+        for (int y = 0; y < H; ++y) std::memcpy(gray->px.data() + (size_t)y * W, plane.data() + (size_t)y * lw, W);
+        return true;
+      }
+      bgr->w = W; bgr->h = H;
+      bgr->bgr.resize((size_t)W * H * 3);
+      if (!chroma) {                                   // grey file: B = G = R = Y
+        for (int y = 0; y < H; ++y)
+          for (int x = 0; x < W; ++x) {
+            const uint8_t v = plane[(size_t)y * lw + x];
+            uint8_t* o = bgr->bgr.data() + 3 * ((size_t)y * W + x);
+            o[0] = o[1] = o[2] = v;
+          }
+        return true;
+      }
+      std::vector<uint8_t> cb, cr;
+      for (int k = 1; k <= 2; ++k) {
+        const Comp& c = comps[k];
+        if (hmax % c.h || vmax % c.v) { err = "unsupported chroma sampling"; return false; }
+        const int dw = (W * c.h + hmax - 1) / hmax, dh = (H * c.v + vmax - 1) / vmax;
+        upsample_plane(cplane[k], cst[k], dw, dh, hmax / c.h, vmax / c.v, W, H, k == 1 ? cb : cr);
+      }
+      // jdcolor.c build_ycc_rgb_table / ycc_rgb_convert (SCALEBITS 16)
+      constexpr int SB = 16;
+      constexpr int64_t HALF = (int64_t)1 << (SB - 1);
+      auto FIX = [](double x) { return (int64_t)(x * (1L << SB) + 0.5); };
+      int cr_r[256], cb_b[256];
+      int64_t cr_g[256], cb_g[256];
+      for (int i = 0; i < 256; ++i) {
+        const int64_t x = i - 128;
+        cr_r[i] = (int)((FIX(1.40200) * x + HALF) >> SB);
+        cb_b[i] = (int)((FIX(1.77200) * x + HALF) >> SB);
+        cr_g[i] = -FIX(0.71414) * x;
+        cb_g[i] = -FIX(0.34414) * x + HALF;
+      }
+      auto lim = [](int v) { return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v)); };
+      for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x) {
+          const size_t i = (size_t)y * W + x;
+          const int Y = plane[(size_t)y * lw + x], b = cb[i], r = cr[i];
+          uint8_t* o = bgr->bgr.data() + 3 * i;
+          o[2] = lim(Y + cr_r[r]);
+          o[1] = lim(Y + (int)((cb_g[b] + cr_g[r]) >> SB));
+          o[0] = lim(Y + cb_b[b]);
+        }
       return true;
     }
     r.pos = end;
   }
+}
+
+bool decode_jpeg_luma(const uint8_t* data, size_t size, GrayImage& img, std::string& err) {
+  return decode_jpeg(data, size, false, &img, nullptr, err);
+}
+bool decode_jpeg_bgr(const uint8_t* data, size_t size, ColorImage& img, std::string& err) {
+  return decode_jpeg(data, size, true, nullptr, &img, err);
 }
 
 }  // namespace dpe_host

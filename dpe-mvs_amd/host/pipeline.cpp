@@ -14,8 +14,11 @@
 //
 // GetProblemEdges (main.cpp:331-388) runs before the first pass as in the reference: edges_<s>.dmb /
 // labels_<s>.dmb that are missing are computed by EdgeSegment (edges.cpp) and written.
-// Not part of this build: RunFusion (fusion=true fails), the viz medium results
-// (ignored).
+// fusion = true runs RunFusion (fusion.cpp) on rank 0 after the outputs: the per-(pixel, view)
+// projection tests on the GPU (dpe_fusion_candidates), the order-dependent rest on the host; with
+// several ranks the final normals and pixel states are all-gathered first.  As in the reference the
+// edges_/labels_ maps are deleted at the end unless keep_intermediate.  Not part of this build: the
+// viz medium results (ignored).
 #include "host.h"
 
 #include <cmath>
@@ -177,6 +180,23 @@ int native_runner(void* user, const DpePassInput* in, const DpePassState* st) {
   return dpe_pm_run(static_cast<DpeContext*>(user), in, st);
 }
 
+struct NativeFusion {
+  DpeContext* ctx = nullptr;
+  bool own = false;
+  const DpeFusionView* staged = nullptr;
+  ~NativeFusion() { if (own && ctx) dpe_destroy(ctx); }
+};
+int native_fusion(void* user, const DpeFusionView* views, int n, int ref, const int* src, int ns, int32_t* idx,
+                  float* val) {
+  NativeFusion* f = static_cast<NativeFusion*>(user);
+  if (f->staged != views) {
+    const int r = dpe_fusion_stage(f->ctx, views, n);
+    if (r != DPE_OK) return r;
+    f->staged = views;
+  }
+  return dpe_fusion_candidates(f->ctx, ref, src, ns, idx, val);
+}
+
 // InuputInitialization + SupportInitialization (DPE.cpp:733-914, 1025-1052), the pass, the epilogue
 bool process_problem(Problem& p, ImageCache& cache, std::map<int, ImageState>& states,
                      const std::map<int, DepthMap>& depth_src, const DpePipelineOptions& opt, Runner& run,
@@ -327,7 +347,6 @@ bool write_outputs(const Problem& p, const ImageState& s, const DpePipelineOptio
 int run(const char* dense_folder, const DpePipelineOptions& opt) {
   std::string& err = g_err;
   err.clear();
-  if (opt.fusion) { err = "fusion=true: RunFusion (DPE.cpp:1220-1370) is not part of this build (SURVEY.md §8f)"; return 1; }
   const int world = std::max(1, opt.world_size), rank = opt.rank;
   if (world > 1 && !opt.allgather) { err = "world_size > 1 needs an all-gather"; return 1; }
   if (rank < 0 || rank >= world) { err = "bad rank"; return 1; }
@@ -428,6 +447,103 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
     const Problem& p = problems[pi];
     if (!write_outputs(p, states[p.ref_image_id], opt, err)) return 1;
   }
+  if (opt.fusion) {   // RunFusion (main.cpp:578-580)
+    std::map<int, ImageState> all;
+    for (int pi : blocks[rank]) all[problems[pi].ref_image_id] = states[problems[pi].ref_image_id];
+    if (world > 1) {   // the final normals and pixel states of every image (depths are in depth_cur)
+      const ImageState& s0 = states[problems[blocks[rank][0]].ref_image_id];
+      const size_t per = (size_t)s0.w * s0.h;
+      size_t nmax = 0;
+      for (auto& b : blocks) nmax = std::max(nmax, b.size());
+      std::vector<float> send(nmax * per * 4, 0.0f), recv(send.size() * world);
+      for (size_t k = 0; k < blocks[rank].size(); ++k) {
+        const ImageState& st = states[problems[blocks[rank][k]].ref_image_id];
+        float* o = send.data() + k * per * 4;
+        std::memcpy(o, st.normal.data(), per * 12);
+        for (size_t i = 0; i < per; ++i) o[3 * per + i] = (float)st.weak[i];
+      }
+      if (opt.allgather(opt.allgather_user, send.data(), send.size(), recv.data()) != 0) { err = "all-gather failed"; return 1; }
+      for (int r = 0; r < world; ++r)
+        for (size_t k = 0; k < blocks[r].size(); ++k) {
+          const int id = problems[blocks[r][k]].ref_image_id;
+          if (all.count(id)) continue;
+          const float* src = recv.data() + ((size_t)r * nmax + k) * per * 4;
+          ImageState st;
+          st.w = s0.w; st.h = s0.h;
+          st.depth = depth_cur[id].d;
+          st.normal.assign(src, src + 3 * per);
+          st.weak.resize(per);
+          for (size_t i = 0; i < per; ++i) st.weak[i] = (uint8_t)src[3 * per + i];
+          all[id] = std::move(st);
+        }
+    }
+    if (rank == 0) {
+      std::vector<FusionView> views(problems.size());
+      const bool use_block = fs::exists(fs::path(dense) / "blocks");
+      for (size_t i = 0; i < problems.size(); ++i) {
+        const Problem& p = problems[i];
+        FusionView& v = views[i];
+        const ImageState& st = all.at(p.ref_image_id);
+        v.image_id = p.ref_image_id;
+        v.src_ids = p.src_image_ids;
+        DpeCamera cam;
+        if (!read_camera((fs::path(dense) / "cams" / (fmt_index(p.ref_image_id) + "_cam.txt")).string(), cam, err)) return 1;
+        ColorImage img;
+        if (!read_bgr((fs::path(dense) / "images" / (fmt_index(p.ref_image_id) + ".jpg")).string(), img, err)) return 1;
+        if (img.w != st.w || img.h != st.h) {   // RescaleImageAndCamera (DPE.cpp:1123-1144), per channel
+          const float sx = st.w / (float)img.w, sy = st.h / (float)img.h;
+          std::vector<uint8_t> ch((size_t)img.w * img.h), och((size_t)st.w * st.h);
+          v.bgr.assign((size_t)st.w * st.h * 3, 0);
+          for (int k = 0; k < 3; ++k) {
+            for (size_t q = 0; q < ch.size(); ++q) ch[q] = img.bgr[3 * q + k];
+            resize_u8(ch.data(), img.w, img.h, och.data(), st.w, st.h);
+            for (size_t q = 0; q < och.size(); ++q) v.bgr[3 * q + k] = och[q];
+          }
+          cam.K[0] *= sx; cam.K[2] *= sx; cam.K[4] *= sy; cam.K[5] *= sy;
+        } else {
+          v.bgr = std::move(img.bgr);
+        }
+        cam.width = st.w; cam.height = st.h;
+        if (use_block) {
+          GrayImage b;
+          if (!read_gray((fs::path(dense) / "blocks" / ("mask_" + std::to_string(p.ref_image_id) + ".jpg")).string(), b, err)) return 1;
+          if (b.w != st.w || b.h != st.h) { err = "block mask size differs from the depth map"; return 1; }
+          v.block = std::move(b.px);
+        }
+        v.view.width = st.w; v.view.height = st.h;
+        v.view.cam = cam;
+        v.view.depth = st.depth.data();
+        v.view.normal = st.normal.data();
+        v.weak = st.weak.data();
+      }
+      NativeFusion nf;
+      dpe_fusion_fn ffn = opt.fusion_runner;
+      void* fuser = opt.fusion_user;
+      if (!ffn) {
+        nf.ctx = runner.ctx;
+        if (!nf.ctx) {
+          nf.ctx = dpe_create(opt.gpu_index);
+          if (!nf.ctx) { err = std::string("dpe_create: ") + dpe_last_error(); return 1; }
+          nf.own = true;
+        }
+        ffn = native_fusion; fuser = &nf;
+      }
+      std::vector<FusedPoint> cloud;
+      if (!run_fusion(views, ffn, fuser, cloud, err)) {
+        if (!opt.fusion_runner) err += std::string(": ") + dpe_last_error();
+        return 1;
+      }
+      if (!export_point_cloud((fs::path(dense) / kOutName / "DPE.ply").string(), cloud, err)) return 1;
+      if (opt.verbose) std::printf("Fused %zu points\n", cloud.size());
+    }
+  }
+  if (!opt.keep_intermediate)   // the reference's clean-up (main.cpp:581-595)
+    for (int pi : blocks[rank])
+      for (int j = 0; j < round_num; j++) {
+        std::error_code ec2;
+        fs::remove(fs::path(problems[pi].result_folder) / ("edges_" + std::to_string(j) + ".dmb"), ec2);
+        fs::remove(fs::path(problems[pi].result_folder) / ("labels_" + std::to_string(j) + ".dmb"), ec2);
+      }
   if (opt.verbose && rank == 0) std::printf("All done\n");
   return 0;
 }

@@ -16,6 +16,9 @@
  *   cv::Canny(L2, aperture 3) DPE.cpp:226        dpe_host_canny
  *   cv::resize INTER_LINEAR 8U DPE.cpp:145,230   dpe_host_resize_u8
  *   Connect                   DPE.cpp:27-127     dpe_host_connect
+ *   RunFusion / ExportPointCloud DPE.cpp:1220,532 inside dpe_run_pipeline (fusion = true): projection
+ *                                                tests on the GPU (dpe_fusion_candidates), serial rest
+ *   cv::imread(IMREAD_COLOR)  DPE.cpp:1253       dpe_host_read_bgr
  *   cv::HoughLinesP           DPE.cpp:186        dpe_host_hough_lines_p
  *
  * Additions for the one-process-per-GPU deployment: a pass runner hook (default: the HIP library
@@ -42,6 +45,11 @@ typedef int (*dpe_pass_runner_fn)(void* user, const DpePassInput* in, const DpeP
 /* All-gather of `count` floats per rank into recv[world * count], rank-major.  0 = success. */
 typedef int (*dpe_allgather_fn)(void* user, const float* send, size_t count, float* recv);
 
+/* Fusion projection tests of one reference view: same contract as dpe_fusion_candidates
+ * (include/dpe_mvs.h) over the given views (the default runs the HIP kernel on gpu_index). */
+typedef int (*dpe_fusion_fn)(void* user, const DpeFusionView* views, int n_views, int ref, const int* src, int ns,
+                             int32_t* idx, float* val);
+
 enum { DPE_SCHEDULE_REFERENCE = 0, DPE_SCHEDULE_JACOBI = 1 };
 
 typedef struct DpePipelineOptions {
@@ -53,7 +61,9 @@ typedef struct DpePipelineOptions {
   dpe_allgather_fn allgather; void* allgather_user;   /* required when world_size > 1 */
   dpe_pass_runner_fn runner; void* runner_user;       /* NULL: libdpe_mvs on gpu_index */
   uint64_t base_seed;       /* Philox key of image i: base_seed ^ (i * 0x9E3779B97F4A7C15) */
-  bool keep_intermediate;   /* also write depths.dmb / normals.dmb / weak.bin / selected_views.bin */
+  bool keep_intermediate;   /* also write depths.dmb / normals.dmb / weak.bin / selected_views.bin and
+                               keep edges_<s>.dmb / labels_<s>.dmb (the reference deletes them) */
+  dpe_fusion_fn fusion_runner; void* fusion_user;     /* NULL: the HIP kernel on gpu_index */
 } DpePipelineOptions;
 
 void dpe_pipeline_default_options(DpePipelineOptions* opt);
@@ -64,6 +74,8 @@ const char* dpe_pipeline_last_error(void);
 /* Grey-level decode of a JPEG (baseline/extended, luma plane) or binary PGM.  Writes up to `cap`
  * bytes into `out` (pass NULL/0 to query the size) and the size into *w, *h.  0 on success. */
 int dpe_host_read_gray(const char* path, uint8_t* out, size_t cap, int* w, int* h);
+/* Colour decode (cv::imread IMREAD_COLOR): 8-bit BGR, up to `cap` bytes; size query with out = NULL. */
+int dpe_host_read_bgr(const char* path, uint8_t* out, size_t cap, int* w, int* h);
 /* ReadCamera (DPE.cpp:341-382): extrinsic, intrinsic, "dmin interval num dmax" line.  0 on success. */
 int dpe_host_read_camera(const char* path, DpeCamera* cam);
 /* cv::resize INTER_LINEAR of a CV_32FC1 image (float weights, horizontal then vertical pass). */

@@ -192,6 +192,30 @@ int dpe_pm_last_timings(DpeContext* ctx, float* ms, int n);
 void dpe_set_counting(DpeContext* ctx, int enable);
 int dpe_pm_last_counts(DpeContext* ctx, unsigned long long* out, int n);
 
+/*
+ * RunFusion (DPE.cpp:1220-1370): the per-(pixel, source view) projection tests on the GPU.  The
+ * order-dependent rest (the masks of already fused pixels, the angle test, the consistency weights,
+ * colours) stays with the caller, in the reference's serial order (the host pipeline's fusion).
+ */
+typedef struct DpeFusionView {
+  int width, height;
+  DpeCamera cam;              /* ReadCamera, scaled to the map size (RescaleImageAndCamera, DPE.cpp:1123) */
+  const float* depth;         /* f32 [H][W] final depth (depths.dmb; <= 0: no depth) */
+  const float* normal;        /* f32 [H][W][3] final world normals (normals.dmb) */
+} DpeFusionView;
+
+/* Uploads every view's depth and normal map (H2D); they stay resident for dpe_fusion_candidates. */
+int dpe_fusion_stage(DpeContext* ctx, const DpeFusionView* views, int n_views);
+
+/* For reference view `ref` and its source views src[0..ns-1] (indices into the staged views),
+ * pixel p (row-major) and source j (DPE.cpp:1303-1343 without the masks):
+ *   idx[p*ns + j] = row-major source pixel int(y+.5)*W + int(x+.5) of the projection when it lies
+ *                   inside the source view on a depth > 0 with reprojection error < 2 and relative
+ *                   depth difference < 0.01; else -1;
+ *   val[(p*ns + j)*3 + k] = (reprojection error, relative depth difference, n_ref . n_src).
+ * HOST output buffers of W*H*ns int32 / W*H*ns*3 floats.  Synchronous. */
+int dpe_fusion_candidates(DpeContext* ctx, int ref, const int* src, int ns, int32_t* idx, float* val);
+
 #ifdef __cplusplus
 }
 #endif

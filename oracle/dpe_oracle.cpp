@@ -36,6 +36,8 @@
 #include "../include/dpe_mvs.h"
 
 #include <algorithm>
+#include <cmath>
+#include <cstring>
 #include <atomic>
 #include <cfloat>
 #include <cstdio>
@@ -1765,6 +1767,173 @@ float oracle_sample(const float* img, int W, int H, float sx, float sy) {
 // pipeline with the oracle in place of the GPU; `user` points to the thread count (int).
 int oracle_pass_runner(void* user, const DpePassInput* in, const DpePassState* st) {
   return oracle_pm_run(in, st, user ? *static_cast<int*>(user) : 1);
+}
+
+// ---- RunFusion (DPE.cpp:1220-1370) -----------------------------------------------------------
+// Restated as the reference writes it.  fz_* follow Get3DPointonWorld / ProjectCamera
+// (DPE.cpp:1170-1206) and GetAngle (:1208-1217) in single precision, expression order kept.
+namespace {
+struct FzP { float x, y, z; };
+FzP fz_world(int x, int y, float depth, const DpeCamera& cam) {
+  FzP p, t, C;
+  p.x = depth * (x - cam.K[2]) / cam.K[0];
+  p.y = depth * (y - cam.K[5]) / cam.K[4];
+  p.z = depth;
+  t.x = cam.R[0] * p.x + cam.R[3] * p.y + cam.R[6] * p.z;
+  t.y = cam.R[1] * p.x + cam.R[4] * p.y + cam.R[7] * p.z;
+  t.z = cam.R[2] * p.x + cam.R[5] * p.y + cam.R[8] * p.z;
+  C.x = -(cam.R[0] * cam.t[0] + cam.R[3] * cam.t[1] + cam.R[6] * cam.t[2]);
+  C.y = -(cam.R[1] * cam.t[0] + cam.R[4] * cam.t[1] + cam.R[7] * cam.t[2]);
+  C.z = -(cam.R[2] * cam.t[0] + cam.R[5] * cam.t[1] + cam.R[8] * cam.t[2]);
+  return FzP{t.x + C.x, t.y + C.y, t.z + C.z};
+}
+void fz_project(const FzP& X, const DpeCamera& cam, float& px, float& py, float& depth) {
+  const float tx = cam.R[0] * X.x + cam.R[1] * X.y + cam.R[2] * X.z + cam.t[0];
+  const float ty = cam.R[3] * X.x + cam.R[4] * X.y + cam.R[5] * X.z + cam.t[1];
+  const float tz = cam.R[6] * X.x + cam.R[7] * X.y + cam.R[8] * X.z + cam.t[2];
+  depth = cam.K[6] * tx + cam.K[7] * ty + cam.K[8] * tz;
+  px = (cam.K[0] * tx + cam.K[1] * ty + cam.K[2] * tz) / depth;
+  py = (cam.K[3] * tx + cam.K[4] * ty + cam.K[5] * tz) / depth;
+}
+// int(v + 0.5f) inside [0, size): on the reference's x86 host an out-of-range / NaN conversion gives
+// INT_MIN, i.e. outside; the float test below is that rule without the undefined conversion.
+bool fz_pixel(float v, int size, int& out) {
+  const float f = v + 0.5f;
+  if (!(f > -1.0f && f < (float)size)) return false;
+  out = (int)f;
+  return true;
+}
+}  // namespace
+
+// One view as RunFusion sees it (test-infrastructure struct, mirrored in oracle/oracle.py).
+typedef struct OracleFusionView {
+  int width, height;
+  DpeCamera cam;
+  const float* depth;      // [H][W]
+  const float* normal;     // [H][W][3]
+  const uint8_t* weak;     // [H][W] PixelState
+  const uint8_t* bgr;      // [H][W][3]
+  const uint8_t* block;    // [H][W] or NULL
+  int image_id;
+  int ns;
+  const int* src_ids;      // pair.txt order
+} OracleFusionView;
+
+// RunFusion's serial loop (DPE.cpp:1286-1367) over `views` in problem order; writes up to `cap`
+// points as (x, y, z, b, g, r) floats into `out` and returns the point count.
+int oracle_run_fusion(const OracleFusionView* views, int n, float* out, int cap) {
+  std::vector<std::vector<uint8_t>> masks(n);
+  for (int i = 0; i < n; ++i) masks[i].assign((size_t)views[i].width * views[i].height, 0);
+  auto idx_of = [&](int id) { for (int k = 0; k < n; ++k) if (views[k].image_id == id) return k; return 0; };
+  int count = 0;
+  for (int i = 0; i < n; ++i) {
+    const int ref = idx_of(views[i].image_id);
+    const OracleFusionView& R = views[ref];
+    const int num_ngb = views[i].ns;
+    std::vector<int> ux(num_ngb), uy(num_ngb);
+    for (int r = 0; r < R.height; ++r)
+      for (int c = 0; c < R.width; ++c) {
+        const size_t rc = (size_t)r * R.width + c;
+        if (R.block && R.block[rc] < 128) continue;
+        if (masks[ref][rc] == 1) continue;
+        const float ref_depth = R.depth[rc];
+        if (ref_depth <= 0.0) continue;
+        const float* rn = R.normal + 3 * rc;
+        const FzP X = fz_world(c, r, ref_depth, R.cam);
+        int num_consistent = 0;
+        float dyn = 0.0f;
+        for (int j = 0; j < num_ngb; ++j) {
+          ux[j] = uy[j] = -1;
+          const int s = idx_of(views[i].src_ids[j]);
+          const OracleFusionView& S = views[s];
+          float px, py, pd;
+          fz_project(X, S.cam, px, py, pd);
+          int src_r, src_c;
+          if (!fz_pixel(py, S.height, src_r) || !fz_pixel(px, S.width, src_c)) continue;
+          const size_t sc = (size_t)src_r * S.width + src_c;
+          if (masks[s][sc] == 1) continue;
+          const float src_depth = S.depth[sc];
+          if (src_depth <= 0.0) continue;
+          const FzP Y = fz_world(src_c, src_r, src_depth, S.cam);
+          float tx, ty;
+          fz_project(Y, R.cam, tx, ty, pd);
+          const float dx = c - tx, dy = r - ty;
+          const float reproj_error = std::sqrt(dx * dx + dy * dy);
+          const float rel = std::fabs(pd - ref_depth) / ref_depth;
+          const float* sn = S.normal + 3 * sc;
+          const float dot = rn[0] * sn[0] + rn[1] * sn[1] + rn[2] * sn[2];
+          float angle = std::acos(dot);
+          if (angle != angle) angle = 0.0f;
+          if (reproj_error < 2.0f && rel < 0.01f && angle < 0.174533f) {
+            ux[j] = src_c; uy[j] = src_r;
+            const float tmp_index = reproj_error + 200 * rel + angle * 10;
+            dyn += std::exp(-tmp_index);
+            num_consistent++;
+          }
+        }
+        const float factor = R.weak[rc] == DPE_WEAK ? 0.45f : 0.3f;
+        if (num_consistent >= 1 && dyn > factor * num_consistent) {
+          float col[3] = {(float)R.bgr[3 * rc], (float)R.bgr[3 * rc + 1], (float)R.bgr[3 * rc + 2]};
+          for (int j = 0; j < num_ngb; ++j) {
+            if (ux[j] == -1) continue;
+            const int s = idx_of(views[i].src_ids[j]);
+            const size_t sc = (size_t)uy[j] * views[s].width + ux[j];
+            masks[s][sc] = 1;
+            col[0] += views[s].bgr[3 * sc]; col[1] += views[s].bgr[3 * sc + 1]; col[2] += views[s].bgr[3 * sc + 2];
+          }
+          for (float& v : col) v /= (num_consistent + 1);
+          if (count < cap && out) {
+            float* o = out + 6 * (size_t)count;
+            o[0] = X.x; o[1] = X.y; o[2] = X.z; o[3] = col[0]; o[4] = col[1]; o[5] = col[2];
+          }
+          count++;
+        }
+      }
+  }
+  return count;
+}
+
+// dpe_fusion_fn (include/dpe_host.h) on the CPU: the per-(pixel, view) tests of RunFusion with the
+// contract of dpe_fusion_candidates (include/dpe_mvs.h).  Checker of the HIP kernel.
+int oracle_fusion_candidates(void* /*user*/, const DpeFusionView* views, int n, int ref, const int* src, int ns,
+                             int32_t* idx, float* val) {
+  if (!views || ref < 0 || ref >= n) return DPE_ERR_ARG;
+  const DpeFusionView& R = views[ref];
+  for (int r = 0; r < R.height; ++r)
+    for (int c = 0; c < R.width; ++c) {
+      const size_t p = (size_t)r * R.width + c;
+      for (int j = 0; j < ns; ++j) {
+        idx[p * ns + j] = -1;
+        val[(p * ns + j) * 3] = val[(p * ns + j) * 3 + 1] = val[(p * ns + j) * 3 + 2] = 0.0f;
+      }
+      const float ref_depth = R.depth[p];
+      if (!(ref_depth > 0.0f)) continue;
+      const FzP X = fz_world(c, r, ref_depth, R.cam);
+      const float* rn = R.normal + 3 * p;
+      for (int j = 0; j < ns; ++j) {
+        const DpeFusionView& S = views[src[j]];
+        float px, py, pd;
+        fz_project(X, S.cam, px, py, pd);
+        int src_r, src_c;
+        if (!fz_pixel(px, S.width, src_c) || !fz_pixel(py, S.height, src_r)) continue;
+        const size_t sp = (size_t)src_r * S.width + src_c;
+        const float sd = S.depth[sp];
+        if (!(sd > 0.0f)) continue;
+        const FzP Y = fz_world(src_c, src_r, sd, S.cam);
+        float tx, ty, pd2;
+        fz_project(Y, R.cam, tx, ty, pd2);
+        const float dx = c - tx, dy = r - ty;
+        const float re = std::sqrt(dx * dx + dy * dy);
+        const float rl = std::fabs(pd2 - ref_depth) / ref_depth;
+        if (re < 2.0f && rl < 0.01f) {
+          idx[p * ns + j] = (int32_t)sp;
+          const float* sn = S.normal + 3 * sp;
+          float* v = val + (p * ns + j) * 3;
+          v[0] = re; v[1] = rl; v[2] = rn[0] * sn[0] + rn[1] * sn[1] + rn[2] * sn[2];
+        }
+      }
+    }
+  return DPE_OK;
 }
 
 }  // extern "C"

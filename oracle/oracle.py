@@ -90,3 +90,40 @@ def philox(ctr, key) -> list:
 def sample(img: np.ndarray, sx: float, sy: float) -> float:
     im = np.ascontiguousarray(img, np.float32)
     return float(lib().oracle_sample(im.ctypes.data_as(C.POINTER(C.c_float)), im.shape[1], im.shape[0], sx, sy))
+
+
+# ------------------------------------------------------------------------------ RunFusion
+class OracleFusionView(C.Structure):
+    _fields_ = [("width", C.c_int), ("height", C.c_int), ("cam", _abi.DpeCamera),
+                ("depth", C.c_void_p), ("normal", C.c_void_p), ("weak", C.c_void_p), ("bgr", C.c_void_p),
+                ("block", C.c_void_p), ("image_id", C.c_int), ("ns", C.c_int), ("src_ids", C.c_void_p)]
+
+
+def fusion_runner():
+    """(function pointer, user) of oracle_fusion_candidates: a dpe_fusion_fn for the host pipeline."""
+    return (C.cast(lib().oracle_fusion_candidates, C.c_void_p), None)
+
+
+def run_fusion(views: list) -> np.ndarray:
+    """RunFusion's serial loop (DPE.cpp:1286-1367) over views = [dict(image_id, src_ids, cam, depth [H,W],
+    normal [H,W,3], weak [H,W] u8, bgr [H,W,3] u8, block or None)] in problem order -> float32 [n, 6]
+    points (x, y, z, b, g, r)."""
+    keep, arr = [], (OracleFusionView * len(views))()
+    for k, v in enumerate(views):
+        d = np.ascontiguousarray(v["depth"], np.float32)
+        n = np.ascontiguousarray(v["normal"], np.float32)
+        w = np.ascontiguousarray(v["weak"], np.uint8)
+        b = np.ascontiguousarray(v["bgr"], np.uint8)
+        s = np.ascontiguousarray(v["src_ids"], np.int32)
+        bl = None if v.get("block") is None else np.ascontiguousarray(v["block"], np.uint8)
+        keep += [d, n, w, b, s, bl]
+        arr[k] = OracleFusionView(d.shape[1], d.shape[0], v["cam"], d.ctypes.data, n.ctypes.data, w.ctypes.data,
+                                  b.ctypes.data, bl.ctypes.data if bl is not None else None, int(v["image_id"]),
+                                  len(s), s.ctypes.data)
+    L = lib()
+    L.oracle_run_fusion.argtypes = [C.POINTER(OracleFusionView), C.c_int, C.c_void_p, C.c_int]
+    L.oracle_run_fusion.restype = C.c_int
+    cnt = L.oracle_run_fusion(arr, len(views), None, 0)
+    out = np.zeros((max(cnt, 1), 6), np.float32)
+    L.oracle_run_fusion(arr, len(views), out.ctypes.data, cnt)
+    return out[:cnt]
