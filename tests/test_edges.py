@@ -218,7 +218,7 @@ def test_pipeline_generates_missing_edges_and_labels(tmp_path):
     import oracle
     threads = C.c_int(4)
     runner = (C.cast(oracle.lib().oracle_pass_runner, C.c_void_p), C.addressof(threads))
-    assert pipeline.run_dpe_pipeline(d, runner=runner, verbose=False) == 0
+    assert pipeline.run_dpe_pipeline(d, runner=runner, verbose=False, keep_intermediate=True) == 0
     img = pipeline.read_gray(os.path.join(d, "images", "00000000.jpg"))
     rf = os.path.join(d, "DPE", "00000000")
     e0 = pipeline.read_bin_mat(os.path.join(rf, "edges_0.dmb"))

@@ -159,9 +159,6 @@ def test_missing_edge_map_is_regenerated(tmp_path, dense4):
     assert np.array_equal(e, pipeline.edge_segment(1, np.rint(half).astype(np.uint8), 0, True, True))
 
 
-def test_fusion_not_built(dense4):
-    with pytest.raises(pipeline.PipelineError, match="RunFusion"):
-        pipeline.run_dpe_pipeline(dense4, runner=oracle_runner(), fusion=True, verbose=False)
 
 
 def test_pipeline_end_to_end(tmp_path, dense4):
