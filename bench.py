@@ -124,6 +124,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-instrument", action="store_true", help="skip the hipEvent / work-counter runs (PMC profiling)")
+    ap.add_argument("--no-pass-types", action="store_true", help="skip the FIRST_INIT / REFINE_INIT passes (kernel traces)")
     ap.add_argument("--width", type=int, default=W_)
     ap.add_argument("--height", type=int, default=H_)
     args = ap.parse_args()
@@ -206,7 +207,7 @@ def main():
 
     # the other pass types of the schedule at the same size (reported per pass type)
     per_type = {"refine_iter": round(value / world, 4)}
-    for kind in ("first_init", "refine_init"):
+    for kind in (() if args.no_pass_types else ("first_init", "refine_init")):
         pk = workload_params(_abi, NV_)
         if kind == "first_init":
             pk.state = _abi.FIRST_INIT; pk.use_APD = False; pk.use_edge = False; pk.geom_consistency = False
