@@ -74,10 +74,11 @@ def pmc_traffic(cls: str):
 
 def cpu_baseline(abi, synthetic, seconds_hint: float = 20.0) -> dict:
     """Scalar C++ restatement (oracle/) timed on this host's cores on a bounded sample of the same
-    workload: the same pass (9 source views, same parameters) on a 160x120 instance of the scene."""
+    workload: the same pass (9 source views, same parameters) on a 640x480 instance of the scene
+    (about 10 s on 16 host threads)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # checker / baseline only
-    w, h = 320, 240
+    w, h = 640, 480
     sc = synthetic.make_scene(w, h, NV_, low_scale=2)
     p = workload_params(abi, NV_)
     inp = synthetic.pass_input(sc, p, depths=synthetic.src_depths(sc))
