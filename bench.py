@@ -97,6 +97,28 @@ def cpu_baseline(abi, synthetic, seconds_hint: float = 20.0) -> dict:
     return base, (inp, st, ref, f"{w}x{h}")
 
 
+def end_to_end(local_rank: int, n_images: int, W: int, H: int, scene=None) -> dict:
+    """SURVEY.md §8d end-to-end rate: n_images * W * H / wall time of DPE_MVS.dpe_mvs() on a synthetic
+    dense_folder (JPEG images, cams, pair.txt; no edge/label maps, so EdgeSegment runs as in the
+    reference): decode, pyramid, EdgeSegment, the whole coarse-to-fine schedule (8 passes per image),
+    the .npy outputs."""
+    import shutil
+    import tempfile
+    from DPE_MVS import synthetic, dpe_mvs
+    d = tempfile.mkdtemp(prefix="dpe_e2e_")
+    try:
+        synthetic.write_dense_folder(d, W, H, n_images, max_src=min(9, n_images - 1), with_edges=False,
+                                     scene=scene if scene is not None and len(scene["views"]) == n_images else None)
+        t0 = time.perf_counter()
+        dpe_mvs(d, local_rank, False, False, False, True, False, False, False)
+        dt = time.perf_counter() - t0
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+    return {"images": n_images, "width": W, "height": H, "src_views": min(9, n_images - 1), "passes_per_image": 8,
+            "wall_s": round(dt, 3), "mpix_s": round(n_images * W * H / dt / 1e6, 4),
+            "note": "dpe_mvs() wall clock incl. JPEG decode, EdgeSegment, host I/O; value is per-pass HBM-resident"}
+
+
 def parity_on_sample(native, local_rank: int, sample) -> dict:
     """The metric's "L1 vs ref": the HIP pass on the cpu_baseline sample against the oracle's output
     of the same run (depth = plane .w; weak/selected-view maps compared exactly)."""
@@ -126,6 +148,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-instrument", action="store_true", help="skip the hipEvent / work-counter runs (PMC profiling)")
     ap.add_argument("--no-pass-types", action="store_true", help="skip the FIRST_INIT / REFINE_INIT passes (kernel traces)")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end dpe_mvs() run")
+    ap.add_argument("--e2e-images", type=int, default=10)
     ap.add_argument("--width", type=int, default=W_)
     ap.add_argument("--height", type=int, default=H_)
     args = ap.parse_args()
@@ -281,12 +305,17 @@ def main():
         "kernel_ms": {k: round(v, 3) for k, v in tim.items()},
         "work": {k: v for k, v in cnt.items() if v["launches"]},
     }
+    if rank == 0 and world == 1 and not args.no_e2e:
+        ctx.close()
+        ctx = None
+        result["end_to_end"] = end_to_end(local_rank, args.e2e_images, Wd, Hd, scene=sc)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"], sample = cpu_baseline(_abi, synthetic)
         result["parity"] = parity_on_sample(native, local_rank, sample)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    ctx.close()
+    if ctx is not None:
+        ctx.close()
     if dist:
         dist.destroy_process_group()
 

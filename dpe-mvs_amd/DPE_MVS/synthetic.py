@@ -260,14 +260,14 @@ def _labels_edges_at(sid: np.ndarray, w: int, h: int):
 
 
 def write_dense_folder(folder: str, W: int, H: int, n_views: int, seed: int = SCENE_SEED, jpeg_quality: int = 95,
-                       max_src: int = 8) -> dict:
+                       max_src: int = 8, with_edges: bool = True, scene: dict | None = None) -> dict:
     """Writes a complete DPE-MVS dense_folder for a synthetic scene: images/%08d.jpg (8-bit grey),
     cams/%08d_cam.txt (4-number depth line), pair.txt, and per reference image the EdgeSegment
     outputs DPE/%08d/edges_<s>.dmb and labels_<s>.dmb for every pyramid scale of the schedule."""
     import os
     from PIL import Image
     from . import pipeline
-    sc = make_scene(W, H, n_views, seed=seed)
+    sc = scene if scene is not None else make_scene(W, H, n_views, seed=seed)
     os.makedirs(os.path.join(folder, "images"), exist_ok=True)
     os.makedirs(os.path.join(folder, "cams"), exist_ok=True)
     for i, v in enumerate(sc["views"]):
@@ -280,6 +280,8 @@ def write_dense_folder(folder: str, W: int, H: int, n_views: int, seed: int = SC
         for i in range(n_views):
             others = sorted((j for j in range(n_views) if j != i), key=lambda j: (abs(j - i), j))[:max_src]
             f.write(f"{i}\n{len(others)} " + " ".join(f"{j} {100.0 - 5 * abs(i - j):.1f}" for j in others) + "\n")
+    if not with_edges:      # leave the edge / label maps to the pipeline's EdgeSegment
+        return sc
     max_size, rounds = max(W, H), 1
     while max_size > 800:
         max_size //= 2

@@ -21,6 +21,7 @@
 // viz medium results (ignored).
 #include "host.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -29,6 +30,7 @@
 #include <map>
 #include <memory>
 #include <sstream>
+#include <thread>
 
 namespace fs = std::filesystem;
 
@@ -388,19 +390,33 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
     std::printf("There are %d resolution stages for coarse-to-fine processing!\n", round_num);
     std::printf("Iteration nums: %d\n", round_num * 4);
   }
-  for (int pi : blocks[rank]) {   // GetProblemEdges for every scale of the schedule (main.cpp:494-501)
-    const Problem& p = problems[pi];
-    int fw, fh;
-    const std::vector<float>* f = cache.full(p.ref_image_id, fw, fh, err);
-    if (!f) return 1;
-    GrayImage g;
-    g.w = fw; g.h = fh;
-    g.px.resize(f->size());
-    for (size_t k = 0; k < f->size(); ++k) g.px[k] = (uint8_t)(*f)[k];
-    for (int i = 0; i < round_num; ++i)
-      if (!get_problem_edges(g, (int)std::pow(2, round_num - 1 - i), p.result_folder, p.params.use_edge,
-                             p.params.use_label, p.params.high_res_img, err))
-        return 1;
+  {   // GetProblemEdges for every scale of the schedule (main.cpp:494-501); images are independent,
+      // so a pool of host threads takes them round-robin (the decode cache is filled first)
+    std::vector<GrayImage> grey(blocks[rank].size());
+    for (size_t k = 0; k < blocks[rank].size(); ++k) {
+      int fw, fh;
+      const std::vector<float>* f = cache.full(problems[blocks[rank][k]].ref_image_id, fw, fh, err);
+      if (!f) return 1;
+      grey[k].w = fw; grey[k].h = fh;
+      grey[k].px.resize(f->size());
+      for (size_t q = 0; q < f->size(); ++q) grey[k].px[q] = (uint8_t)(*f)[q];
+    }
+    const int nt = (int)std::max<size_t>(1, std::min<size_t>({grey.size(), (size_t)16,
+                                                              (size_t)std::max(1u, std::thread::hardware_concurrency())}));
+    std::vector<std::string> terr(nt);
+    std::vector<std::thread> pool;
+    for (int t = 0; t < nt; ++t)
+      pool.emplace_back([&, t]() {
+        for (size_t k = t; k < grey.size(); k += nt) {
+          const Problem& p = problems[blocks[rank][k]];
+          for (int i = 0; i < round_num && terr[t].empty(); ++i)
+            if (!get_problem_edges(grey[k], (int)std::pow(2, round_num - 1 - i), p.result_folder, p.params.use_edge,
+                                   p.params.use_label, p.params.high_res_img, terr[t]) && terr[t].empty())
+              terr[t] = "EdgeSegment failed";
+        }
+      });
+    for (auto& th : pool) th.join();
+    for (auto& e : terr) if (!e.empty()) { err = e; return 1; }
   }
   for (auto& p : problems) p.params.max_scale_size = std::max(1, (int)std::pow(2, round_num - 1));
   std::map<int, ImageState> states;
