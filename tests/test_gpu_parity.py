@@ -129,3 +129,28 @@ def test_gpu_non_integer_images(ctx):
     st = synthetic.gt_state(sc)
     inp = synthetic.pass_input(sc, p, depths=synthetic.src_depths(sc))
     assert_same(ctx.run(inp, st), oracle.run_pass(inp, st), "f32 images")
+
+
+def test_image_ids_keep_images_resident(ctx):
+    """DpePassInput.image_ids: images uploaded once per (id, size); later passes reuse the HBM copies
+    and give the same bits as uploading every time."""
+    sc = synthetic.make_scene(96, 72, 4)
+    p = _abi.default_params()
+    p.state = _abi.REFINE_ITER
+    p.geom_consistency = True
+    p.rotate_time = 2
+    p.ransac_threshold = 0.00875
+    p.max_scale_size = 2
+    inp = synthetic.pass_input(sc, p, depths=synthetic.src_depths(sc))
+    st = synthetic.gt_state(sc)
+    plain = ctx.run(inp, st)
+    inp_ids = dict(inp, image_ids=[7, 3, 9, 11])
+    first = ctx.run(inp_ids, st)
+    again = ctx.run(inp_ids, st)                                   # all four from the cache
+    for k in ("planes", "weak", "sel", "costs"):
+        assert plain[k].tobytes() == first[k].tobytes() == again[k].tobytes(), k
+    other = synthetic.make_scene(96, 72, 4, seed=synthetic.SCENE_SEED + 5)
+    inp2 = dict(synthetic.pass_input(other, p, depths=synthetic.src_depths(other)), image_ids=[21, 22, 23, 24])
+    ref2 = ctx.run(dict(inp2, image_ids=None), synthetic.gt_state(other))
+    got2 = ctx.run(inp2, synthetic.gt_state(other))
+    assert ref2["planes"].tobytes() == got2["planes"].tobytes()
