@@ -6,6 +6,7 @@ Submodules:
   _abi       ctypes mirror of include/dpe_mvs.h
   pipeline   ctypes side of the C++ host pipeline (lib/libdpe_host.so): multi-rank runs, hooks
   _dpe       pybind11 module of the C++ host pipeline (built by make): dpe_mvs()
+  colmap2mvsnet  COLMAP sparse model -> dense_folder converter (python -m DPE_MVS.colmap2mvsnet)
 """
 from __future__ import annotations
 
