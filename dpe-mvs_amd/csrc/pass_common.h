@@ -252,6 +252,30 @@ DEV bool rcp_range_ok(const Homog& H, float x0, float x1, float y0, float y1) {
          amax < 1.2676506002282294e+30f;
 }
 
+// True when every tap of the rectangle projects to sx <= W - 1 and sy <= H - 1, so the upper clamp
+// of the fixed-point coordinate (fixed_coord) is the identity for all of them.  Call only after
+// rcp_range_ok on the same rectangle (qz of one sign, exact reciprocal).  The corners are computed
+// with the taps' own operations; with qz of one sign the exact projective map of the rectangle lies
+// within its corner values, and the computed taps differ from the exact map by < 1e-3 px for any
+// corner value below W, so the one-pixel margin covers the rounding.  NaN -> false.
+DEV bool patch_inside(const Homog& H, float x0, float x1, float y0, float y1, int W, int Hh) {
+  const float lx = (float)(W - 1), ly = (float)(Hh - 1);
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const float x = i ? x1 : x0;
+    const float bx = __builtin_fmaf(H.h[0], x, H.h[2]), by = __builtin_fmaf(H.h[3], x, H.h[5]);
+    const float bz = __builtin_fmaf(H.h[6], x, H.h[8]);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const float y = j ? y1 : y0;
+      const float iz = d_rcp_fast(__builtin_fmaf(H.h[7], y, bz));
+      ok = ok && (__builtin_fmaf(H.h[1], y, bx) * iz <= lx) && (__builtin_fmaf(H.h[4], y, by) * iz <= ly);   // NaN -> false
+    }
+  }
+  return ok;
+}
+
 // ------------------------------------------------------------------------------ sampling
 DEV float ref_texel(const float* ref, int W, int H, int x, int y) {
   x = x < 0 ? 0 : (x > W - 1 ? W - 1 : x);
@@ -343,26 +367,30 @@ DEV f2v fma2(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
 #ifndef DPE_SAT_CLAMP
 #define DPE_SAT_CLAMP 1
 #endif
+// IN: the caller has proven s <= lim for this tap (patch_inside), so the min is the identity and is
+// skipped (the saturating conversion alone handles the low side).
+template <bool IN = false>
 DEV uint32_t fixed_coord(float s, uint32_t umax) {
 #if DPE_SAT_CLAMP
   const float u = __builtin_fmaf(s, 256.0f, 256.5f);
   uint32_t r;
   asm("v_cvt_u32_f32 %0, %1" : "=v"(r) : "v"(u));
+  if constexpr (IN) return r;
   return min(r, umax);
 #else
   const float lim = (float)((umax - 256u) >> 8);
   return (uint32_t)(int)__builtin_fmaf(__builtin_amdgcn_fmed3f(s, -1.0f, lim), 256.0f, 256.5f);
 #endif
 }
-template <int T>
+template <int T, bool IN = false>
 DEV float tap_u8_fast(const DevBufs& B, uint32_t vofs, uint32_t stride, f2v lim, const float* h, f2v bxy, float bz,
                       float yf) {
   const f2v q = fma2((f2v){h[1], h[4]}, f2s(yf), bxy);
   const float iz = d_rcp_fast(__builtin_fmaf(h[7], yf, bz));
   const f2v sxy = q * f2s(iz);
 #if DPE_SAT_CLAMP
-  const uint32_t ux = fixed_coord(sxy.x, (uint32_t)lim.x * 256u + 256u);
-  const uint32_t uy = fixed_coord(sxy.y, (uint32_t)lim.y * 256u + 256u);
+  const uint32_t ux = fixed_coord<IN>(sxy.x, (uint32_t)lim.x * 256u + 256u);
+  const uint32_t uy = fixed_coord<IN>(sxy.y, (uint32_t)lim.y * 256u + 256u);
 #else
   const float xb = __builtin_amdgcn_fmed3f(sxy.x, -1.0f, lim.x);
   const float yb = __builtin_amdgcn_fmed3f(sxy.y, -1.0f, lim.y);
@@ -391,7 +419,7 @@ DEV float tap_u8_fast(const DevBufs& B, uint32_t vofs, uint32_t stride, f2v lim,
 #ifndef DPE_TAP_PAIR
 #define DPE_TAP_PAIR 1
 #endif
-template <int T>
+template <int T, bool IN = false>
 DEV f2v tap2_fast(const DevBufs& B, uint32_t vofs, uint32_t stride, f2v lim, const float* h, f2v bxy, float bz, f2v yf) {
   const f2v qx = fma2(f2s(h[1]), yf, f2s(bxy.x));
   const f2v qy = fma2(f2s(h[4]), yf, f2s(bxy.y));
@@ -400,8 +428,8 @@ DEV f2v tap2_fast(const DevBufs& B, uint32_t vofs, uint32_t stride, f2v lim, con
   const f2v iz = fma2(fma2(-qz, r, f2s(1.0f)), r, r);
   const f2v sx = qx * iz, sy = qy * iz;
   const uint32_t mx = (uint32_t)lim.x * 256u + 256u, my = (uint32_t)lim.y * 256u + 256u;
-  const uint32_t ux0 = fixed_coord(sx.x, mx), ux1 = fixed_coord(sx.y, mx);
-  const uint32_t uy0 = fixed_coord(sy.x, my), uy1 = fixed_coord(sy.y, my);
+  const uint32_t ux0 = fixed_coord<IN>(sx.x, mx), ux1 = fixed_coord<IN>(sx.y, mx);
+  const uint32_t uy0 = fixed_coord<IN>(sy.x, my), uy1 = fixed_coord<IN>(sy.y, my);
   const uint8_t* base = tex_base<T>(B);
   const uint8_t* p0 = base + (vofs + (__umul24(uy0 >> 8, stride) + (ux0 >> 8)) * tex_bytes<T>());
   const uint8_t* p1 = base + (vofs + (__umul24(uy1 >> 8, stride) + (ux1 >> 8)) * tex_bytes<T>());

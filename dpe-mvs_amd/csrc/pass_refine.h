@@ -62,7 +62,7 @@ DEV void patch_lds_pre(const float* pw, float& p_inv, float& p_mref, float& p_va
   ncc_pre(a_ref, a_rr, a_w, p_inv, p_mref, p_var);
 }
 // Old NCC with the patch read from LDS (same arithmetic as ncc_old_patch36)
-template <int U8, bool FAST>
+template <int U8, bool FAST, bool IN = false>
 DEV void lds_taps(const float* pw, int px, int py, const PassConst& pc, const DevBufs& B, int v, const Homog& H,
                   float* acc) {
   const int W = pc.W, Hh = pc.H;
@@ -91,7 +91,7 @@ DEV void lds_taps(const float* pw, int px, int py, const PassConst& pc, const De
 #if DPE_TAP_PAIR
 #pragma unroll
       for (int b = 0; b < 6; b += 2) {
-        const f2v sp = tap2_fast<U8>(B, vofs, stride, lim, H.h, bxy, bz,
+        const f2v sp = tap2_fast<U8, IN>(B, vofs, stride, lim, H.h, bxy, bz,
                                      (f2v){(float)(py - 5 + 2 * b), (float)(py - 3 + 2 * b)});
         const f2v w0 = wp[a * 6 + b], w1 = wp[a * 6 + b + 1];
         const f2v ws = (f2v){w0.x, w1.x} * sp;
@@ -103,7 +103,7 @@ DEV void lds_taps(const float* pw, int px, int py, const PassConst& pc, const De
 #else
 #pragma unroll
       for (int b = 0; b < 6; ++b) {
-        const float sp = tap_u8_fast<U8>(B, vofs, stride, lim, H.h, bxy, bz, (float)(py - 5 + 2 * b));
+        const float sp = tap_u8_fast<U8, IN>(B, vofs, stride, lim, H.h, bxy, bz, (float)(py - 5 + 2 * b));
         const f2v w = wp[a * 6 + b];
         r_sr = fma2(w, f2s(sp), r_sr);
         const float ws = w.x * sp;
@@ -140,24 +140,34 @@ DEV void lds_taps(const float* pw, int px, int py, const PassConst& pc, const De
     acc[0] = s_src; acc[1] = s_ss; acc[2] = s_rs;
   }
 }
-template <int U8>
+#ifndef DPE_CLAMP_ELIDE
+#define DPE_CLAMP_ELIDE 1
+#endif
+template <int U8, bool ELIDE = false>
 DEV float ncc_old_lds(const float* pw, float s_ref, float s_rr, float s_w, int px, int py, const PassConst& pc,
                       const DevBufs& B, int v, const float4& pl) {
   const Homog H = make_homography(pc, v, pl);
   if (center_outside(pc, v, H, px, py)) { count_work(B, 1, 0); return 2.0f; }
   count_work(B, 1, 36);
   float a[3];
-  if (rcp_range_ok(H, (float)(px - 5), (float)(px + 5), (float)(py - 5), (float)(py + 5)))
-    lds_taps<U8, true>(pw, px, py, pc, B, v, H, a);
-  else
+  if (rcp_range_ok(H, (float)(px - 5), (float)(px + 5), (float)(py - 5), (float)(py + 5))) {
+#if DPE_CLAMP_ELIDE
+    if (ELIDE && patch_inside(H, (float)(px - 5), (float)(px + 5), (float)(py - 5), (float)(py + 5), pc.W, pc.H))
+      lds_taps<U8, true, true>(pw, px, py, pc, B, v, H, a);
+    else
+#endif
+      lds_taps<U8, true>(pw, px, py, pc, B, v, H, a);
+  } else
     lds_taps<U8, false>(pw, px, py, pc, B, v, H, a);
   return ncc_finalize_pre(s_ref, s_rr, s_w, a[0], a[1], a[2]);   // (inv, mref, var_ref) of patch_lds_pre
 }
 
-template <int U8>
+// ELIDE: try the clamp-free tap loop on patches that project inside the image (patch_inside); it
+// pays in DepthToWeak and the weak sweep, not in the strong sweep or LocalRefine (A/B).
+template <int U8, bool ELIDE = false>
 DEV float ncc_old_any(bool fast, const float* pw, float s_ref, float s_rr, float s_w, int px, int py,
                       const PassConst& pc, const DevBufs& B, int v, const float4& pl) {
-  if (fast) return ncc_old_lds<U8>(pw, s_ref, s_rr, s_w, px, py, pc, B, v, pl);
+  if (fast) return ncc_old_lds<U8, ELIDE>(pw, s_ref, s_rr, s_w, px, py, pc, B, v, pl);
   return ncc_old_generic<U8>(pc, B, px, py, v, pl);
 }
 
@@ -231,7 +241,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_depth_to_weak(const Pass
         const int vi = si - 1;
         if (isSet(sel, vi)) {
           float tcst = 0.0f;
-          tcst += ncc_old_any<U8>(fast, pw, s_ref, s_rr, s_w, x, y, pc, B, si, tp);
+          tcst += ncc_old_any<U8, true>(fast, pw, s_ref, s_rr, s_w, x, y, pc, B, si, tp);
           PHASE(1);
           if (pc.P.geom_consistency) tcst += pc.P.geom_factor * geom_cost_at(pc, B, x, y, si, fw);
           PHASE(2);

@@ -636,7 +636,7 @@ struct WeakTab {
 // patch NCC with tabulated weights; the same tap order and arithmetic as patch_ncc_generic.
 // NN > 0: the patch side n is the compile-time NN, so the tap loop unrolls and the gathers of a
 // patch are in flight together (the weak sweep's patches are 3x3 and 4..6 square).
-template <int U8, bool FAST, int NN = 0>
+template <int U8, bool FAST, int NN = 0, bool IN = false>
 DEV void tab_taps(const PassConst& pc, const DevBufs& B, int v, const Homog& H, int cx, int cy, int rad, int inc,
                   int n_rt, const float* __restrict__ tw, float* acc) {
   const int W = pc.W, Hh = pc.H;
@@ -656,7 +656,7 @@ DEV void tab_taps(const PassConst& pc, const DevBufs& B, int v, const Homog& H, 
       float r_ss = 0;
 #pragma unroll
       for (int b = 0; b < (NN > 0 ? NN : n); ++b) {
-        const float sp = tap_u8_fast<U8>(B, vofs, stride, lim, H.h, bxy, bz, (float)(cy - rad + b * inc));
+        const float sp = tap_u8_fast<U8, IN>(B, vofs, stride, lim, H.h, bxy, bz, (float)(cy - rad + b * inc));
         const f2v w = wp[a * n + b];
         r_sr = fma2(w, f2s(sp), r_sr);
         const float ws = w.x * sp;
@@ -1065,7 +1065,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassCons
   if (active) {
     const float4 fin = hyp[5];
     for (int k = c; k < nsel; k += C)
-      hv[k] = ncc_old_any<U8>(fast_old, pw, osum[0], osum[1], osum[2], x, y, pc, B, sel_list[k] + 1, fin);
+      hv[k] = ncc_old_any<U8, true>(fast_old, pw, osum[0], osum[1], osum[2], x, y, pc, B, sel_list[k] + 1, fin);
   }
   wave_sync();
   PHASE(10);
