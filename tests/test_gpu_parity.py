@@ -53,6 +53,15 @@ def _params(kind, iters=3):
     elif kind == "refine_iter_lowres":
         p.state = _abi.REFINE_ITER; p.geom_consistency = True; p.rotate_time = 1; p.ransac_threshold = 0.01
         p.high_res_img = False; p.use_label = True; p.weak_peak_radius = 4
+    elif kind == "acmh_geom":            # ACMH candidate scheme (no APD / edges) with geometric consistency
+        p.state = _abi.REFINE_ITER; p.use_APD = False; p.use_edge = False; p.geom_consistency = True
+        p.rotate_time = 2; p.ransac_threshold = 0.00875
+    elif kind == "no_limit":             # no edge limit, labels or radius map (DPE.cu:2116-2124, 1690-1700)
+        p.state = _abi.REFINE_INIT; p.use_limit = False; p.use_label = False; p.use_radius = False
+        p.rotate_time = 2; p.ransac_threshold = 0.0075
+    elif kind == "weak_generic":         # 5x5 neighbour patches: the untabulated NCC-New path
+        p.state = _abi.REFINE_ITER; p.geom_consistency = True; p.rotate_time = 2; p.ransac_threshold = 0.00875
+        p.weak_radius = 6; p.weak_increment = 3; p.sigma_spatial = 4.0; p.sigma_color = 6.0
     return p
 
 
@@ -64,6 +73,9 @@ CASES = [
     (77, 33, 3, "refine_iter"),          # odd H with (H/2) % 16 == 0: last row outside the red/black grid
     (64, 48, 2, "first"),                # 1 source view
     (72, 54, 5, "refine_iter_lowres"),
+    (80, 60, 4, "acmh_geom"),
+    (88, 66, 4, "no_limit"),
+    (72, 56, 3, "weak_generic"),
 ]
 
 
@@ -71,7 +83,7 @@ CASES = [
 def test_gpu_matches_oracle(ctx, W, H, N, kind):
     sc = synthetic.make_scene(W, H, N)
     p = _params(kind)
-    geom = kind.startswith("refine_iter")
+    geom = p.geom_consistency
     st = synthetic.first_init_state(sc) if kind == "first" else synthetic.gt_state(sc, seed=W + H)
     inp = synthetic.pass_input(sc, p, depths=synthetic.src_depths(sc) if geom else None, seed=W * 7 + N)
     assert_same(ctx.run(inp, st), oracle.run_pass(inp, st), f"{W}x{H}x{N} {kind}")
