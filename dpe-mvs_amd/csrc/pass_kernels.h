@@ -102,6 +102,9 @@ __global__ void k_gen_edge_inform(const PassConst* __restrict__ pcp, DevBufs B) 
 #ifndef DPE_GN_WAVES
 #define DPE_GN_WAVES 1
 #endif
+#ifndef DPE_GN_SPEC
+#define DPE_GN_SPEC 4
+#endif
 __global__ void __launch_bounds__(256, DPE_GN_WAVES) k_gen_neighbours(const PassConst* __restrict__ pcp, DevBufs B,
                                                         const int* __restrict__ list, const int* __restrict__ nlist_p) {   // DPE.cu:2103-2463
   const PassConst& pc = *pcp;
@@ -146,6 +149,54 @@ __global__ void __launch_bounds__(256, DPE_GN_WAVES) k_gen_neighbours(const Pass
         for (int radius = 2; radius <= 4096; radius = MINo(radius * 2, radius + 25)) {
           const float tpx = (float)x + od.x * radius, tpy = (float)y + od.y * radius;
           if (tpx < 0 || tpy < 0 || tpx >= W || tpy >= H) break;
+#if DPE_GN_SPEC > 1
+          // DPE_GN_SPEC attempts at a time: their draws, targets and weak[] / nearest[] loads are all
+          // issued first, then the attempts are tested in order; the stream is put back to just
+          // after the attempt that succeeded, so the draws consumed are the serial loop's.
+          bool found = false;
+          for (int radius_iter = 0; radius_iter < 4 && !found; radius_iter += DPE_GN_SPEC) {
+            short2 cand[DPE_GN_SPEC], nnv[DPE_GN_SPEC];
+            uint8_t wkv[DPE_GN_SPEC];
+            bool inm[DPE_GN_SPEC];
+            uint32_t rb[DPE_GN_SPEC][4], rc[DPE_GN_SPEC];
+            int ri[DPE_GN_SPEC];
+#pragma unroll
+            for (int q = 0; q < DPE_GN_SPEC; ++q) {
+              const uint32_t r1 = rng_u32(rs); const uint32_t r2 = rng_u32(rs);
+              const int rxs = (int)(((r1 % 2 == 0) ? 1u : 0xFFFFFFFFu) * r2 % (uint32_t)shift_range);
+              const uint32_t r3 = rng_u32(rs); const uint32_t r4 = rng_u32(rs);
+              const int rys = (int)(((r3 % 2 == 0) ? 1u : 0xFFFFFFFFu) * r4 % (uint32_t)shift_range);
+              rb[q][0] = rs.b0; rb[q][1] = rs.b1; rb[q][2] = rs.b2; rb[q][3] = rs.b3; rc[q] = rs.ctr; ri[q] = rs.idx;
+              float2 dir = make_float2(od.x * 20 + (float)rxs, od.y * 20 + (float)rys);
+              normalize2(dir);
+              const short2 np = make_short2((short)f2i((float)x + dir.x * radius), (short)f2i((float)y + dir.y * radius));
+              inm[q] = !(np.x < min_margin || np.y < min_margin || np.x >= W - min_margin || np.y >= H - min_margin);
+              const int npc = inm[q] ? np.x + np.y * W : center;
+              wkv[q] = B.weak[npc];
+              nnv[q] = B.nearest[npc];
+              cand[q] = np;
+            }
+#pragma unroll
+            for (int q = 0; q < DPE_GN_SPEC; ++q) {
+              if (found || !inm[q]) continue;
+              short2 np = cand[q];
+              if (wkv[q] != DPE_STRONG) {
+                np = nnv[q];
+                if (np.x == -1 || np.y == -1) continue;
+              }
+              float2 td = make_float2((float)(np.x - x), (float)(np.y - y));
+              normalize2(td);
+              const float ca = td.x * od.x + td.y * od.y;
+              if (ca > threshhold && (!edge_limit || !bresenham(pc, B, x, y, np.x, np.y))) {
+                strong_points[dir_index] = np;
+                dir_valid |= (1ull << dir_index);
+                strong_point_size++;
+                found = true;
+                rs.b0 = rb[q][0]; rs.b1 = rb[q][1]; rs.b2 = rb[q][2]; rs.b3 = rb[q][3]; rs.ctr = rc[q]; rs.idx = ri[q];
+              }
+            }
+          }
+#else
           for (int radius_iter = 0; radius_iter < 4; ++radius_iter) {
             const uint32_t r1 = rng_u32(rs); const uint32_t r2 = rng_u32(rs);
             const int rxs = (int)(((r1 % 2 == 0) ? 1u : 0xFFFFFFFFu) * r2 % (uint32_t)shift_range);
@@ -173,6 +224,7 @@ __global__ void __launch_bounds__(256, DPE_GN_WAVES) k_gen_neighbours(const Pass
               break;
             }
           }
+#endif
           if ((dir_valid >> dir_index) & 1ull) break;
         }
         float2 rd = make_float2(od.x * cos_angle - od.y * sin_angle, od.x * sin_angle + od.y * cos_angle);
