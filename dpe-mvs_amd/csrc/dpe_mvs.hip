@@ -40,7 +40,7 @@ static constexpr int kWeakLanes = DPE_WEAK_LANES;   // lanes per weak pixel in k
 #define DPE_TEX_D2W TEX_F16
 #endif
 #ifndef DPE_TEX_LR
-#define DPE_TEX_LR TEX_U8
+#define DPE_TEX_LR TEX_F16
 #endif
 static constexpr int kTexInit = TEX_U8, kTexStrong = DPE_TEX_STRONG, kTexWeak = DPE_TEX_WEAK;
 static constexpr int kTexD2W = DPE_TEX_D2W, kTexLR = DPE_TEX_LR;

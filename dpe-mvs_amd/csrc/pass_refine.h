@@ -292,6 +292,9 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_depth_to_weak(const Pass
 // view counts are.  Per-hypothesis sums over views then run on one lane each, in ascending view
 // order (the reference's si loop), and the arg-min on the pixel's first lane.
 constexpr int kLrPix = 4;
+#ifndef DPE_LR_VIEW_MAJOR
+#define DPE_LR_VIEW_MAJOR 1
+#endif
 template <int U8>
 __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_local_refine_jobs(const PassConst* __restrict__ pcp, DevBufs B) {   // DPE.cu:2749-2835
   __shared__ float s_patch[4][kLrPix][108];
@@ -371,8 +374,16 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_local_refine_jobs(const 
     }
     const int ns = s_cnt[wave][p][0];
     unsigned m = (unsigned)s_cnt[wave][p][1];
+#if DPE_LR_VIEW_MAJOR
+    // view-major: a pixel's hypotheses (depths a disparity step apart, one normal) of one view sit
+    // on adjacent lanes, so their taps gather from neighbouring texels
+    const int nh = __popc(m);
+    for (int q = r % nh; q > 0; --q) m &= m - 1;      // the (r % nh)-th valid hypothesis
+    const int h = __builtin_ctz(m), k = r / nh;
+#else
     for (int q = r / ns; q > 0; --q) m &= m - 1;     // the (r / ns)-th valid hypothesis
     const int h = __builtin_ctz(m), k = r % ns;
+#endif
     const long px = base + p;
     const int jx = (int)(px % W), jy = (int)(px / W);
     const int si = s_sel[wave][p][k] + 1;

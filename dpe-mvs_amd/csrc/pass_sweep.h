@@ -759,6 +759,9 @@ DEV float ncc_new_tab(const PassConst& pc, const DevBufs& B, const WeakTab& T, i
   return (float)(0.25 * (double)center_cost + 0.75 * (double)strong_cost);
 }
 
+#ifndef DPE_WEAK_VIEW_MAJOR
+#define DPE_WEAK_VIEW_MAJOR 1
+#endif
 // LDS floats per weak pixel (fixed part 480, see the carve in k_weak_coop); multiple of 4
 __host__ __device__ inline int weak_lds_per_pixel(int nv) { return (480 + 17 * nv + 3) & ~3; }
 
@@ -911,8 +914,13 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassCons
     const int ncand = __builtin_popcount(um);
     for (int j = c; j < ncand * nv; j += C) {
       uint32_t m = um;
+#if DPE_WEAK_VIEW_MAJOR
+      for (int q = j % ncand; q > 0; --q) m &= m - 1;     // view-major: a round's lanes share views
+      const int i = __builtin_ctz(m), v = j / ncand + 1;
+#else
       for (int q = j / nv; q > 0; --q) m &= m - 1;
       const int i = __builtin_ctz(m), v = j % nv + 1;
+#endif
       cost[i * nv + v - 1] = ncc_new_tab<U8>(pc, B, T, x, y, v, cpl[i]);
     }
   }
