@@ -42,7 +42,10 @@ static constexpr int kWeakLanes = DPE_WEAK_LANES;   // lanes per weak pixel in k
 #ifndef DPE_TEX_LR
 #define DPE_TEX_LR TEX_F16
 #endif
-static constexpr int kTexInit = TEX_U8, kTexStrong = DPE_TEX_STRONG, kTexWeak = DPE_TEX_WEAK;
+#ifndef DPE_TEX_INIT
+#define DPE_TEX_INIT TEX_F16
+#endif
+static constexpr int kTexInit = DPE_TEX_INIT, kTexStrong = DPE_TEX_STRONG, kTexWeak = DPE_TEX_WEAK;
 static constexpr int kTexD2W = DPE_TEX_D2W, kTexLR = DPE_TEX_LR;
 
 namespace {
