@@ -96,6 +96,8 @@ struct DpeContext {
   std::vector<CachedImage*> icache;
   uint64_t icache_clock = 0;
   hipStream_t stream = nullptr;
+  hipStream_t aux = nullptr;         // GenNeighbours beside the first strong half-sweep
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   bool staged = false;
   bool timing = false;
   bool counting = false;
@@ -186,6 +188,11 @@ DpeContext* dpe_create(int device) {
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     g_err = "dpe_create: stream"; delete c; return nullptr;
   }
+  if (hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
+    g_err = "dpe_create: aux stream"; delete c; return nullptr;
+  }
   for (auto& e : c->ev) hipEventCreate(&e);
   return c;
 }
@@ -222,6 +229,9 @@ void dpe_destroy(DpeContext* c) {
   c->cnt.release();
   c->tab_right.release(); c->tab_down.release();
   c->lists.release(); c->row_counts.release(); c->list_totals.release();
+  hipStreamSynchronize(c->aux);
+  hipEventDestroy(c->ev_fork); hipEventDestroy(c->ev_join);
+  hipStreamDestroy(c->aux);
   hipStreamDestroy(c->stream);
   delete c;
 }
@@ -438,8 +448,9 @@ extern "C" int dpe_pm_stage(DpeContext* c, const DpePassInput* in, const DpePass
   HIPC(c->nb.ensure(L * 9)); HIPC(c->nearest.ensure(L)); HIPC(c->edge_neigh.ensure(L * 8)); HIPC(c->lab_bound.ensure(L * 8));
   HIPC(c->radius.ensure(L));
   HIPC(c->tab_right.ensure(L)); HIPC(c->tab_down.ensure(L));
-  HIPC(c->lists.ensure(4 * (L / 2 + 64) + L + 64)); HIPC(c->row_counts.ensure(4 * (size_t)H + 4)); HIPC(c->list_totals.ensure(8));
+  HIPC(c->lists.ensure(5 * (L / 2 + 64) + L + 64)); HIPC(c->row_counts.ensure(4 * (size_t)H + 4)); HIPC(c->list_totals.ensure(8));
   B.planes = c->planes.p; B.planes_snap = c->planes_snap.p; B.fit_plane = c->fit_plane.p;
+  B.planes0 = c->planes0.p;
   B.costs = c->costs.p; B.costs_snap = c->costs_snap.p; B.complex_ = c->complex_.p;
   B.sel = c->sel.p; B.sel_snap = c->sel_snap.p;
   B.weak = c->weak.p; B.weak_rel = c->weak_rel.p; B.vw = c->vw.p;
@@ -497,7 +508,7 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   HIPC(hipMemsetAsync(B.costs, 0, L * sizeof(float), s));
   HIPC(hipMemsetAsync(B.fit_plane, 0, L * sizeof(float4), s));
   HIPC(hipMemsetAsync(B.complex_, 0, L * sizeof(float), s));
-  HIPC(hipMemsetAsync(B.weak_rel, 0, L, s));
+  HIPC(hipMemsetAsync(B.weak_rel, 0xFF, L, s));   // GenNeighbours writes 0 / 1 for every WEAK pixel
   HIPC(hipMemsetAsync(B.vw, 0, L * DPE_MAX_IMAGES, s));
   HIPC(hipMemsetAsync(B.nb, 0xFF, L * 9 * sizeof(short2), s));
   HIPC(hipMemsetAsync(B.nearest, 0xFF, L * sizeof(short2), s));
@@ -516,43 +527,75 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   k_strong_tables_rows<<<(H + 63) / 64, 64, 0, s>>>(dpc, Bc, c->tab_right.p);
   k_strong_tables_cols<<<(W + 63) / 64, 64, 0, s>>>(dpc, Bc, c->tab_down.p);
   k_find_nearest_strong<<<fg, fb, 0, s>>>(dpc, Bc, c->tab_right.p, c->tab_down.p);
-  // list of all WEAK pixels (list slot 4), then GenNeighbours one wave per WEAK pixel
+  // list of all WEAK pixels (list slot 4), then GenNeighbours one thread per WEAK pixel
   const long list_stride = (long)(L / 2 + 64);
   int* weak_list = c->lists.p + 4 * list_stride;
+  int* failed_list = weak_list + L + 64;             // MODE 2 list (slot 5 of list_totals)
   k_list_count<1><<<(H + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p);
   k_list_scan<1><<<1, 64, 0, s>>>(dpc, c->row_counts.p, c->list_totals.p + 4);
   k_list_fill<1><<<(H + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p, weak_list, (long)L);
-  k_gen_neighbours<<<(unsigned)((L + 255) / 256), 256, 0, s>>>(dpc, Bc, weak_list, c->list_totals.p + 4);
-  k_neighbour_update<<<fg, fb, 0, s>>>(dpc, Bc);
-  // per-colour pixel lists of the sweeps (weak_info is fixed from here until DepthToWeak)
-  k_list_count<0><<<(pc.half_rows + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p);
-  k_list_scan<0><<<1, 256, 0, s>>>(dpc, c->row_counts.p, c->list_totals.p);
-  k_list_fill<0><<<(pc.half_rows + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p, c->lists.p, list_stride);
+  // GenNeighbours + NeigbourUpdate only decide which WEAK pixels join the strong lists; nothing the
+  // first strong half-sweep (iteration 0, colour 0) or RandomInitialization reads is written by
+  // them, and GenNeighbours reads the staged planes, not the ones those two rewrite.  So they run
+  // on the aux stream beside RandomInitialization + that half-sweep over the pixels that were not
+  // WEAK; the colour-0 pixels whose GenNeighbours failed (NeigbourUpdate makes them UNKNOWN) get the
+  // same half-sweep (same snapshot) once the streams join.  Pixels of one half-sweep are
+  // independent, so this is the reference's order of results.  Timed / counting executes keep
+  // one stream (per-class events).
+  const bool overlap = !timing && !c->counting;
+  hipStream_t a = overlap ? c->aux : s;
+  if (overlap) {   // pre-GenNeighbours sweep lists (the colour-0 strong list is the one used)
+    k_list_count<0><<<(pc.half_rows + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p);
+    k_list_scan<0><<<1, 256, 0, s>>>(dpc, c->row_counts.p, c->list_totals.p);
+    k_list_fill<0><<<(pc.half_rows + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p, c->lists.p, list_stride);
+    HIPC(hipEventRecord(c->ev_fork, s));
+    HIPC(hipStreamWaitEvent(a, c->ev_fork, 0));
+  }
+  k_gen_neighbours<<<(unsigned)((L + 255) / 256), 256, 0, a>>>(dpc, Bc, weak_list, c->list_totals.p + 4);
+  k_neighbour_update<<<fg, fb, 0, a>>>(dpc, Bc);
+  if (overlap) {
+    k_list_count<2><<<(pc.half_rows + 3) / 4, 256, 0, a>>>(dpc, Bc, c->row_counts.p);
+    k_list_scan<2><<<1, 64, 0, a>>>(dpc, c->row_counts.p, c->list_totals.p + 5);
+    k_list_fill<2><<<(pc.half_rows + 3) / 4, 256, 0, a>>>(dpc, Bc, c->row_counts.p, failed_list, list_stride);
+    HIPC(hipEventRecord(c->ev_join, a));
+  } else {
+    // per-colour pixel lists of the sweeps (weak_info is fixed from here until DepthToWeak)
+    k_list_count<0><<<(pc.half_rows + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p);
+    k_list_scan<0><<<1, 256, 0, s>>>(dpc, c->row_counts.p, c->list_totals.p);
+    k_list_fill<0><<<(pc.half_rows + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p, c->lists.p, list_stride);
+  }
   end();
   Bc = begin(DPE_CLASS_INIT);
   if (c->img8) k_random_init<kTexInit><<<fg, fb, 0, s>>>(dpc, Bc); else k_random_init<TEX_F32><<<fg, fb, 0, s>>>(dpc, Bc);
   end();
   HIPC(hipGetLastError());
+  auto strong_sweep = [&](const DevBufs& Bs, int it, const int* lst, const int* cnt) {
+    const bool edge = pc.P.use_edge;
+    const int P = edge ? 4 : 8, C = edge ? 16 : 8;
+    const size_t lds = (size_t)4 * strong_lds_per_wave(P, C, nv) * sizeof(float);
+    const unsigned grid = (unsigned)((L / 2 + 1 + 4 * P - 1) / (4 * P));
+    if (edge) {
+      if (c->img8) k_strong_coop<kTexStrong, true><<<grid, 256, lds, s>>>(dpc, Bs, it, lst, cnt);
+      else k_strong_coop<TEX_F32, true><<<grid, 256, lds, s>>>(dpc, Bs, it, lst, cnt);
+    } else {
+      if (c->img8) k_strong_coop<kTexStrong, false><<<grid, 256, lds, s>>>(dpc, Bs, it, lst, cnt);
+      else k_strong_coop<TEX_F32, false><<<grid, 256, lds, s>>>(dpc, Bs, it, lst, cnt);
+    }
+  };
   for (int it = 0; it < pc.P.max_iterations; ++it) {
     for (int colour = 0; colour < 2; ++colour) {
       HIPC(hipMemcpyAsync(B.planes_snap, B.planes, L * sizeof(float4), hipMemcpyDeviceToDevice, s));
       HIPC(hipMemcpyAsync(B.costs_snap, B.costs, L * sizeof(float), hipMemcpyDeviceToDevice, s));
       HIPC(hipMemcpyAsync(B.sel_snap, B.sel, L * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
       Bc = begin(DPE_CLASS_STRONG);
-      {
-        const int* lst = c->lists.p + (colour * 2 + 0) * list_stride;
-        const int* cnt = c->list_totals.p + colour * 2 + 0;
-        const bool edge = pc.P.use_edge;
-        const int P = edge ? 4 : 8, C = edge ? 16 : 8;
-        const size_t lds = (size_t)4 * strong_lds_per_wave(P, C, nv) * sizeof(float);
-        const unsigned grid = (unsigned)((L / 2 + 1 + 4 * P - 1) / (4 * P));
-        if (edge) {
-          if (c->img8) k_strong_coop<kTexStrong, true><<<grid, 256, lds, s>>>(dpc, Bc, it, lst, cnt);
-          else k_strong_coop<TEX_F32, true><<<grid, 256, lds, s>>>(dpc, Bc, it, lst, cnt);
-        } else {
-          if (c->img8) k_strong_coop<kTexStrong, false><<<grid, 256, lds, s>>>(dpc, Bc, it, lst, cnt);
-          else k_strong_coop<TEX_F32, false><<<grid, 256, lds, s>>>(dpc, Bc, it, lst, cnt);
-        }
+      strong_sweep(Bc, it, c->lists.p + (colour * 2 + 0) * list_stride, c->list_totals.p + colour * 2 + 0);
+      if (overlap && it == 0 && colour == 0) {
+        HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
+        strong_sweep(Bc, it, failed_list, c->list_totals.p + 5);
+        // the sweep lists after NeigbourUpdate (weak_info is fixed from here until DepthToWeak)
+        k_list_count<0><<<(pc.half_rows + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p);
+        k_list_scan<0><<<1, 256, 0, s>>>(dpc, c->row_counts.p, c->list_totals.p);
+        k_list_fill<0><<<(pc.half_rows + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p, c->lists.p, list_stride);
       }
       end();
     }

@@ -43,6 +43,7 @@ struct DevBufs {
   const float* depth[DPE_MAX_IMAGES];
   const float* ref;
   float4* planes; float4* planes_snap; float4* fit_plane;
+  const float4* planes0;                  // the staged initial planes (read by GenNeighbours)
   float* costs; float* costs_snap; float* complex_;
   uint32_t* sel; uint32_t* sel_snap;
   uint8_t* weak; uint8_t* weak_rel; uint8_t* vw;

@@ -313,13 +313,13 @@ __global__ void __launch_bounds__(256, DPE_GN_WAVES) k_gen_neighbours(const Pass
   float spd[64];
   int valid_count = 0;
   float X[3];
-  get3d(camera, x, y, B.planes[center].w, X);
+  get3d(camera, x, y, B.planes0[center].w, X);
   const float cpz = X[2];
   for (int i = 0; i < 64; ++i) {
     if ((dir_valid >> i) & 1ull) {
       const short2 sp = strong_points[i];
       spv[valid_count] = sp;
-      spd[valid_count] = B.planes[sp.x + sp.y * W].w;
+      spd[valid_count] = B.planes0[sp.x + sp.y * W].w;
       valid_count++;
     }
   }
@@ -335,7 +335,7 @@ __global__ void __launch_bounds__(256, DPE_GN_WAVES) k_gen_neighbours(const Pass
     return make_float3(Y[0], Y[1], Y[2]);
   };
   auto normal3 = [&](int i) -> float3 {
-    const float4 n4 = transform_normal_ref(camera, B.planes[spv[i].x + spv[i].y * W]);
+    const float4 n4 = transform_normal_ref(camera, B.planes0[spv[i].x + spv[i].y * W]);
     return make_float3(n4.x, n4.y, n4.z);
   };
   PHASE(2);

@@ -21,9 +21,13 @@ namespace dpe {
 // MODE 0: list[k] (k = colour*2 + weak?1:0) = pixels of that colour and class inside the red/black
 //         grid (rows < half_rows), for the sweeps (built after NeigbourUpdate).
 // MODE 1: one list of all WEAK pixels (rows < H), for GenNeighbours (built before it).
+// MODE 2: colour-0 pixels of the red/black grid whose GenNeighbours failed (weak_rel == 0; the
+//         pixels NeigbourUpdate turns UNKNOWN), for the iteration-0 colour-0 strong sweep that runs
+//         beside GenNeighbours on the pre-GenNeighbours list (see dpe_pm_execute).
 // Row-major order; one wave per row; ballot compaction keeps the order deterministic.
-template <int MODE> DEV int list_rows(const PassConst& pc) { return MODE ? pc.H : pc.half_rows; }
+template <int MODE> DEV int list_rows(const PassConst& pc) { return MODE == 1 ? pc.H : pc.half_rows; }
 template <int MODE> DEV int list_key(const PassConst& pc, const DevBufs& B, int x, int y) {
+  if constexpr (MODE == 2) return (((x + y) & 1) == 0 && B.weak_rel[y * pc.W + x] == 0) ? 0 : -1;
   const bool wk = B.weak[y * pc.W + x] == DPE_WEAK;
   if constexpr (MODE == 1) return wk ? 0 : -1;
   else return (((x + y) & 1) << 1) | (wk ? 1 : 0);

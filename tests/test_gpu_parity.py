@@ -120,6 +120,23 @@ def test_execute_idempotent_and_deterministic(ctx):
         assert bits_equal(a[k], b[k]), k
 
 
+def test_overlapped_and_sequential_schedules_agree(ctx):
+    # untimed executes run GenNeighbours on a second stream beside the first strong half-sweep;
+    # timed executes keep one stream.  Both must give the oracle's bits.
+    sc = synthetic.make_scene(128, 96, 6)
+    p = _params("refine_iter")
+    st = synthetic.gt_state(sc, seed=11)
+    inp = synthetic.pass_input(sc, p, depths=synthetic.src_depths(sc), seed=5)
+    ctx.stage(inp, st)
+    ctx.set_timing(True)
+    ctx.execute(); seq = ctx.fetch()
+    ctx.set_timing(False)
+    ctx.execute(); ovl = ctx.fetch()
+    for k in seq:
+        assert bits_equal(seq[k], ovl[k]), k
+    assert_same(ovl, oracle.run_pass(inp, st), "overlapped schedule")
+
+
 def test_error_paths(ctx):
     from DPE_MVS import native
     sc = synthetic.make_scene(32, 24, 2)

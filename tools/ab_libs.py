@@ -8,6 +8,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "dpe-mvs_amd"))
+import torch  # noqa: E402  (initialised before the libraries, as in bench.py)
+torch.cuda.set_device(0)
 import bench  # noqa: E402
 from DPE_MVS import _abi, native, synthetic  # noqa: E402
 
@@ -37,7 +39,24 @@ for rnd in range(3):
         buf = (C.c_float * 9)()
         lib.dpe_pm_last_timings(ctx, buf, 9)
         res[path].append([float(x) for x in buf])
+# wall clock of untimed executes (per-class events off: the pass may then overlap streams)
+import time  # noqa: E402
+wall = {path: [] for path in libs}
+for path, lib, ctx, bufs in ctxs:
+    lib.dpe_set_timing(ctx, 0)
+for rnd in range(3):
+    for path, lib, ctx, bufs in ctxs:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(5):
+            assert lib.dpe_pm_execute(ctx, None) == 0
+        assert lib.dpe_pm_fetch(ctx, C.byref(bufs.st)) == 0
+        torch.cuda.synchronize()
+        wall[path].append((time.perf_counter() - t0) / 5 * 1e3)
+        assert bufs.planes.tobytes() == ref, f"{path}: untimed output differs from {libs[0]}"
 names = ["total"] + native.CLASSES
 for path in libs:
     best = min(res[path], key=lambda t: t[0])
-    print(os.path.basename(path), json.dumps({k: round(v, 2) for k, v in zip(names, best)}), flush=True)
+    d = {k: round(v, 2) for k, v in zip(names, best)}
+    d["wall_ms"] = round(min(wall[path]), 2)
+    print(os.path.basename(path), json.dumps(d), flush=True)
