@@ -542,7 +542,9 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   // same half-sweep (same snapshot) once the streams join.  Pixels of one half-sweep are
   // independent, so this is the reference's order of results.  Timed / counting executes keep
   // one stream (per-class events).
-  const bool overlap = !timing && !c->counting;
+  // DPE_OVERLAP=0 keeps one stream (profiling runs whose per-kernel durations must not overlap)
+  static const bool overlap_env = [] { const char* e = getenv("DPE_OVERLAP"); return !(e && atoi(e) == 0); }();
+  const bool overlap = overlap_env && !timing && !c->counting;
   hipStream_t a = overlap ? c->aux : s;
   if (overlap) {   // pre-GenNeighbours sweep lists (the colour-0 strong list is the one used)
     k_list_count<0><<<(pc.half_rows + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p);
