@@ -154,7 +154,10 @@ int dpe_pm_stage(DpeContext* ctx, const DpePassInput* in, const DpePassState* st
 /*
  * Runs the whole pass (DPE.cu:3150-3226) on device-resident data on `stream` (a hipStream_t,
  * NULL = the context's stream).  Every call starts from the staged initial state, so repeated
- * calls are idempotent.  Asynchronous w.r.t. the host.
+ * calls are idempotent.  Asynchronous w.r.t. the host.  Part of the pass (GenNeighbours) runs on
+ * the context's second stream, forked from and joined back into `stream` with events, so all
+ * work is complete when `stream` reaches the end of the call's enqueued work (environment
+ * DPE_OVERLAP=0, timing or counting keep everything on `stream`).
  */
 int dpe_pm_execute(DpeContext* ctx, void* stream);
 
