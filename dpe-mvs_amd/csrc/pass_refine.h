@@ -140,6 +140,66 @@ DEV void lds_taps(const float* pw, int px, int py, const PassConst& pc, const De
     acc[0] = s_src; acc[1] = s_ss; acc[2] = s_rs;
   }
 }
+// Row a of lds_taps<U8, FAST> with the same operations: (r_src, r_ss, r_rs) of taps (a, 0..5).
+// lds_taps adds its six row triplets to zero in row order, so summing these in row order gives
+// its result bit for bit; the strong sweep's pool uses this to split the jobs of a nearly empty
+// last round over several lanes.
+template <int U8, bool FAST>
+DEV void lds_row(const float* pw, int px, int py, const PassConst& pc, const DevBufs& B, int v, const Homog& H, int a,
+                 float* r3) {
+  const int W = pc.W, Hh = pc.H;
+  const float x = (float)(px - 5 + 2 * a);
+  if constexpr (U8 != TEX_F32 && FAST && DPE_PACKED_TAP) {
+    const uint32_t vofs = (uint32_t)v * tex_view<U8>(B), stride = (uint32_t)(W + 2);
+    const f2v lim = (f2v){(float)W, (float)Hh};
+    const f2v* wp = (const f2v*)pw;
+    const f2v bxy = fma2((f2v){H.h[0], H.h[3]}, f2s(x), (f2v){H.h[2], H.h[5]});
+    const float bz = __builtin_fmaf(H.h[6], x, H.h[8]);
+    f2v r_sr = f2s(0.0f);
+    float r_ss = 0;
+#if DPE_TAP_PAIR
+#pragma unroll
+    for (int b = 0; b < 6; b += 2) {
+      const f2v sp = tap2_fast<U8>(B, vofs, stride, lim, H.h, bxy, bz, (f2v){(float)(py - 5 + 2 * b), (float)(py - 3 + 2 * b)});
+      const f2v w0 = wp[a * 6 + b], w1 = wp[a * 6 + b + 1];
+      const f2v ws = (f2v){w0.x, w1.x} * sp;
+      r_sr = fma2(w0, f2s(sp.x), r_sr);
+      r_ss = __builtin_fmaf(ws.x, sp.x, r_ss);
+      r_sr = fma2(w1, f2s(sp.y), r_sr);
+      r_ss = __builtin_fmaf(ws.y, sp.y, r_ss);
+    }
+#else
+#pragma unroll
+    for (int b = 0; b < 6; ++b) {
+      const float sp = tap_u8_fast<U8>(B, vofs, stride, lim, H.h, bxy, bz, (float)(py - 5 + 2 * b));
+      const f2v w = wp[a * 6 + b];
+      r_sr = fma2(w, f2s(sp), r_sr);
+      const float ws = w.x * sp;
+      r_ss = __builtin_fmaf(ws, sp, r_ss);
+    }
+#endif
+    r3[0] = r_sr.x; r3[1] = r_ss; r3[2] = r_sr.y;
+  } else {
+    const float bx = __builtin_fmaf(H.h[0], x, H.h[2]);
+    const float by = __builtin_fmaf(H.h[3], x, H.h[5]);
+    const float bz = __builtin_fmaf(H.h[6], x, H.h[8]);
+    float r_src = 0, r_ss = 0, r_rs = 0;
+#pragma unroll
+    for (int b = 0; b < 6; ++b) {
+      const float y = (float)(py - 5 + 2 * b);
+      const float qx = __builtin_fmaf(H.h[1], y, bx);
+      const float qy = __builtin_fmaf(H.h[4], y, by);
+      const float iz = rcp_sel<FAST>(__builtin_fmaf(H.h[7], y, bz));
+      const float sp = sample_src<U8>(B, v, W, Hh, qx * iz, qy * iz);
+      const float w = pw[2 * (a * 6 + b)], wr = pw[2 * (a * 6 + b) + 1];
+      r_src = __builtin_fmaf(w, sp, r_src);
+      const float ws = w * sp;
+      r_ss = __builtin_fmaf(ws, sp, r_ss);
+      r_rs = __builtin_fmaf(wr, sp, r_rs);
+    }
+    r3[0] = r_src; r3[1] = r_ss; r3[2] = r_rs;
+  }
+}
 #ifndef DPE_CLAMP_ELIDE
 #define DPE_CLAMP_ELIDE 1
 #endif

@@ -285,8 +285,13 @@ DEV int acmh_candidate(const PassConst& pc, const float* __restrict__ costs, int
 __host__ __device__ inline int strong_lds_base(int P, int C, int nv) {   // floats before the plane table
   return (P * (165 + 2 * C + (C + 8) * nv) + 3) & ~3;
 }
+#ifndef DPE_TAIL_SPLIT
+#define DPE_TAIL_SPLIT 1
+#endif
+constexpr int kTailJobs = 16;   // a last round of at most this many jobs is split by patch rows
 __host__ __device__ inline int strong_lds_per_wave(int P, int C, int nv) {
-  return strong_lds_base(P, C, nv) + P * (C + 1) * 5;   // + planes [P][C+1] float4 + alias [P][C+1]
+  // + planes [P][C+1] float4 + alias [P][C+1] (+ the split tail's row sums [kTailJobs][6][3])
+  return strong_lds_base(P, C, nv) + P * (C + 1) * 5 + (DPE_TAIL_SPLIT ? kTailJobs * 18 : 0);
 }
 
 // Job pools of a wave: the NCCs of all its pixels are dealt round-robin over the 64 lanes, so a
@@ -432,7 +437,12 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_strong_coop(const PassCo
 #pragma unroll
     for (int q = 0; q < P; ++q) { cnt[q] = ib_all[q * ibs + C + 8 + 1]; S += cnt[q]; }
     int q, r;
-    for (int j = lane; j < S * nv; j += 64) {
+    const int total = S * nv, tail = total & 63;
+    // a last round with at most kTailJobs jobs: each job's 6 patch rows go to 64 / tail lanes (rows
+    // per lane 1 or 2), the row sums meet in LDS, and one lane per job adds them in row order
+    const bool split = DPE_TAIL_SPLIT && fast && tail > 0 && tail <= kTailJobs;
+    const int jend = split ? total - tail : total;
+    for (int j = lane; j < jend; j += 64) {
       job_decode<P>(cnt, j % S, q, r);
       const int* iq = ib_all + q * ibs;
       const int slot = iq[C + 16 + nv + r], v = j / S + 1;
@@ -442,6 +452,48 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_strong_coop(const PassCo
       const float* sm = sums_all + q * 4;
       cost_all[(q * (C + 1) + slot) * nv + v - 1] =
           ncc_old_any<U8>(fast, pw_all + q * 108, sm[0], sm[1], sm[2], qx, qy, pc, B, v, pl);
+    }
+    if (split) {
+      float* tb = wl + strong_lds_per_wave(P, C, nv) - kTailJobs * 18;   // [job][row][3]
+      const int rpp = 64 / tail >= 6 ? 1 : 2, npc = 6 / rpp;            // rows per lane, lanes per job
+      if (lane < tail * npc) {
+        const int j = jend + lane / npc, a0 = (lane % npc) * rpp;
+        job_decode<P>(cnt, j % S, q, r);
+        const int slot = ib_all[q * ibs + C + 16 + nv + r], v = j / S + 1;
+        const int cq = list[wbase + q];
+        const int qx = cq % W, qy = cq / W;
+        const Homog H = make_homography(pc, v, cpl_all[q * (C + 1) + slot]);
+        if (!center_outside(pc, v, H, qx, qy)) {
+          const bool fr = rcp_range_ok(H, (float)(qx - 5), (float)(qx + 5), (float)(qy - 5), (float)(qy + 5));
+          for (int a = a0; a < a0 + rpp; ++a) {
+            float* r3 = tb + ((lane / npc) * 6 + a) * 3;
+            if (fr) lds_row<U8, true>(pw_all + q * 108, qx, qy, pc, B, v, H, a, r3);
+            else lds_row<U8, false>(pw_all + q * 108, qx, qy, pc, B, v, H, a, r3);
+          }
+        }
+      }
+      wave_sync();
+      if (lane < tail) {
+        const int j = jend + lane;
+        job_decode<P>(cnt, j % S, q, r);
+        const int slot = ib_all[q * ibs + C + 16 + nv + r], v = j / S + 1;
+        const int cq = list[wbase + q];
+        const Homog H = make_homography(pc, v, cpl_all[q * (C + 1) + slot]);
+        float cst = 2.0f;
+        if (center_outside(pc, v, H, cq % W, cq / W)) {
+          count_work(B, 1, 0);
+        } else {
+          count_work(B, 1, 36);
+          float s_src = 0, s_ss = 0, s_rs = 0;
+          for (int a = 0; a < 6; ++a) {
+            const float* r3 = tb + (lane * 6 + a) * 3;
+            s_src += r3[0]; s_ss += r3[1]; s_rs += r3[2];
+          }
+          const float* sm = sums_all + q * 4;
+          cst = ncc_finalize_pre(sm[0], sm[1], sm[2], s_src, s_ss, s_rs);
+        }
+        cost_all[(q * (C + 1) + slot) * nv + v - 1] = cst;
+      }
     }
   }
   wave_sync();
