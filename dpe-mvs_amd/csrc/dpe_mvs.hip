@@ -191,7 +191,13 @@ DpeContext* dpe_create(int device) {
   if (hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
-    g_err = "dpe_create: aux stream"; delete c; return nullptr;
+    g_err = "dpe_create: aux stream";
+    if (c->ev_join) hipEventDestroy(c->ev_join);
+    if (c->ev_fork) hipEventDestroy(c->ev_fork);
+    if (c->aux) hipStreamDestroy(c->aux);
+    hipStreamDestroy(c->stream);
+    delete c;
+    return nullptr;
   }
   for (auto& e : c->ev) hipEventCreate(&e);
   return c;
