@@ -76,6 +76,8 @@ CASES = [
     (80, 60, 4, "acmh_geom"),
     (88, 66, 4, "no_limit"),
     (72, 56, 3, "weak_generic"),
+    (23, 131, 3, "refine_iter"),         # tall, narrow: W < one block, ragged in both axes
+    (193, 29, 3, "first"),               # W = 3*64+1: one pixel into a fourth wave-width column
 ]
 
 
