@@ -36,6 +36,7 @@ HBM_PEAK_GBS = 8000.0           # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 FLOP_PER_TAP = 32               # algorithmic model: 36-tap NCC = 36*32 + 120
 FLOP_PER_HOMOGRAPHY = 120
 FLOP_PER_GEOM = 60
+MODEL_FLOP_PER_PX = (36 * FLOP_PER_TAP + FLOP_PER_HOMOGRAPHY) * (42 * (NV_ - 1) + 75 * 4)   # 0.86 MFLOP
 # per-dispatch HBM bytes from the committed PMC passes (tools/pmc.sh + tools/prof_summary.py)
 PMC_JSON = os.path.join(ROOT, "profiles", "r01_pmc.json")
 CLASS_KERNEL = {"strong": "k_strong_coop", "weak": "k_weak_coop", "depth_to_weak": "k_depth_to_weak",
@@ -72,29 +73,65 @@ def pmc_traffic(cls: str):
     return sum(vals) / len(vals) if vals else None
 
 
-def cpu_baseline(abi, synthetic, seconds_hint: float = 20.0) -> dict:
-    """Scalar C++ restatement (oracle/) timed on this host's cores on a bounded sample of the same
-    workload: the same pass (9 source views, same parameters) on a 640x480 instance of the scene
-    (about 10 s on 16 host threads)."""
+def crop_rows(sc: dict, y0: int, y1: int) -> dict:
+    """The scene restricted to reference-image rows [y0, y1) of every view: images, depths, edges and
+    labels cropped, principal point and height of every camera moved with the crop.  A valid pass of
+    the same workload on a full-width band (a 256-row crop, extrapolated in rows)."""
+    import copy
+    out = dict(sc)
+    out["H"] = y1 - y0
+    cams = []
+    for c in sc["cams"]:
+        c2 = copy.deepcopy(c)
+        c2.K[5] = float(np.float32(c.K[5]) - np.float32(y0))
+        c2.height = y1 - y0
+        cams.append(c2)
+    out["cams"] = cams
+    out["images"] = [np.ascontiguousarray(im[y0:y1]) for im in sc["images"]]
+    out["views"] = [dict(v, depth=np.ascontiguousarray(v["depth"][y0:y1]), normals=np.ascontiguousarray(v["normals"][y0:y1]),
+                         sid=v["sid"][y0:y1], image=out["images"][k]) for k, v in enumerate(sc["views"])]
+    out["edge"] = np.ascontiguousarray(sc["edge"][y0:y1])
+    out["label"] = np.ascontiguousarray(sc["label"][y0:y1])
+    lo = (y0 // 2, (y1 + 1) // 2)
+    out["edge_low"] = np.ascontiguousarray(sc["edge_low"][lo[0]:lo[1]])
+    out["weak_gt"] = sc["weak_gt"][y0:y1]
+    return out
+
+
+def cpu_baseline(abi, synthetic, sc: dict) -> tuple:
+    """Scalar C++ restatement (oracle/) timed on this host's cores: the headline pass
+    (same parameters, 9 source views) on full-width row bands of the 1600x1200 scene, extrapolated
+    linearly in rows -- all host threads on a 256-row band, 1 thread on a 32-row band (bounded:
+    about 10-30 s of CPU work each on the GPU box)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # checker / baseline only
-    w, h = 640, 480
-    sc = synthetic.make_scene(w, h, NV_, low_scale=2)
+    W, H = sc["W"], sc["H"]
     p = workload_params(abi, NV_)
-    inp = synthetic.pass_input(sc, p, depths=synthetic.src_depths(sc))
-    st = synthetic.gt_state(sc)
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    cores = max(1, min(cores, 16))
-    t0 = time.perf_counter()
-    ref = oracle.run_pass(inp, st, threads=cores)
-    dt = time.perf_counter() - t0
-    base = {"value": round(w * h / dt / 1e6, 6), "unit": "Mpix/s", "cores": cores, "kind": "port",
-            "sample": f"one full REFINE_ITER+geom pass, {w}x{h}, 9 source views, oracle/ scalar C++ "
-                      f"restatement, {cores} threads, {dt:.1f} s"}
-    return base, (inp, st, ref, f"{w}x{h}")
+    res = {}
+    sample = None
+    for threads, rows in ((oracle.host_threads(), 256), (1, 32)):
+        y0 = (H - rows) // 2
+        band = crop_rows(sc, y0, y0 + rows)
+        inp = synthetic.pass_input(band, p, depths=synthetic.src_depths(band))
+        st = synthetic.gt_state(band)
+        t0 = time.perf_counter()
+        ref = oracle.run_pass(inp, st, threads=threads)
+        dt = time.perf_counter() - t0
+        res[threads] = (dt, rows, dt * H / rows)
+        if sample is None:
+            sample = (inp, st, ref, f"{W}x{rows} band (rows {y0}..{y0 + rows - 1})")
+    nt = max(res)
+    dt, rows, full = res[nt]
+    dt1, rows1, full1 = res[1]
+    base = {"value": round(W * H / full / 1e6, 6), "unit": "Mpix/s", "cores": nt, "kind": "port",
+            "sample": f"the headline REFINE_ITER+geom pass (9 source views) on a full-width {rows}-row band "
+                      f"({W}x{rows}), oracle/ scalar C++ restatement, {nt} threads, {dt:.1f} s, extrapolated "
+                      f"x{H / rows:.2f} in rows to {full:.1f} s per {W}x{H} pass",
+            "single_thread": {"value": round(W * H / full1 / 1e6, 6), "unit": "Mpix/s", "cores": 1,
+                              "sample": f"{W}x{rows1} band, 1 thread, {dt1:.1f} s, extrapolated to {full1:.1f} s per pass"},
+            "host_cpus": os.cpu_count(), "threads_note": "threads = OMP_NUM_THREADS (the GPU box's CPU share) "
+                                                          "or the affinity mask; host_cpus = the whole machine"}
+    return base, sample
 
 
 def end_to_end(local_rank: int, n_images: int, W: int, H: int, scene=None) -> dict:
@@ -283,7 +320,7 @@ def main():
                    "width": Wd, "height": Hd, "num_images": NV_, "max_iterations": 3,
                    "parallelism": f"reference-image sharding x{world}" + (" + RCCL depth all-gather" if world > 1 else "")},
         "roofline": {
-            "bound": "mfma",
+            "bound": "valu",
             "kernel": f"k_{dom}",
             "achieved": round(achieved_tflops, 3),
             "peak": FP32_PEAK_TFLOPS,
@@ -291,11 +328,21 @@ def main():
             "frac": round(achieved_tflops / FP32_PEAK_TFLOPS, 4),
             "traffic": pmc_traffic(dom),
             "traffic_source": os.path.relpath(PMC_JSON, ROOT) + " (FETCH_SIZE x2 x1024 + WRITE_SIZE x1024, per launch)",
-            "note": "FP32-ALU bound (no MFMA-shaped work; the f32 MFMA peak equals the f32 VALU peak). "
-                    "achieved = algorithmic FLOP per launch (120/homography + 32/bilinear tap + 60/geom term, "
-                    "counted on device) / avg launch time (hipEvents)",
+            "note": "FP32 VALU bound (gathers + projective arithmetic, no MFMA-shaped work); peak = the f32 "
+                    "vector peak. achieved = algorithmic FLOP per launch (120/homography + 32/bilinear tap + "
+                    "60/geom term, counted on device) / avg launch time (hipEvents on the pass stream)",
             "avg_launch_ms": round(avg_launch_ms, 3),
             "flop_per_launch": flop_per_launch,
+            # SURVEY.md §8(d)'s fixed model for the whole pass, independent of the device counters (and so of
+            # any work the implementation skips): F = (36*32 + 120) * S per px, S = 42*Ns + 75*4 NCCs
+            "model": {"flop_per_px": MODEL_FLOP_PER_PX, "pass_flop": MODEL_FLOP_PER_PX * L,
+                      "achieved": round(MODEL_FLOP_PER_PX * L / (ms_per_step * 1e-3) / 1e12, 3),
+                      "frac": round(MODEL_FLOP_PER_PX * L / (ms_per_step * 1e-3) / 1e12 / FP32_PEAK_TFLOPS, 4),
+                      "scope": "whole pass wall time (ms_per_step)"},
+            "device_counted": {"pass_flop": pass_flops,
+                               "frac": round(pass_flops / (ms_per_step * 1e-3) / 1e12 / FP32_PEAK_TFLOPS, 4),
+                               "scope": "whole pass wall time; fewer FLOP than the model (identical candidate "
+                                        "planes share one NCC)"},
         },
         "hbm": {"pass_algorithmic_bytes": pass_bytes,
                 "achieved_GBps": round(pass_bytes / (ms_per_step * 1e-3) / 1e9, 2), "peak_GBps": HBM_PEAK_GBS},
@@ -311,7 +358,7 @@ def main():
         ctx = None
         result["end_to_end"] = end_to_end(local_rank, args.e2e_images, Wd, Hd, scene=sc)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"], sample = cpu_baseline(_abi, synthetic)
+        result["cpu_baseline"], sample = cpu_baseline(_abi, synthetic, sc)
         result["parity"] = parity_on_sample(native, local_rank, sample)
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -56,7 +56,23 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.dpe_set_counting.restype = None
     lib.dpe_pm_last_counts.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_int]
     lib.dpe_pm_last_counts.restype = C.c_int
+    lib.dpe_fusion_stage.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+    lib.dpe_fusion_stage.restype = C.c_int
+    lib.dpe_fusion_candidates.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+    lib.dpe_fusion_candidates.restype = C.c_int
     return lib
+
+
+def fusion_view_array(views):
+    """[(depth f32 [H,W], normal f32 [H,W,3], DpeCamera)] -> (DpeFusionView array, arrays to keep alive)."""
+    arr = (_abi.DpeFusionView * len(views))()
+    keep = []
+    for k, (d, n, cam) in enumerate(views):
+        d = np.ascontiguousarray(d, np.float32)
+        n = np.ascontiguousarray(n, np.float32)
+        keep += [d, n]
+        arr[k] = _abi.DpeFusionView(d.shape[1], d.shape[0], cam, d.ctypes.data, n.ctypes.data)
+    return arr, keep
 
 
 _LIB = load_library()
@@ -130,6 +146,18 @@ class PatchMatchContext:
         _LIB.dpe_pm_last_counts(self._ctx, buf, 32)
         return {name: {"ncc": int(buf[4 * i]), "taps": int(buf[4 * i + 1]), "geom": int(buf[4 * i + 2]),
                        "launches": int(buf[4 * i + 3])} for i, name in enumerate(CLASSES)}
+
+    def fusion_candidates(self, views, ref: int, src) -> tuple:
+        """RunFusion's projection tests on the GPU (dpe_fusion_stage + dpe_fusion_candidates) for
+        views = [(depth, normal, DpeCamera)]: (idx int32 [L*ns], val f32 [L*ns*3])."""
+        arr, keep = fusion_view_array(views)
+        _check(_LIB.dpe_fusion_stage(self._ctx, arr, len(views)), "dpe_fusion_stage")
+        s = np.ascontiguousarray(src, np.int32)
+        L = views[ref][0].size
+        idx, val = np.empty(L * len(s), np.int32), np.empty(L * len(s) * 3, np.float32)
+        _check(_LIB.dpe_fusion_candidates(self._ctx, int(ref), s.ctypes.data, len(s), idx.ctypes.data, val.ctypes.data),
+               "dpe_fusion_candidates")
+        return idx, val
 
     def device_planes(self) -> int:
         return int(_LIB.dpe_pm_device_planes(self._ctx) or 0)

@@ -42,6 +42,7 @@ class DpePipelineOptions(C.Structure):
         ("base_seed", C.c_uint64),
         ("keep_intermediate", C.c_bool),
         ("fusion_runner", C.c_void_p), ("fusion_user", C.c_void_p),
+        ("max_iterations", C.c_int), ("photometric_only", C.c_bool),
     ]
 
 
@@ -246,11 +247,14 @@ def _torch_allgather(dist):
 def run_dpe_pipeline(dense_folder: str, gpu_index: int = 0, verbose: bool = True, fusion: bool = False,
                      viz: bool = False, depth: bool = True, normal: bool = False, weak: bool = False,
                      edge: bool = False, schedule: str = "reference", dist=None, runner=None,
-                     base_seed: int = 0x5EED, keep_intermediate: bool = False, fusion_runner=None) -> int:
+                     base_seed: int = 0x5EED, keep_intermediate: bool = False, fusion_runner=None,
+                     max_iterations: int = 0, photometric_only: bool = False) -> int:
     """RunDPEPipeline (main.cpp:474) through libdpe_host.  `dist`: an initialised torch.distributed
     (one process per GPU; problems split in contiguous blocks, depth maps all-gathered per pass).
     `runner`: (C function pointer, user pointer) of a dpe_pass_runner_fn; default the HIP library.
-    `fusion_runner`: (C function pointer, user pointer) of a dpe_fusion_fn; default the HIP kernel."""
+    `fusion_runner`: (C function pointer, user pointer) of a dpe_fusion_fn; default the HIP kernel.
+    `max_iterations` (0 = the reference's 3) and `photometric_only` (no geometric passes) are the
+    schedule knobs of BASELINE configs 1 and 2."""
     o = DpePipelineOptions()
     lib().dpe_pipeline_default_options(C.byref(o))
     o.gpu_index = gpu_index
@@ -258,6 +262,8 @@ def run_dpe_pipeline(dense_folder: str, gpu_index: int = 0, verbose: bool = True
     o.schedule = {"reference": SCHEDULE_REFERENCE, "jacobi": SCHEDULE_JACOBI}[schedule]
     o.base_seed = base_seed
     o.keep_intermediate = keep_intermediate
+    o.max_iterations = max_iterations
+    o.photometric_only = photometric_only
     keep = []
     if dist is not None and dist.get_world_size() > 1:
         o.rank, o.world_size = dist.get_rank(), dist.get_world_size()

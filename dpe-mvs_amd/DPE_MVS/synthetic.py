@@ -14,6 +14,7 @@ boundary pixels (CV_32SC1, the labels_<s>.dmb convention).
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
 
@@ -173,15 +174,29 @@ def make_scene(W: int, H: int, n_views: int, seed: int = SCENE_SEED, low_scale: 
         sgn = 1 if i % 2 == 1 else -1
         angles.append(sgn * 15.0 * k / max(1, (n_views) // 2))
     pix_world = 5.0 / fx
-    views = []
-    for i, a in enumerate(angles):
-        th = math.radians(a)
+
+    def one(i):
+        th = math.radians(angles[i])
         C = O + 5.0 * np.array([math.sin(th), 0.0, -math.cos(th)])
         C[1] += 0.25 * math.sin(1.7 * i)
         R = _look_at(C, O)
         t = -R @ C
         depth, sid, normals, img = render_view(surfs, K, R, C, W, H, pix_world)
-        views.append(dict(K=K, R=R, t=t, C=C, depth=depth, sid=sid, normals=normals, image=img))
+        return dict(K=K, R=R, t=t, C=C, depth=depth, sid=sid, normals=normals, image=img)
+
+    # views are independent and numpy releases the GIL in the large array operations: render them on
+    # a few threads (same arrays as a serial loop)
+    from concurrent.futures import ThreadPoolExecutor
+    try:
+        ncpu = len(os.sched_getaffinity(0))
+    except AttributeError:
+        ncpu = os.cpu_count() or 1
+    workers = max(1, min(len(angles), ncpu, 8))   # ~0.5 GB of temporaries per worker at 1600x1200
+    if workers == 1:
+        views = [one(i) for i in range(len(angles))]
+    else:
+        with ThreadPoolExecutor(workers) as ex:
+            views = list(ex.map(one, range(len(angles))))
     zmin = min(float(v["depth"][np.isfinite(v["depth"])].min()) for v in views)
     zmax = max(float(v["depth"][np.isfinite(v["depth"])].max()) for v in views)
     dmin, dmax = 0.75 * zmin, 1.25 * zmax

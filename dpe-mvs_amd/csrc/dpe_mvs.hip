@@ -67,12 +67,12 @@ struct DevArr {
   size_t n = 0;
   hipError_t ensure(size_t count) {
     if (count <= n && p) return hipSuccess;
-    if (p) { hipFree(p); p = nullptr; n = 0; }
+    if (p) { (void)hipFree(p); p = nullptr; n = 0; }
     hipError_t e = hipMalloc((void**)&p, count * sizeof(T) + 256);
     if (e == hipSuccess) n = count;
     return e;
   }
-  void release() { if (p) hipFree(p); p = nullptr; n = 0; }
+  void release() { if (p) (void)hipFree(p); p = nullptr; n = 0; }
 };
 
 }  // namespace
@@ -98,13 +98,16 @@ struct DpeContext {
   hipStream_t stream = nullptr;
   hipStream_t aux = nullptr;         // GenNeighbours beside the first strong half-sweep
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  hipEvent_t ev_done = nullptr;      // end of the last dpe_pm_execute's work on its stream
+  bool pending = false;              // ev_done recorded and not yet waited for
   bool staged = false;
   bool timing = false;
   bool counting = false;
   float timings[DPE_NUM_CLASSES + 1] = {0};
   int launches[DPE_NUM_CLASSES + 1] = {0};
   unsigned long long counts[DPE_NUM_CLASSES * 4] = {0};
-  hipEvent_t ev[2 * 64] = {};
+  std::vector<hipEvent_t> ev;        // timing: (start, end) per launch class slot
+  hipEvent_t ev_start = nullptr;     // timing: start of the pass
   DevArr<unsigned long long> cnt;
   DevArr<unsigned long long> phase;  // DPE_PHASE_PROF builds: per-phase cycle sums
   PassConst hc;                  // host copy of the pass constants
@@ -190,36 +193,52 @@ DpeContext* dpe_create(int device) {
   }
   if (hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreate(&c->ev_start) != hipSuccess) {
     g_err = "dpe_create: aux stream";
-    if (c->ev_join) hipEventDestroy(c->ev_join);
-    if (c->ev_fork) hipEventDestroy(c->ev_fork);
-    if (c->aux) hipStreamDestroy(c->aux);
-    hipStreamDestroy(c->stream);
+    if (c->ev_start) (void)hipEventDestroy(c->ev_start);
+    if (c->ev_done) (void)hipEventDestroy(c->ev_done);
+    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    if (c->aux) (void)hipStreamDestroy(c->aux);
+    (void)hipStreamDestroy(c->stream);
     delete c;
     return nullptr;
   }
-  for (auto& e : c->ev) hipEventCreate(&e);
   return c;
+}
+
+// Host-waits for the work of the last dpe_pm_execute, which may have been enqueued on a caller
+// stream: staging, fetching and freeing must not overwrite or release buffers that pass still uses.
+static hipError_t wait_pending(DpeContext* c) {
+  hipError_t e = hipSuccess;
+  if (c->pending) { e = hipEventSynchronize(c->ev_done); c->pending = false; }
+  return e;
 }
 
 void dpe_image_cache_clear(DpeContext* c) {
   if (!c) return;
-  hipSetDevice(c->device);
-  hipStreamSynchronize(c->stream);
+  (void)hipSetDevice(c->device);
+  (void)wait_pending(c);
+  (void)hipStreamSynchronize(c->stream);
   for (CachedImage* e : c->icache) { e->release(); delete e; }
   c->icache.clear();
 }
 
 void dpe_destroy(DpeContext* c) {
   if (!c) return;
-  hipSetDevice(c->device);
-  hipStreamSynchronize(c->stream);
+  (void)hipSetDevice(c->device);
+  (void)wait_pending(c);
+  (void)hipStreamSynchronize(c->stream);
+  (void)hipStreamSynchronize(c->aux);
   dpe_image_cache_clear(c);
   for (auto& a : c->fz_depth) a.release();
   for (auto& a : c->fz_normal) a.release();
   c->fz_views.release(); c->fz_cams.release(); c->fz_src.release(); c->fz_idx.release(); c->fz_val.release();
-  for (auto& e : c->ev) hipEventDestroy(e);
+  for (auto& e : c->ev) (void)hipEventDestroy(e);
+  (void)hipEventDestroy(c->ev_start);
+  (void)hipEventDestroy(c->ev_done);
   c->dc.release();
   for (int i = 0; i < DPE_MAX_IMAGES; ++i) { c->img_plain[i].release(); c->imgq[i].release(); c->depth[i].release(); }
   c->imgq8_all.release();
@@ -235,10 +254,10 @@ void dpe_destroy(DpeContext* c) {
   c->cnt.release();
   c->tab_right.release(); c->tab_down.release();
   c->lists.release(); c->row_counts.release(); c->list_totals.release();
-  hipStreamSynchronize(c->aux);
-  hipEventDestroy(c->ev_fork); hipEventDestroy(c->ev_join);
-  hipStreamDestroy(c->aux);
-  hipStreamDestroy(c->stream);
+  (void)hipStreamSynchronize(c->aux);
+  (void)hipEventDestroy(c->ev_fork); (void)hipEventDestroy(c->ev_join);
+  (void)hipStreamDestroy(c->aux);
+  (void)hipStreamDestroy(c->stream);
   delete c;
 }
 
@@ -316,6 +335,7 @@ extern "C" int dpe_pm_stage(DpeContext* c, const DpePassInput* in, const DpePass
   }
   if (P.use_label && !in->label) { g_err = "dpe_pm_stage: use_label needs label"; return DPE_ERR_ARG; }
   HIPC(hipSetDevice(c->device));
+  HIPC(wait_pending(c));   // an earlier execute on a caller stream may still read what is overwritten here
   const int W = in->width, H = in->height, N = in->num_images;
   const size_t L = (size_t)W * H;
   PassConst& pc = c->hc;
@@ -473,6 +493,8 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   if (!c->staged) { g_err = "dpe_pm_execute: call dpe_pm_stage first"; return DPE_ERR_STATE; }
   HIPC(hipSetDevice(c->device));
   hipStream_t s = stream_ ? (hipStream_t)stream_ : c->stream;
+  // a previous execute, possibly on another stream, still uses the working buffers this one resets
+  if (c->pending) HIPC(hipStreamWaitEvent(s, c->ev_done, 0));
   const PassConst& pc = c->hc;
   const PassConst* dpc = c->dc.p;
   const int W = pc.W, H = pc.H, nv = pc.N - 1;
@@ -492,21 +514,28 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
     HIPC(c->cnt.ensure(DPE_NUM_CLASSES * 4));
     HIPC(hipMemsetAsync(c->cnt.p, 0, DPE_NUM_CLASSES * 4 * sizeof(unsigned long long), s));
   }
-  // per-launch events: slot pairs (start, end) + class id
-  int nev = 0;
-  int ev_class[64];
+  // per-launch events: slot pairs (start, end) + class id; one slot per class section of the
+  // launch sequence (setup, init, 5 per iteration, filter, DepthToWeak, LocalRefine)
   const bool timing = c->timing;
+  const int max_slots = 5 + 5 * std::max(0, pc.P.max_iterations);
+  if (timing && (int)c->ev.size() < 2 * max_slots) {
+    const size_t have = c->ev.size();
+    c->ev.resize(2 * max_slots, nullptr);
+    for (size_t k = have; k < c->ev.size(); ++k) HIPC(hipEventCreate(&c->ev[k]));
+  }
+  int nev = 0;
+  std::vector<int> ev_class(timing ? max_slots : 0);
   for (int k = 0; k <= DPE_NUM_CLASSES; ++k) c->launches[k] = 0;
   auto begin = [&](int cls) -> DevBufs {
     DevBufs Bc = B;
     if (c->counting) Bc.cnt = c->cnt.p + 4 * cls;
     c->launches[cls]++;
-    if (timing && nev < 64) { ev_class[nev] = cls; hipEventRecord(c->ev[2 * nev], s); }
+    if (timing && nev < max_slots) { ev_class[nev] = cls; (void)hipEventRecord(c->ev[2 * nev], s); }
     return Bc;
   };
-  auto end = [&]() { if (timing && nev < 64) { hipEventRecord(c->ev[2 * nev + 1], s); nev++; } };
+  auto end = [&]() { if (timing && nev < max_slots) { (void)hipEventRecord(c->ev[2 * nev + 1], s); nev++; } };
 
-  if (timing) hipEventRecord(c->ev[2 * 64 - 2], s);
+  if (timing) (void)hipEventRecord(c->ev_start, s);
   // initial state (the reference uploads it in CudaSpaceInitialization, DPE.cpp:964-1015)
   HIPC(hipMemcpyAsync(B.planes, c->planes0.p, L * sizeof(float4), hipMemcpyDeviceToDevice, s));
   HIPC(hipMemcpyAsync(B.weak, c->weak0.p, L, hipMemcpyDeviceToDevice, s));
@@ -550,7 +579,8 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   // one stream (per-class events).
   // DPE_OVERLAP=0 keeps one stream (profiling runs whose per-kernel durations must not overlap)
   static const bool overlap_env = [] { const char* e = getenv("DPE_OVERLAP"); return !(e && atoi(e) == 0); }();
-  const bool overlap = overlap_env && !timing && !c->counting;
+  // (the join into `s` sits in the first strong half-sweep, so a pass without iterations keeps one stream)
+  const bool overlap = overlap_env && !timing && !c->counting && pc.P.max_iterations >= 1;
   hipStream_t a = overlap ? c->aux : s;
   if (overlap) {   // pre-GenNeighbours sweep lists (the colour-0 strong list is the one used)
     k_list_count<0><<<(pc.half_rows + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p);
@@ -648,10 +678,10 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
     HIPC(hipEventSynchronize(c->ev[2 * nev - 1]));
     for (int k = 0; k <= DPE_NUM_CLASSES; ++k) c->timings[k] = 0.0f;
     float ms = 0;
-    hipEventElapsedTime(&ms, c->ev[2 * 64 - 2], c->ev[2 * nev - 1]);
+    (void)hipEventElapsedTime(&ms, c->ev_start, c->ev[2 * nev - 1]);
     c->timings[0] = ms;
     for (int e = 0; e < nev; ++e) {
-      hipEventElapsedTime(&ms, c->ev[2 * e], c->ev[2 * e + 1]);
+      (void)hipEventElapsedTime(&ms, c->ev[2 * e], c->ev[2 * e + 1]);
       c->timings[1 + ev_class[e]] += ms;
     }
   }
@@ -672,6 +702,8 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
     HIPC(hipStreamSynchronize(s));
     for (int k = 0; k < DPE_NUM_CLASSES; ++k) c->counts[4 * k + 3] = (unsigned long long)c->launches[k];
   }
+  HIPC(hipEventRecord(c->ev_done, s));
+  c->pending = true;
   return DPE_OK;
 }
 
@@ -681,8 +713,8 @@ extern "C" int dpe_pm_fetch(DpeContext* c, const DpePassState* st) {
   if (!c->staged) { g_err = "dpe_pm_fetch: nothing staged"; return DPE_ERR_STATE; }
   HIPC(hipSetDevice(c->device));
   const size_t L = (size_t)c->hc.W * c->hc.H;
+  HIPC(wait_pending(c));
   HIPC(hipStreamSynchronize(c->stream));
-  HIPC(hipDeviceSynchronize());
   if (st->planes) HIPC(hipMemcpy(st->planes, c->bufs.planes, L * sizeof(float4), hipMemcpyDeviceToHost));
   if (st->weak_info) HIPC(hipMemcpy(st->weak_info, c->bufs.weak, L, hipMemcpyDeviceToHost));
   if (st->selected_views) HIPC(hipMemcpy(st->selected_views, c->bufs.sel, L * sizeof(uint32_t), hipMemcpyDeviceToHost));
@@ -711,6 +743,7 @@ extern "C" int dpe_pm_export_depth(DpeContext* c, float* dev_dst, void* stream_)
   if (!c->staged) { g_err = "dpe_pm_export_depth: nothing staged"; return DPE_ERR_STATE; }
   HIPC(hipSetDevice(c->device));
   hipStream_t s = stream_ ? (hipStream_t)stream_ : c->stream;
+  if (c->pending) HIPC(hipStreamWaitEvent(s, c->ev_done, 0));   // after the pass that writes the planes
   const size_t L = (size_t)c->hc.W * c->hc.H;
   k_export_depth<<<(unsigned)((L + 255) / 256), 256, 0, s>>>(c->bufs.planes, dev_dst, L);
   HIPC(hipGetLastError());

@@ -5,7 +5,8 @@
 // so the walk is order-dependent.  Everything except the masks is independent per (pixel, view):
 // the two projections, the reprojection error, the relative depth difference and the normal dot
 // product.  This kernel computes exactly that part, one thread per reference pixel, in the
-// reference's single-precision expression order (-ffp-contract=off, IEEE division and sqrt), and
+// reference's expression order and precision (-ffp-contract=off, IEEE division and sqrt; single
+// precision except the reprojection error, whose pow() promotes to double), and
 // the host finishes with the masks, the angle test (acosf), the weights (expf) and the colours in
 // the reference's serial order (host/fusion.cpp).
 #pragma once
@@ -89,7 +90,9 @@ __global__ void __launch_bounds__(256) k_fusion_candidates(const DpeCamera* __re
         float tx, ty, pd2;
         fz_project(Y, rc, tx, ty, pd2);
         const float dx = (float)c - tx, dy = (float)r - ty;
-        const float re = __builtin_sqrtf(dx * dx + dy * dy);
+        // DPE.cpp:1331 sqrt(pow(c - x, 2) + pow(r - y, 2)): pow(float, int) promotes to double, so the
+        // squares, the sum and the root are double, rounded to float once
+        const float re = (float)__builtin_sqrt((double)dx * dx + (double)dy * dy);
         const float rl = __builtin_fabsf(pd2 - ref_depth) / ref_depth;
         if (re < 2.0f && rl < 0.01f) {
           o = sp; e = re; rel = rl;

@@ -434,6 +434,8 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
         p.scale_size = (int)std::pow(2, round_num - 1 - i);
         p.params.scale_size = p.scale_size;
         pass_params(p.params, i, j);
+        if (opt.max_iterations > 0) p.params.max_iterations = opt.max_iterations;
+        if (opt.photometric_only) p.params.geom_consistency = false;
         if (!process_problem(p, cache, states, depth_src, opt, runner, err)) return 1;
         const ImageState& s = states[p.ref_image_id];
         depth_cur[p.ref_image_id] = DepthMap{s.w, s.h, s.depth};

@@ -64,6 +64,9 @@ typedef struct DpePipelineOptions {
   bool keep_intermediate;   /* also write depths.dmb / normals.dmb / weak.bin / selected_views.bin and
                                keep edges_<s>.dmb / labels_<s>.dmb (the reference deletes them) */
   dpe_fusion_fn fusion_runner; void* fusion_user;     /* NULL: the HIP kernel on gpu_index */
+  int max_iterations;       /* PatchMatch iterations per pass; 0 = the reference's 3 (main.cpp:527, 554) */
+  bool photometric_only;    /* geom_consistency = false on every pass (BASELINE config 2; the
+                               reference always runs its geometric passes, main.cpp:549) */
 } DpePipelineOptions;
 
 void dpe_pipeline_default_options(DpePipelineOptions* opt);

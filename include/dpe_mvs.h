@@ -148,13 +148,16 @@ void dpe_destroy(DpeContext* ctx);
 /* Last error message of the calling thread ("" if none). */
 const char* dpe_last_error(void);
 
-/* Uploads inputs and the initial state (H2D), builds the device layouts. Synchronous. */
+/* Uploads inputs and the initial state (H2D), builds the device layouts. Synchronous.  Waits first
+ * for the work of the previous dpe_pm_execute (on whatever stream it was enqueued), so stage(A);
+ * execute(A, s); stage(B) never overwrites inputs pass A still reads. */
 int dpe_pm_stage(DpeContext* ctx, const DpePassInput* in, const DpePassState* state);
 
 /*
  * Runs the whole pass (DPE.cu:3150-3226) on device-resident data on `stream` (a hipStream_t,
  * NULL = the context's stream).  Every call starts from the staged initial state, so repeated
- * calls are idempotent.  Asynchronous w.r.t. the host.  Part of the pass (GenNeighbours) runs on
+ * calls are idempotent.  Asynchronous w.r.t. the host; ordered after the previous execute (the stream
+ * waits on its completion event), and dpe_pm_stage / dpe_pm_fetch / dpe_destroy wait for it.  Part of the pass (GenNeighbours) runs on
  * the context's second stream, forked from and joined back into `stream` with events, so all
  * work is complete when `stream` reaches the end of the call's enqueued work (environment
  * DPE_OVERLAP=0, timing or counting keep everything on `stream`).

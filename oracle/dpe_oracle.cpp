@@ -43,6 +43,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <thread>
+#include <chrono>
 #include <vector>
 
 using namespace oracle;
@@ -1650,25 +1651,43 @@ static int RunPass(Pass& S) {
     S.gn_thr = (float)cos((double)(angle / 2.0f) * M_PI / 180.0f);
     S.gn_shift = MAXo(o_d2i(tan((double)(angle / 2.0f) * M_PI / 180.0f) * 20), 1);
   }
+  // ORACLE_PROFILE=1: wall time of each stage on stderr (where the checker's time goes)
+  static const bool prof = [] { const char* e = getenv("ORACLE_PROFILE"); return e && atoi(e) != 0; }();
+  auto t0 = std::chrono::steady_clock::now();
+  auto mark = [&](const char* what) {
+    if (!prof) return;
+    const auto t1 = std::chrono::steady_clock::now();
+    fprintf(stderr, "oracle %-16s %8.3f s\n", what, std::chrono::duration<double>(t1 - t0).count());
+    t0 = t1;
+  };
   // RunPatchMatch launch sequence (DPE.cu:3150-3226)
   Full(S, [&](int x, int y) { GenEdgeInform(S, x, y); });
   Full(S, [&](int x, int y) { FindNearestStrongPoint(S, x, y); });
+  mark("edge+nearest");
   Full(S, [&](int x, int y) { GenNeighbours(S, x, y); });
   Full(S, [&](int x, int y) { NeigbourUpdate(S, x, y); });
+  mark("gen_neighbours");
   Full(S, [&](int x, int y) { RandomInitialization(S, x, y); });
+  mark("init");
   for (int it = 0; it < S.P.max_iterations; ++it) {
     for (int colour = 0; colour < 2; ++colour) {
       S.planes_snap = S.planes; S.costs_snap = S.costs; S.sel_snap = S.sel;
       HalfSweep(S, colour, [&](int x, int y) { if (S.weak[x + y * S.W] != DPE_WEAK) PropagationStrong(S, x, y, it); });
     }
+    mark("strong");
     Full(S, [&](int x, int y) { RANSACFitPlane(S, x, y, it); });
+    mark("ransac");
     for (int colour = 0; colour < 2; ++colour)
       HalfSweep(S, colour, [&](int x, int y) { if (S.weak[x + y * S.W] == DPE_WEAK) PropagationWeak(S, x, y, it); });
+    mark("weak");
   }
   Full(S, [&](int x, int y) { GetDepthandNormal(S, x, y); });
   for (int colour = 0; colour < 2; ++colour) HalfSweep(S, colour, [&](int x, int y) { FilterStrong(S, x, y); });
+  mark("filter");
   Full(S, [&](int x, int y) { DepthToWeak(S, x, y); });
+  mark("depth_to_weak");
   Full(S, [&](int x, int y) { LocalRefine(S, x, y); });
+  mark("local_refine");
   return 0;
 }
 
@@ -1771,7 +1790,8 @@ int oracle_pass_runner(void* user, const DpePassInput* in, const DpePassState* s
 
 // ---- RunFusion (DPE.cpp:1220-1370) -----------------------------------------------------------
 // Restated as the reference writes it.  fz_* follow Get3DPointonWorld / ProjectCamera
-// (DPE.cpp:1170-1206) and GetAngle (:1208-1217) in single precision, expression order kept.
+// (DPE.cpp:1170-1206) and GetAngle (:1208-1217) in single precision, expression order kept; the
+// reprojection error's pow(float, int) (:1331) promotes to double.
 namespace {
 struct FzP { float x, y, z; };
 FzP fz_world(int x, int y, float depth, const DpeCamera& cam) {
@@ -1858,7 +1878,8 @@ int oracle_run_fusion(const OracleFusionView* views, int n, float* out, int cap)
           float tx, ty;
           fz_project(Y, R.cam, tx, ty, pd);
           const float dx = c - tx, dy = r - ty;
-          const float reproj_error = std::sqrt(dx * dx + dy * dy);
+          // sqrt(pow(c - x, 2) + pow(r - y, 2)) (DPE.cpp:1331): pow(float, int) promotes to double
+          const float reproj_error = (float)std::sqrt((double)dx * dx + (double)dy * dy);
           const float rel = std::fabs(pd - ref_depth) / ref_depth;
           const float* sn = S.normal + 3 * sc;
           const float dot = rn[0] * sn[0] + rn[1] * sn[1] + rn[2] * sn[2];
@@ -1923,7 +1944,7 @@ int oracle_fusion_candidates(void* /*user*/, const DpeFusionView* views, int n, 
         float tx, ty, pd2;
         fz_project(Y, R.cam, tx, ty, pd2);
         const float dx = c - tx, dy = r - ty;
-        const float re = std::sqrt(dx * dx + dy * dy);
+        const float re = (float)std::sqrt((double)dx * dx + (double)dy * dy);   // DPE.cpp:1331 (double pow)
         const float rl = std::fabs(pd2 - ref_depth) / ref_depth;
         if (re < 2.0f && rl < 0.01f) {
           idx[p * ns + j] = (int32_t)sp;

@@ -62,10 +62,22 @@ def lib():
     return _lib
 
 
+def host_threads() -> int:
+    """Host threads this process may use: OMP_NUM_THREADS when set (the GPU box sets it to its CPU
+    share), else the affinity mask."""
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    if env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
 def run_pass(pass_input: dict, state: dict, threads: int = 0) -> dict:
     """One PatchMatch pass on the CPU (same semantics as dpe_pm_run)."""
     if threads <= 0:
-        threads = os.cpu_count() or 1
+        threads = host_threads()
     b = _abi.PassBuffers(pass_input, state)
     rc = lib().oracle_pm_run(C.byref(b.inp), C.byref(b.st), int(threads))
     if rc != 0:
@@ -97,6 +109,21 @@ class OracleFusionView(C.Structure):
     _fields_ = [("width", C.c_int), ("height", C.c_int), ("cam", _abi.DpeCamera),
                 ("depth", C.c_void_p), ("normal", C.c_void_p), ("weak", C.c_void_p), ("bgr", C.c_void_p),
                 ("block", C.c_void_p), ("image_id", C.c_int), ("ns", C.c_int), ("src_ids", C.c_void_p)]
+
+
+def fusion_candidates(views, ref: int, src) -> tuple:
+    """oracle_fusion_candidates for views = [(depth, normal, DpeCamera)]: (idx int32 [L*ns], val f32 [L*ns*3])."""
+    from DPE_MVS.native import fusion_view_array
+    arr, keep = fusion_view_array(views)
+    s = np.ascontiguousarray(src, np.int32)
+    L = views[ref][0].size
+    idx, val = np.empty(L * len(s), np.int32), np.empty(L * len(s) * 3, np.float32)
+    f = lib().oracle_fusion_candidates
+    f.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+    f.restype = C.c_int
+    if f(None, arr, len(views), int(ref), s.ctypes.data, len(s), idx.ctypes.data, val.ctypes.data) != 0:
+        raise RuntimeError("oracle_fusion_candidates failed")
+    return idx, val
 
 
 def fusion_runner():

@@ -185,3 +185,31 @@ def test_image_ids_keep_images_resident(ctx):
     ref2 = ctx.run(dict(inp2, image_ids=None), synthetic.gt_state(other))
     got2 = ctx.run(inp2, synthetic.gt_state(other))
     assert ref2["planes"].tobytes() == got2["planes"].tobytes()
+
+
+def test_stage_waits_for_execute_on_a_foreign_stream(ctx):
+    """dpe_pm_stage host-waits for the previous execute even when it was enqueued on a caller stream:
+    stage(A); execute(A, s); stage(B) must not overwrite inputs pass A is still reading."""
+    import torch
+    sa, sb = synthetic.make_scene(160, 120, 5), synthetic.make_scene(160, 120, 5, seed=synthetic.SCENE_SEED + 9)
+    p = _params("refine_iter")
+    ia, sta = synthetic.pass_input(sa, p, depths=synthetic.src_depths(sa)), synthetic.gt_state(sa)
+    ib, stb = synthetic.pass_input(sb, p, depths=synthetic.src_depths(sb), seed=4), synthetic.gt_state(sb, seed=3)
+    want = ctx.run(ia, sta)
+    s = torch.cuda.Stream()
+    ctx.stage(ia, sta)
+    ctx.execute(s.cuda_stream)
+    ctx.stage(ib, stb)                  # returns only after pass A is done
+    got = ctx.fetch()                   # the working buffers still hold pass A's result
+    for k in want:
+        assert bits_equal(want[k], got[k]), k
+    torch.cuda.synchronize()
+
+
+def test_zero_iterations_joins_the_aux_stream(ctx):
+    # max_iterations = 0: no sweep joins the GenNeighbours stream, so the pass keeps one stream
+    sc = synthetic.make_scene(96, 72, 4)
+    p = _params("refine_iter", iters=0)
+    st = synthetic.gt_state(sc)
+    inp = synthetic.pass_input(sc, p, depths=synthetic.src_depths(sc))
+    assert_same(ctx.run(inp, st), oracle.run_pass(inp, st), "max_iterations 0")
