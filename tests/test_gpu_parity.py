@@ -189,21 +189,28 @@ def test_image_ids_keep_images_resident(ctx):
 
 def test_stage_waits_for_execute_on_a_foreign_stream(ctx):
     """dpe_pm_stage host-waits for the previous execute even when it was enqueued on a caller stream:
-    stage(A); execute(A, s); stage(B) must not overwrite inputs pass A is still reading."""
-    import torch
+    stage(A); execute(A, s); stage(B) must not overwrite inputs pass A is still reading.  The caller
+    stream comes from the HIP runtime the library itself links (torch's HIP runtime is a second copy
+    that cannot open the device once the library has)."""
+    import ctypes as C
+    hip = C.CDLL("libamdhip64.so.7", mode=C.RTLD_GLOBAL)
     sa, sb = synthetic.make_scene(160, 120, 5), synthetic.make_scene(160, 120, 5, seed=synthetic.SCENE_SEED + 9)
     p = _params("refine_iter")
     ia, sta = synthetic.pass_input(sa, p, depths=synthetic.src_depths(sa)), synthetic.gt_state(sa)
     ib, stb = synthetic.pass_input(sb, p, depths=synthetic.src_depths(sb), seed=4), synthetic.gt_state(sb, seed=3)
     want = ctx.run(ia, sta)
-    s = torch.cuda.Stream()
-    ctx.stage(ia, sta)
-    ctx.execute(s.cuda_stream)
-    ctx.stage(ib, stb)                  # returns only after pass A is done
-    got = ctx.fetch()                   # the working buffers still hold pass A's result
-    for k in want:
-        assert bits_equal(want[k], got[k]), k
-    torch.cuda.synchronize()
+    s = C.c_void_p()
+    assert hip.hipStreamCreateWithFlags(C.byref(s), 1) == 0          # hipStreamNonBlocking
+    try:
+        ctx.stage(ia, sta)
+        ctx.execute(s.value)
+        ctx.stage(ib, stb)                  # returns only after pass A is done
+        got = ctx.fetch()                   # the working buffers still hold pass A's result
+        for k in want:
+            assert bits_equal(want[k], got[k]), k
+    finally:
+        assert hip.hipStreamSynchronize(s) == 0
+        assert hip.hipStreamDestroy(s) == 0
 
 
 def test_zero_iterations_joins_the_aux_stream(ctx):
