@@ -420,8 +420,9 @@ DEV float tap_u8_fast(const DevBufs& B, uint32_t vofs, uint32_t stride, f2v lim,
 #ifndef DPE_TAP_PAIR
 #define DPE_TAP_PAIR 1
 #endif
+// `base` is the texel array the byte offsets index (tex_base of the layout; vofs selects the view).
 template <int T, bool IN = false>
-DEV f2v tap2_fast(const DevBufs& B, uint32_t vofs, uint32_t stride, f2v lim, const float* h, f2v bxy, float bz, f2v yf) {
+DEV f2v tap2_at(const uint8_t* base, uint32_t vofs, uint32_t stride, f2v lim, const float* h, f2v bxy, float bz, f2v yf) {
   const f2v qx = fma2(f2s(h[1]), yf, f2s(bxy.x));
   const f2v qy = fma2(f2s(h[4]), yf, f2s(bxy.y));
   const f2v qz = fma2(f2s(h[7]), yf, f2s(bz));
@@ -431,7 +432,6 @@ DEV f2v tap2_fast(const DevBufs& B, uint32_t vofs, uint32_t stride, f2v lim, con
   const uint32_t mx = (uint32_t)lim.x * 256u + 256u, my = (uint32_t)lim.y * 256u + 256u;
   const uint32_t ux0 = fixed_coord<IN>(sx.x, mx), ux1 = fixed_coord<IN>(sx.y, mx);
   const uint32_t uy0 = fixed_coord<IN>(sy.x, my), uy1 = fixed_coord<IN>(sy.y, my);
-  const uint8_t* base = tex_base<T>(B);
   const uint8_t* p0 = base + (vofs + (__umul24(uy0 >> 8, stride) + (ux0 >> 8)) * tex_bytes<T>());
   const uint8_t* p1 = base + (vofs + (__umul24(uy1 >> 8, stride) + (ux1 >> 8)) * tex_bytes<T>());
   const f2v ay = (f2v){(float)(uy0 & 255u), (float)(uy1 & 255u)} * f2s(0.00390625f);
@@ -440,6 +440,10 @@ DEV f2v tap2_fast(const DevBufs& B, uint32_t vofs, uint32_t stride, f2v lim, con
   texel_rows<T>(p1, (float)(ux1 & 255u), b0, b1);
   const f2v r0 = (f2v){a0, b0}, r1 = (f2v){a1, b1};
   return fma2(ay, r1 - r0, r0);
+}
+template <int T, bool IN = false>
+DEV f2v tap2_fast(const DevBufs& B, uint32_t vofs, uint32_t stride, f2v lim, const float* h, f2v bxy, float bz, f2v yf) {
+  return tap2_at<T, IN>(tex_base<T>(B), vofs, stride, lim, h, bxy, bz, yf);
 }
 
 template <int U8> DEV float sample_src(const DevBufs& B, int v, int W, int H, float sx, float sy) {

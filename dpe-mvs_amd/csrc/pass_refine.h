@@ -61,15 +61,14 @@ DEV void patch_lds_pre(const float* pw, float& p_inv, float& p_mref, float& p_va
   }
   ncc_pre(a_ref, a_rr, a_w, p_inv, p_mref, p_var);
 }
-// Old NCC with the patch read from LDS (same arithmetic as ncc_old_patch36)
-template <int U8, bool FAST, bool IN = false>
-DEV void lds_taps(const float* pw, int px, int py, const PassConst& pc, const DevBufs& B, int v, const Homog& H,
-                  float* acc) {
-  const int W = pc.W, Hh = pc.H;
-  if constexpr (U8 != TEX_F32 && FAST && DPE_PACKED_TAP) {
+// The 36 taps of the packed fast path on the texel array `base` (texel (tx, ty) of the view at byte
+// base + vofs + (ty * stride + tx) * texel bytes, 32-bit arithmetic).
+// Packed form: (r_src, r_rs) accumulate as one pair; weights are (w, w*grey) pairs in LDS; the two
+// taps of a row pair share each packed op (tap2_at).
+template <int U8, bool IN = false>
+DEV void taps36_at(const float* pw, int px, int py, f2v lim, const uint8_t* base, uint32_t vofs, uint32_t stride,
+                   const Homog& H, float* acc) {
     // packed form: (r_src, r_rs) accumulate as one pair; weights are (w, w*grey) pairs in LDS
-    const uint32_t vofs = (uint32_t)v * tex_view<U8>(B), stride = (uint32_t)(W + 2);
-    const f2v lim = (f2v){(float)W, (float)Hh};
     const f2v* wp = (const f2v*)pw;
     f2v s_sr = f2s(0.0f);
     float s_ss = 0;
@@ -88,11 +87,10 @@ DEV void lds_taps(const float* pw, int px, int py, const PassConst& pc, const De
       const float bz = __builtin_fmaf(H.h[6], x, H.h[8]);
       f2v r_sr = f2s(0.0f);
       float r_ss = 0;
-#if DPE_TAP_PAIR
 #pragma unroll
       for (int b = 0; b < 6; b += 2) {
-        const f2v sp = tap2_fast<U8, IN>(B, vofs, stride, lim, H.h, bxy, bz,
-                                     (f2v){(float)(py - 5 + 2 * b), (float)(py - 3 + 2 * b)});
+        const f2v sp = tap2_at<U8, IN>(base, vofs, stride, lim, H.h, bxy, bz,
+                                   (f2v){(float)(py - 5 + 2 * b), (float)(py - 3 + 2 * b)});
         const f2v w0 = wp[a * 6 + b], w1 = wp[a * 6 + b + 1];
         const f2v ws = (f2v){w0.x, w1.x} * sp;
         r_sr = fma2(w0, f2s(sp.x), r_sr);
@@ -100,19 +98,18 @@ DEV void lds_taps(const float* pw, int px, int py, const PassConst& pc, const De
         r_sr = fma2(w1, f2s(sp.y), r_sr);
         r_ss = __builtin_fmaf(ws.y, sp.y, r_ss);
       }
-#else
-#pragma unroll
-      for (int b = 0; b < 6; ++b) {
-        const float sp = tap_u8_fast<U8, IN>(B, vofs, stride, lim, H.h, bxy, bz, (float)(py - 5 + 2 * b));
-        const f2v w = wp[a * 6 + b];
-        r_sr = fma2(w, f2s(sp), r_sr);
-        const float ws = w.x * sp;
-        r_ss = __builtin_fmaf(ws, sp, r_ss);
-      }
-#endif
       s_sr += r_sr; s_ss += r_ss;
     }
     acc[0] = s_sr.x; acc[1] = s_ss; acc[2] = s_sr.y;
+}
+// Old NCC with the patch read from LDS (same arithmetic as ncc_old_patch36)
+template <int U8, bool FAST, bool IN = false>
+DEV void lds_taps(const float* pw, int px, int py, const PassConst& pc, const DevBufs& B, int v, const Homog& H,
+                  float* acc) {
+  const int W = pc.W, Hh = pc.H;
+  if constexpr (U8 != TEX_F32 && FAST && DPE_PACKED_TAP) {
+    taps36_at<U8, IN>(pw, px, py, (f2v){(float)W, (float)Hh}, tex_base<U8>(B), (uint32_t)v * tex_view<U8>(B),
+                      (uint32_t)(W + 2), H, acc);
   } else {
     float s_src = 0, s_ss = 0, s_rs = 0;
 #pragma unroll
@@ -250,6 +247,34 @@ DEV void baseline_and_weights(const PassConst& pc, uint32_t sel, const uint8_t* 
 }
 
 // ------------------------------------------------------------------------------ DepthToWeak
+// The classification of DPE.cu:2700-2745 from the 61-sample cost curve `pcs` and its local minima
+// `is_peak` (bit i = sample i): the reference's in-order scan over the peaks (non-peaks never update
+// it), then the single-peak / peak-variance rules.
+DEV uint8_t d2w_class(const PassConst& pc, const float* pcs, uint64_t is_peak) {
+  const int radius = 30;
+  const int peak_count = __popcll(is_peak);
+  int min_peak = 0;
+  float min_cost = 2.0f;
+  for (uint64_t m = is_peak; m; m &= m - 1) {
+    const int i = __builtin_ctzll(m);
+    if (pcs[i] < min_cost) { min_peak = i; min_cost = pcs[i]; }
+  }
+  uint8_t cls;
+  if (abs(min_peak - radius) > pc.P.weak_peak_radius || pcs[min_peak] > 0.5f) cls = DPE_WEAK;
+  else if (peak_count == 1) cls = pcs[min_peak] <= 0.15f ? DPE_STRONG : DPE_WEAK;
+  else {
+    float var = 0.0f;
+    for (uint64_t m = is_peak; m; m &= m - 1) {
+      const int i = __builtin_ctzll(m);
+      if (i != min_peak) { const float d = pcs[i] - min_cost; var += d * d; }
+    }
+    var = __builtin_sqrtf(var);
+    var /= (peak_count - 1);
+    cls = var > 0.2f ? DPE_STRONG : DPE_WEAK;
+  }
+  return cls;
+}
+
 // grid: one wave per pixel, 4 waves per 256-thread workgroup.
 template <int U8>
 __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_depth_to_weak(const PassConst* __restrict__ pcp, DevBufs B) {   // DPE.cu:2593-2747
@@ -323,28 +348,9 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_depth_to_weak(const Pass
   PHASE(4);
   PHASE_END(3);
   if (lane != 0) return;
-  const int peak_count = __popcll(is_peak);
-  int min_peak = 0;
-  float min_cost = 2.0f;
-  for (uint64_t m = is_peak; m; m &= m - 1) {
-    const int i = __builtin_ctzll(m);
-    if (pcs[i] < min_cost) { min_peak = i; min_cost = pcs[i]; }
-  }
-  uint8_t cls;
-  if (abs(min_peak - radius) > pc.P.weak_peak_radius || pcs[min_peak] > 0.5f) cls = DPE_WEAK;
-  else if (peak_count == 1) cls = pcs[min_peak] <= 0.15f ? DPE_STRONG : DPE_WEAK;
-  else {
-    float var = 0.0f;
-    for (uint64_t m = is_peak; m; m &= m - 1) {
-      const int i = __builtin_ctzll(m);
-      if (i != min_peak) { const float d = pcs[i] - min_cost; var += d * d; }
-    }
-    var = __builtin_sqrtf(var);
-    var /= (peak_count - 1);
-    cls = var > 0.2f ? DPE_STRONG : DPE_WEAK;
-  }
-  B.weak[center] = cls;
+  B.weak[center] = d2w_class(pc, pcs, is_peak);
 }
+
 
 // ------------------------------------------------------------------------------ LocalRefine
 // LocalRefine with a flat job pool: a wave owns 4 pixels; every (pixel, hypothesis, selected view)
