@@ -372,14 +372,46 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
     if (!ok) { err = "Images may error, check it! " + err; std::fprintf(stderr, "Images may error, check it!\n"); return 1; }
   }
   const int n = (int)problems.size();
+  // every rank reads the same pair.txt, so every rank takes this exit together (no collective yet)
+  if (world > n) { err = "world_size " + std::to_string(world) + " exceeds the " + std::to_string(n) + " problems"; return 1; }
   std::vector<std::vector<int>> blocks(world);
   for (int r = 0; r < world; ++r) for (int i = r * n / world; i < (r + 1) * n / world; ++i) blocks[r].push_back(i);
+  // Multi-rank failure handling: a rank whose own work fails keeps joining the collectives with a
+  // failure flag in its message, so every rank sees it at the same exchange and all return 1 together
+  // (an early return on one rank would leave the others blocked in the all-gather).
+  bool failed = false;
+  std::string first_err;
+  auto fail = [&](const std::string& e) { if (!failed) { failed = true; first_err = e; } };
+  // all-gather of `per` floats per rank plus one status float; false (err set) when any rank failed
+  auto exchange = [&](std::vector<float>& send, std::vector<float>& recv) -> bool {
+    const size_t per = send.size();
+    send.push_back(failed ? 1.0f : 0.0f);
+    recv.assign((per + 1) * world, 0.0f);
+    if (opt.allgather(opt.allgather_user, send.data(), per + 1, recv.data()) != 0) {
+      err = "all-gather failed";
+      return false;
+    }
+    send.pop_back();
+    std::vector<float> packed(per * world);
+    int bad = -1;
+    for (int r = 0; r < world; ++r) {
+      std::memcpy(packed.data() + (size_t)r * per, recv.data() + (size_t)r * (per + 1), per * sizeof(float));
+      if (bad < 0 && recv[(size_t)r * (per + 1) + per] != 0.0f) bad = r;
+    }
+    recv.swap(packed);
+    if (bad >= 0) {
+      err = bad == rank ? first_err : "rank " + std::to_string(bad) + " failed";
+      return false;
+    }
+    return true;
+  };
   Runner runner;
   if (opt.runner) { runner.fn = opt.runner; runner.user = opt.runner_user; }
   else {
     runner.ctx = dpe_create(opt.gpu_index);
-    if (!runner.ctx) { err = std::string("dpe_create: ") + dpe_last_error(); return 1; }
-    runner.fn = native_runner; runner.user = runner.ctx;
+    if (!runner.ctx) fail(std::string("dpe_create: ") + dpe_last_error());
+    else { runner.fn = native_runner; runner.user = runner.ctx; }
+    if (world == 1 && failed) { err = first_err; return 1; }
   }
   int w0, h0;
   cache.full(problems[0].ref_image_id, w0, h0, err);
@@ -397,7 +429,7 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
     for (size_t k = 0; k < blocks[rank].size(); ++k) {
       int fw, fh;
       const std::vector<float>* f = cache.full(problems[blocks[rank][k]].ref_image_id, fw, fh, err);
-      if (!f) return 1;
+      if (!f) return 1;   // decoded in CheckImages above: cannot fail here
       grey[k].w = fw; grey[k].h = fh;
       grey[k].px.resize(f->size());
       for (size_t q = 0; q < f->size(); ++q) grey[k].px[q] = (uint8_t)(*f)[q];
@@ -417,7 +449,8 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
         }
       });
     for (auto& th : pool) th.join();
-    for (auto& e : terr) if (!e.empty()) { err = e; return 1; }
+    for (auto& e : terr) if (!e.empty()) { fail(e); break; }
+    if (world == 1 && failed) return 1;
   }
   for (auto& p : problems) p.params.max_scale_size = std::max(1, (int)std::pow(2, round_num - 1));
   std::map<int, ImageState> states;
@@ -427,31 +460,35 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
     for (int j = -1; j < 3; ++j) {
       const std::map<int, DepthMap> snapshot = jacobi ? depth_cur : std::map<int, DepthMap>{};
       const auto& depth_src = jacobi ? snapshot : depth_cur;
-      int pw = 0, ph = 0;
+      // pass size: ImageCache::level's rounding of the first image (CheckImages: all the same size)
+      const int scale = (int)std::pow(2, round_num - 1 - i);
+      const int pw = scale == 1 ? w0 : std_round(w0 * (1.0f / (float)scale));
+      const int ph = scale == 1 ? h0 : std_round(h0 * (1.0f / (float)scale));
       for (int pi : blocks[rank]) {
+        if (failed) break;
         Problem& p = problems[pi];
         p.iteration = iteration_index;
-        p.scale_size = (int)std::pow(2, round_num - 1 - i);
+        p.scale_size = scale;
         p.params.scale_size = p.scale_size;
         pass_params(p.params, i, j);
         if (opt.max_iterations > 0) p.params.max_iterations = opt.max_iterations;
         if (opt.photometric_only) p.params.geom_consistency = false;
-        if (!process_problem(p, cache, states, depth_src, opt, runner, err)) return 1;
+        std::string perr;
+        if (!process_problem(p, cache, states, depth_src, opt, runner, perr)) { fail(perr); break; }
         const ImageState& s = states[p.ref_image_id];
         depth_cur[p.ref_image_id] = DepthMap{s.w, s.h, s.depth};
-        pw = s.w; ph = s.h;
       }
+      if (world == 1 && failed) { err = first_err; return 1; }
       if (world > 1) {   // all-gather of the depth maps (the pass's only cross-image data)
-        if (blocks[rank].empty()) { err = "empty rank block"; return 1; }
         size_t nmax = 0;
         for (auto& b : blocks) nmax = std::max(nmax, b.size());
         const size_t per = (size_t)pw * ph;
-        std::vector<float> send(nmax * per, 0.0f), recv(nmax * per * world);
-        for (size_t k = 0; k < blocks[rank].size(); ++k) {
+        std::vector<float> send(nmax * per, 0.0f), recv;
+        for (size_t k = 0; !failed && k < blocks[rank].size(); ++k) {
           const auto& d = depth_cur[problems[blocks[rank][k]].ref_image_id];
           std::memcpy(send.data() + k * per, d.d.data(), per * 4);
         }
-        if (opt.allgather(opt.allgather_user, send.data(), send.size(), recv.data()) != 0) { err = "all-gather failed"; return 1; }
+        if (!exchange(send, recv)) return 1;
         for (int r = 0; r < world; ++r)
           for (size_t k = 0; k < blocks[r].size(); ++k) {
             const float* src = recv.data() + ((size_t)r * nmax + k) * per;
@@ -464,8 +501,10 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
   }
   for (int pi : blocks[rank]) {
     const Problem& p = problems[pi];
-    if (!write_outputs(p, states[p.ref_image_id], opt, err)) return 1;
+    std::string werr;
+    if (!write_outputs(p, states[p.ref_image_id], opt, werr)) { fail(werr); break; }
   }
+  if (failed && !(world > 1 && opt.fusion)) { err = first_err; return 1; }   // else reported at the exchange
   if (opt.fusion) {   // RunFusion (main.cpp:578-580)
     std::map<int, ImageState> all;
     for (int pi : blocks[rank]) all[problems[pi].ref_image_id] = states[problems[pi].ref_image_id];
@@ -481,7 +520,7 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
         std::memcpy(o, st.normal.data(), per * 12);
         for (size_t i = 0; i < per; ++i) o[3 * per + i] = (float)st.weak[i];
       }
-      if (opt.allgather(opt.allgather_user, send.data(), send.size(), recv.data()) != 0) { err = "all-gather failed"; return 1; }
+      if (!exchange(send, recv)) return 1;
       for (int r = 0; r < world; ++r)
         for (size_t k = 0; k < blocks[r].size(); ++k) {
           const int id = problems[blocks[r][k]].ref_image_id;

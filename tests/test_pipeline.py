@@ -214,6 +214,56 @@ def test_two_rank_jacobi_matches_one_rank(tmp_path, dense4):
         assert a[k].dtype == b[k].dtype and a[k].tobytes() == b[k].tobytes(), k
 
 
+def _rank_fail_main(rank, world, port, folder, mode, q):
+    """One rank of a 2-rank run that must fail on every rank without hanging: `mode` "one_problem"
+    (world_size > problems) or "rank1_runner" (rank 1's pass runner fails in its third pass)."""
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    runner = oracle_runner()
+    keep = None
+    if mode == "rank1_runner" and rank == 1:
+        base = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p)(runner[0].value)
+        calls = [0]
+
+        def failing(user, inp, st):
+            calls[0] += 1
+            return -7 if calls[0] == 3 else base(user, inp, st)
+        keep = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p)(failing)
+        runner = (C.cast(keep, C.c_void_p).value, runner[1])
+    try:
+        pipeline.run_dpe_pipeline(folder, runner=runner, verbose=False, dist=dist)
+        q.put((rank, "returned 0"))
+    except pipeline.PipelineError as e:
+        q.put((rank, str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("mode", ["one_problem", "rank1_runner"])
+def test_multi_rank_failure_ends_every_rank(tmp_path, dense4, mode):
+    """A failure on one rank (or a world larger than the problem list) ends every rank with an error
+    at the same collective instead of leaving the others blocked in the all-gather."""
+    import torch.multiprocessing as mp
+    if mode == "one_problem":
+        d = str(tmp_path / "one")
+        synthetic.write_dense_folder(d, 64, 48, 1)
+    else:
+        d = _copy(dense4, tmp_path, "fail")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    mp.start_processes(_rank_fail_main, args=(2, _free_port(), d, mode, q), nprocs=2, join=True, start_method="spawn")
+    got = dict(q.get(timeout=10) for _ in range(2))
+    assert set(got) == {0, 1}
+    if mode == "one_problem":
+        assert all("exceeds" in m for m in got.values()), got
+    else:
+        assert "rank 1 failed" in got[0], got
+        assert "PatchMatch pass failed (-7)" in got[1], got
+
+
 def test_reference_schedule_reconstructs(tmp_path, dense4):
     d = _copy(dense4, tmp_path, "gs")
     assert pipeline.run_dpe_pipeline(d, runner=oracle_runner(), verbose=False) == 0
