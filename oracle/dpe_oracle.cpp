@@ -10,7 +10,9 @@
 // PARITY UNPINNED: the reference cannot be built here (needs nvcc, CUDA textures, cuRAND, OpenCV —
 // SURVEY.md §8c) and holds no tests, golden vectors or fixtures for this path, so
 // no reference output pins this restatement.  What pins it: the published Philox4x32-10 KATs
-// (Random123), per-function known-answer / invariant tests (tests/test_oracle_kat.py) and the
+// (Random123), per-function known-answer / invariant tests (tests/test_oracle_kat.py,
+// tests/test_oracle_functions.py: homography vs the literal float32 sequence, NCC-New, geometric
+// cost, median filter, DepthToWeak classes, GetDepthandNormal, LocalRefine) and the
 // self-generated golden fixtures that freeze it (tests/golden/).  See DESIGN.md §4.
 //
 // Deliberate, documented restatement choices:
@@ -1535,6 +1537,28 @@ static CostNow CostAndBaseline(Pass& S, int x, int y, const float4_& op, float o
   return r;
 }
 
+// DepthToWeak's classification (DPE.cu:2700-2745) of the 61-sample cost curve pc[pd + 30]
+static uint8_t ClassifyCostCurve(const float* pc, int weak_peak_radius) {
+  const int radius = 30, n = 2 * radius + 1;
+  bool is_peak[61];
+  for (int i = 0; i < n; ++i) is_peak[i] = false;
+  int peak_count = 0, min_peak = 0;
+  float min_cost = 2.0f;
+  for (int i = 2; i < n - 2; ++i) {
+    if (pc[i - 1] > pc[i] && pc[i + 1] > pc[i]) {
+      is_peak[i] = true; peak_count++;
+      if (pc[i] < min_cost) { min_peak = i; min_cost = pc[i]; }
+    }
+  }
+  if (abs(min_peak - radius) > weak_peak_radius || pc[min_peak] > 0.5f) return DPE_WEAK;
+  if (peak_count == 1) return pc[min_peak] <= 0.15f ? DPE_STRONG : DPE_WEAK;
+  float var = 0.0f;
+  for (int i = 2; i < n - 2; ++i) if (is_peak[i] && i != min_peak) { float d = pc[i] - min_cost; var += d * d; }
+  var = sqrtf(var);
+  var /= (peak_count - 1);
+  return var > 0.2f ? DPE_STRONG : DPE_WEAK;
+}
+
 // DepthToWeak (DPE.cu:2593-2747)
 static void DepthToWeak(Pass& S, int x, int y) {
   const int W = S.W, H = S.H;
@@ -1552,7 +1576,6 @@ static void DepthToWeak(Pass& S, int x, int y) {
   cn.base_line /= cn.valid;
   float disp = c0.K[0] * cn.base_line / od;
   const int radius = 30;
-  const int n = 2 * radius + 1;
   float pc[61];
   for (int pd = -radius; pd <= radius; pd += 1) {
     float p_depth = c0.K[0] * cn.base_line / (disp + (float)pd);
@@ -1572,23 +1595,20 @@ static void DepthToWeak(Pass& S, int x, int y) {
     p_cost /= cn.weight_normal;
     pc[pd + radius] = MINo(2.0f, p_cost);
   }
-  bool is_peak[61];
-  for (int i = 0; i < n; ++i) is_peak[i] = false;
-  int peak_count = 0, min_peak = 0;
-  float min_cost = 2.0f;
-  for (int i = 2; i < n - 2; ++i) {
-    if (pc[i - 1] > pc[i] && pc[i + 1] > pc[i]) {
-      is_peak[i] = true; peak_count++;
-      if (pc[i] < min_cost) { min_peak = i; min_cost = pc[i]; }
-    }
+  S.weak[center] = ClassifyCostCurve(pc, S.P.weak_peak_radius);
+}
+
+// LocalRefine's choice (DPE.cu:2796-2834): the in-range hypothesis of least cost in pd order (first
+// of equals), taken when it improves the current cost by more than 0.1 (compared in double).
+static bool LocalRefineSelect(const float* tc, const int* ok, const float* p_depth, float cost_now, float od,
+                              float* out_depth) {
+  float min_cost = 2.0f, best_depth = od;
+  for (int k = 0; k < 11; ++k) {
+    if (!ok[k]) continue;
+    if (tc[k] < min_cost) { min_cost = tc[k]; best_depth = p_depth[k]; }
   }
-  if (abs(min_peak - radius) > S.P.weak_peak_radius || pc[min_peak] > 0.5f) { S.weak[center] = DPE_WEAK; return; }
-  if (peak_count == 1) { S.weak[center] = pc[min_peak] <= 0.15f ? DPE_STRONG : DPE_WEAK; return; }
-  float var = 0.0f;
-  for (int i = 2; i < n - 2; ++i) if (is_peak[i] && i != min_peak) { float d = pc[i] - min_cost; var += d * d; }
-  var = sqrtf(var);
-  var /= (peak_count - 1);
-  S.weak[center] = var > 0.2f ? DPE_STRONG : DPE_WEAK;
+  *out_depth = best_depth;
+  return (double)(cost_now - min_cost) > 0.1;
 }
 
 // LocalRefine (DPE.cu:2749-2835)
@@ -1605,10 +1625,14 @@ static void LocalRefine(Pass& S, int x, int y) {
   cn.base_line /= cn.valid;
   float disp = c0.K[0] * cn.base_line / od;
   const int radius = 5;
-  float min_cost = 2.0f, best_depth = od;
+  float tcs[11], depths[11];
+  int ok[11];
   for (int pd = -radius; pd <= radius; ++pd) {
     float p_depth = c0.K[0] * cn.base_line / (disp + (float)pd);
-    if (p_depth < S.P.depth_min || p_depth > S.P.depth_max) continue;
+    depths[pd + radius] = p_depth;
+    ok[pd + radius] = !(p_depth < S.P.depth_min || p_depth > S.P.depth_max);
+    tcs[pd + radius] = 2.0f;
+    if (!ok[pd + radius]) continue;
     float4_ tp = op;
     tp.w = GetDistance2Origin(c0, x, y, p_depth, tp);
     float tc = 0.0f;
@@ -1620,9 +1644,10 @@ static void LocalRefine(Pass& S, int x, int y) {
       }
     }
     tc /= cn.weight_normal;
-    if (tc < min_cost) { min_cost = tc; best_depth = p_depth; }
+    tcs[pd + radius] = tc;
   }
-  if ((double)(cn.cost_now - min_cost) > 0.1) S.planes[center].w = best_depth;
+  float best_depth;
+  if (LocalRefineSelect(tcs, ok, depths, cn.cost_now, od, &best_depth)) S.planes[center].w = best_depth;
 }
 
 // half-sweep geometry (DPE.cu:1864-1938): Black = (x+y) even, Red = (x+y) odd.
@@ -1768,6 +1793,84 @@ float oracle_ncc_old(const DpePassInput* in, int x, int y, int view, const float
   ComputeViewConstants(S);
   float4_ p = {plane[0], plane[1], plane[2], plane[3]};
   return NCCOld(S, x, y, view, p);
+}
+// Pass S from the inputs of a per-function test (images, cameras, params, depths when geom)
+static void kat_pass(Pass& S, const DpePassInput* in) {
+  S.W = in->width; S.H = in->height; S.N = in->num_images; S.P = in->params;
+  const size_t L = (size_t)S.W * S.H;
+  S.cams.assign(in->cams, in->cams + S.N);
+  S.img.resize(S.N);
+  for (int i = 0; i < S.N; ++i) if (in->images && in->images[i]) S.img[i].assign(in->images[i], in->images[i] + L);
+  if (in->depths) {
+    S.dep.resize(S.N);
+    for (int i = 1; i < S.N; ++i) if (in->depths[i]) S.dep[i].assign(in->depths[i], in->depths[i] + L);
+  }
+  ComputeViewConstants(S);
+}
+// MakeHomography (restatement choice 3) of source view `view` for a reference-frame plane
+void oracle_homography(const DpePassInput* in, int view, const float plane[4], float H[9]) {
+  Pass S;
+  kat_pass(S, in);
+  const float4_ p = {plane[0], plane[1], plane[2], plane[3]};
+  const Homog h = MakeHomography(S, view, p);
+  for (int k = 0; k < 9; ++k) H[k] = h.h[k];
+}
+void oracle_project(const float H[9], float x, float y, float out[2]) {
+  Homog h;
+  for (int k = 0; k < 9; ++k) h.h[k] = H[k];
+  const float2_ r = Project(h, x, y);
+  out[0] = r.x; out[1] = r.y;
+}
+// ComputeBilateralNCCNew of (x, y) with the given pixel states, view masks, deformable neighbours
+// (short2 [L][9]) and radius map
+float oracle_ncc_new(const DpePassInput* in, const uint8_t* weak, const uint32_t* sel, const int16_t* neighbours,
+                     const int32_t* radius, int x, int y, int view, const float plane[4]) {
+  Pass S;
+  kat_pass(S, in);
+  const size_t L = (size_t)S.W * S.H;
+  S.weak.assign(weak, weak + L);
+  S.sel.assign(sel, sel + L);
+  S.neighbours.resize(L * 9);
+  std::memcpy(S.neighbours.data(), neighbours, L * 9 * sizeof(short2_));
+  S.radius.assign(L, 0);
+  if (radius) S.radius.assign(radius, radius + L);
+  const float4_ p = {plane[0], plane[1], plane[2], plane[3]};
+  return NCCNew(S, x, y, view, p);
+}
+// ComputeGeomConsistencyCost of (x, y) against the source depth map of `view`
+float oracle_geom_cost(const DpePassInput* in, int x, int y, int view, const float plane[4]) {
+  Pass S;
+  kat_pass(S, in);
+  const float4_ p = {plane[0], plane[1], plane[2], plane[3]};
+  return GeomCost(S, x, y, view, p);
+}
+// CheckerboardFilterStrong at (x, y): the resulting depth (.w) of the pixel
+float oracle_filter_strong(int W, int H, const float* planes, const uint8_t* weak, const float* costs, int x, int y) {
+  Pass S;
+  S.W = W; S.H = H;
+  const size_t L = (size_t)W * H;
+  S.planes.resize(L);
+  std::memcpy(S.planes.data(), planes, L * sizeof(float4_));
+  S.weak.assign(weak, weak + L);
+  S.costs.assign(costs, costs + L);
+  FilterStrong(S, x, y);
+  return S.planes[(size_t)y * W + x].w;
+}
+int oracle_d2w_class(const float pc[61], int weak_peak_radius) { return ClassifyCostCurve(pc, weak_peak_radius); }
+// GetDepthandNormal of one pixel: out = (world normal, depth)
+void oracle_depth_normal(const DpeCamera* cam, const float plane[4], int x, int y, float out[4]) {
+  Pass S;
+  S.W = x + 1; S.H = y + 1;
+  S.cams.assign(cam, cam + 1);
+  S.planes.assign((size_t)S.W * S.H, {0, 0, 0, 0});
+  S.planes[(size_t)y * S.W + x] = {plane[0], plane[1], plane[2], plane[3]};
+  GetDepthandNormal(S, x, y);
+  const float4_ r = S.planes[(size_t)y * S.W + x];
+  out[0] = r.x; out[1] = r.y; out[2] = r.z; out[3] = r.w;
+}
+int oracle_local_refine_select(const float tc[11], const int ok[11], const float p_depth[11], float cost_now, float od,
+                               float* out_depth) {
+  return LocalRefineSelect(tc, ok, p_depth, cost_now, od, out_depth) ? 1 : 0;
 }
 float oracle_expf(float x) { return o_expf(x); }
 float oracle_sinf(float x) { return o_sinf(x); }

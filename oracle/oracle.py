@@ -5,7 +5,7 @@ The product path never imports this module.
 
 Parity status: the reference (CUDA + cuRAND + textures + OpenCV, --use_fast_math) cannot be built
 or run in this image and ships no tests or golden vectors, so the restatement
-is pinned by per-function known-answer tests (tests/test_oracle_kat.py) and the committed golden
+is pinned by per-function known-answer tests (tests/test_oracle_kat.py, tests/test_oracle_functions.py) and the committed golden
 fixtures it produced (tests/golden/) rather than by reference outputs: PARITY VS THE CUDA BINARY IS
 UNPINNED; parity of the HIP path is bit-exact against this restatement.
 """
@@ -49,6 +49,25 @@ def _load():
     lib.oracle_philox.restype = None
     lib.oracle_sample.argtypes = [C.POINTER(C.c_float), C.c_int, C.c_int, C.c_float, C.c_float]
     lib.oracle_sample.restype = C.c_float
+    P = C.POINTER
+    inp = P(_abi.DpePassInput)
+    lib.oracle_homography.argtypes = [inp, C.c_int, P(C.c_float), P(C.c_float)]
+    lib.oracle_homography.restype = None
+    lib.oracle_project.argtypes = [P(C.c_float), C.c_float, C.c_float, P(C.c_float)]
+    lib.oracle_project.restype = None
+    lib.oracle_ncc_new.argtypes = [inp, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
+                                   P(C.c_float)]
+    lib.oracle_ncc_new.restype = C.c_float
+    lib.oracle_geom_cost.argtypes = [inp, C.c_int, C.c_int, C.c_int, P(C.c_float)]
+    lib.oracle_geom_cost.restype = C.c_float
+    lib.oracle_filter_strong.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int]
+    lib.oracle_filter_strong.restype = C.c_float
+    lib.oracle_d2w_class.argtypes = [P(C.c_float), C.c_int]
+    lib.oracle_d2w_class.restype = C.c_int
+    lib.oracle_depth_normal.argtypes = [P(_abi.DpeCamera), P(C.c_float), C.c_int, C.c_int, P(C.c_float)]
+    lib.oracle_depth_normal.restype = None
+    lib.oracle_local_refine_select.argtypes = [P(C.c_float), P(C.c_int), P(C.c_float), C.c_float, C.c_float, P(C.c_float)]
+    lib.oracle_local_refine_select.restype = C.c_int
     return lib
 
 
@@ -91,6 +110,76 @@ def ncc_old(pass_input: dict, x: int, y: int, view: int, plane) -> float:
                                       "sel": np.zeros(pass_input["images"][0].shape, np.uint32)})
     pl = (C.c_float * 4)(*[float(v) for v in plane])
     return float(lib().oracle_ncc_old(C.byref(b.inp), x, y, view, pl))
+
+
+# ---- per-function entry points (tests/test_oracle_functions.py) ---------------------------------
+def _kat_buffers(pass_input: dict) -> _abi.PassBuffers:
+    h, w = pass_input["images"][0].shape
+    return _abi.PassBuffers(pass_input, {"planes": np.zeros((h * w, 4), np.float32), "weak": np.zeros((h, w), np.uint8),
+                                         "sel": np.zeros((h, w), np.uint32)})
+
+
+def _f4(v):
+    return (C.c_float * len(v))(*[float(x) for x in v])
+
+
+def homography(pass_input: dict, view: int, plane) -> np.ndarray:
+    """The restatement's homography of source `view` for a reference-frame plane (n, w): 9 floats."""
+    b = _kat_buffers(pass_input)
+    out = (C.c_float * 9)()
+    lib().oracle_homography(C.byref(b.inp), view, _f4(plane), out)
+    return np.array(out[:], np.float32)
+
+
+def project(H, x: float, y: float) -> tuple:
+    out = (C.c_float * 2)()
+    lib().oracle_project(_f4(H), x, y, out)
+    return out[0], out[1]
+
+
+def ncc_new(pass_input: dict, weak, sel, neighbours, radius, x: int, y: int, view: int, plane) -> float:
+    """ComputeBilateralNCCNew with the given weak [H,W] u8, sel [H,W] u32, neighbours [H,W,9,2] i16
+    ((-1, -1) = none) and radius [H,W] i32 (or None)."""
+    b = _kat_buffers(pass_input)
+    wk = np.ascontiguousarray(weak, np.uint8)
+    sl = np.ascontiguousarray(sel, np.uint32)
+    nb = np.ascontiguousarray(neighbours, np.int16)
+    rd = None if radius is None else np.ascontiguousarray(radius, np.int32)
+    return float(lib().oracle_ncc_new(C.byref(b.inp), wk.ctypes.data, sl.ctypes.data, nb.ctypes.data,
+                                      None if rd is None else rd.ctypes.data, x, y, view, _f4(plane)))
+
+
+def geom_cost(pass_input: dict, x: int, y: int, view: int, plane) -> float:
+    b = _kat_buffers(pass_input)
+    return float(lib().oracle_geom_cost(C.byref(b.inp), x, y, view, _f4(plane)))
+
+
+def filter_strong(planes, weak, costs, x: int, y: int) -> float:
+    """CheckerboardFilterStrong at (x, y) over planes [H,W,4], weak [H,W], costs [H,W]: the new depth."""
+    pl = np.ascontiguousarray(planes, np.float32)
+    wk = np.ascontiguousarray(weak, np.uint8)
+    co = np.ascontiguousarray(costs, np.float32)
+    H, W = wk.shape
+    return float(lib().oracle_filter_strong(W, H, pl.ctypes.data, wk.ctypes.data, co.ctypes.data, x, y))
+
+
+def d2w_class(curve, weak_peak_radius: int) -> int:
+    c = np.ascontiguousarray(curve, np.float32)
+    assert c.size == 61
+    return int(lib().oracle_d2w_class(c.ctypes.data_as(C.POINTER(C.c_float)), weak_peak_radius))
+
+
+def depth_normal(cam, plane, x: int, y: int) -> np.ndarray:
+    out = (C.c_float * 4)()
+    lib().oracle_depth_normal(C.byref(cam), _f4(plane), x, y, out)
+    return np.array(out[:], np.float32)
+
+
+def local_refine_select(tc, ok, depths, cost_now: float, od: float) -> tuple:
+    d = C.c_float()
+    okv = (C.c_int * 11)(*[int(bool(v)) for v in ok])
+    r = lib().oracle_local_refine_select(_f4(tc), okv, _f4(depths), cost_now, od, C.byref(d))
+    return bool(r), d.value
 
 
 def philox(ctr, key) -> list:
