@@ -29,9 +29,12 @@ static const int kDefaultXcdRows = 1;
 #endif
 static constexpr int kWeakLanes = DPE_WEAK_LANES;   // lanes per weak pixel in k_weak_coop (16 or 32)
 // source-image layout of each kernel for 8-bit grey-level images (pass_common.h TEX_*): TEX_F16
-// issues fewer VALU ops per tap, TEX_U8 touches half the bytes (better for scattered gathers)
+// issues fewer VALU ops per tap, TEX_U8 touches half the bytes (better for scattered gathers),
+// TEX_P16 is in between (half the bytes, 2 more ops per tap than TEX_F16, one unaligned 8-B load).
+// A/B on the bench pass (two runs): P16 strong -0.85 / -0.32 ms; DepthToWeak -0.9 / +0.9 (noise),
+// LocalRefine +0.2 / -0.2, weak +3 (the 8-B unaligned gathers of its scattered patches cost more)
 #ifndef DPE_TEX_STRONG
-#define DPE_TEX_STRONG TEX_F16
+#define DPE_TEX_STRONG TEX_P16
 #endif
 #ifndef DPE_TEX_WEAK
 #define DPE_TEX_WEAK TEX_U8
@@ -85,10 +88,11 @@ struct CachedImage {
   DevArr<float> plain;
   DevArr<uint32_t> q8;      // TEX_U8 quad texels (8-bit images)
   DevArr<uint2> q16;        // TEX_F16 quad texels (8-bit images)
+  DevArr<uint32_t> qp;      // TEX_P16 column pairs (8-bit images)
   DevArr<float4> qf;        // f32 quad texels (built on demand)
   uint64_t last_use = 0;
-  size_t bytes() const { return plain.n * 4 + q8.n * 4 + q16.n * 8 + qf.n * 16; }
-  void release() { plain.release(); q8.release(); q16.release(); qf.release(); }
+  size_t bytes() const { return plain.n * 4 + q8.n * 4 + q16.n * 8 + qp.n * 4 + qf.n * 16; }
+  void release() { plain.release(); q8.release(); q16.release(); qp.release(); qf.release(); }
 };
 
 struct DpeContext {
@@ -117,6 +121,7 @@ struct DpeContext {
   DevArr<float4> imgq[DPE_MAX_IMAGES];
   DevArr<uint32_t> imgq8_all;        // all 8-bit quad images, TEX_U8 layout, one allocation
   DevArr<uint2> imgq16_all;          //   and TEX_F16 layout (32-bit tap offsets)
+  DevArr<uint32_t> imgqp_all;        //   and TEX_P16 column pairs
   bool img8 = false;                 // all images are 8-bit grey levels -> u8 quad layout
   DevArr<float> depth[DPE_MAX_IMAGES];
   DevArr<uint8_t> edge, edge_low;
@@ -243,6 +248,7 @@ void dpe_destroy(DpeContext* c) {
   for (int i = 0; i < DPE_MAX_IMAGES; ++i) { c->img_plain[i].release(); c->imgq[i].release(); c->depth[i].release(); }
   c->imgq8_all.release();
   c->imgq16_all.release();
+  c->imgqp_all.release();
   c->edge.release(); c->edge_low.release(); c->label.release();
   c->planes0.release(); c->weak0.release(); c->sel0.release();
   c->planes.release(); c->planes_snap.release(); c->fit_plane.release();
@@ -362,6 +368,8 @@ extern "C" int dpe_pm_stage(DpeContext* c, const DpePassInput* in, const DpePass
     return true;
   };
   const size_t plane = (size_t)(W + 2) * (H + 2);
+  const size_t pplane = (size_t)(W + 3) * (H + 2);        // TEX_P16
+  const dim3 pg((W + 3 + 15) / 16, (H + 2 + 15) / 16);
   if (in->image_ids) {   // device-resident images: upload and build layouts once per (id, size)
     CachedImage* ent[DPE_MAX_IMAGES];
     for (int i = 0; i < N; ++i) {
@@ -385,8 +393,9 @@ extern "C" int dpe_pm_stage(DpeContext* c, const DpePassInput* in, const DpePass
         HIPC(e->plain.ensure(L));
         HIPC(hipMemcpyAsync(e->plain.p, in->images[i], L * sizeof(float), hipMemcpyHostToDevice, c->stream));
         if (e->is8) {
-          HIPC(e->q8.ensure(plane)); HIPC(e->q16.ensure(plane));
+          HIPC(e->q8.ensure(plane)); HIPC(e->q16.ensure(plane)); HIPC(e->qp.ensure(pplane));
           k_build_quad8<<<qg, qb, 0, c->stream>>>(e->plain.p, e->q8.p, e->q16.p, W, H);
+          k_build_pair16<<<pg, qb, 0, c->stream>>>(e->plain.p, e->qp.p, W, H);
           HIPC(hipGetLastError());
         }
       }
@@ -399,12 +408,15 @@ extern "C" int dpe_pm_stage(DpeContext* c, const DpePassInput* in, const DpePass
     if (img8) {
       HIPC(c->imgq8_all.ensure(plane * N));
       HIPC(c->imgq16_all.ensure(plane * N));
+      HIPC(c->imgqp_all.ensure(pplane * N));
       for (int i = 0; i < N; ++i) {   // the per-pass views in one allocation (32-bit tap offsets)
         HIPC(hipMemcpyAsync(c->imgq8_all.p + plane * i, ent[i]->q8.p, plane * 4, hipMemcpyDeviceToDevice, c->stream));
         HIPC(hipMemcpyAsync(c->imgq16_all.p + plane * i, ent[i]->q16.p, plane * 8, hipMemcpyDeviceToDevice, c->stream));
+        HIPC(hipMemcpyAsync(c->imgqp_all.p + pplane * i, ent[i]->qp.p, pplane * 4, hipMemcpyDeviceToDevice, c->stream));
       }
       B.img8 = (const uint8_t*)c->imgq8_all.p; B.img8_view = (uint32_t)(plane * 4);
       B.img16 = (const uint8_t*)c->imgq16_all.p; B.img16_view = (uint32_t)(plane * 8);
+      B.imgp = (const uint8_t*)c->imgqp_all.p; B.imgp_view = (uint32_t)(pplane * 4);
     } else {
       for (int i = 0; i < N; ++i) {
         if (!ent[i]->qf.p) {
@@ -427,12 +439,16 @@ extern "C" int dpe_pm_stage(DpeContext* c, const DpePassInput* in, const DpePass
     if (img8) {
       HIPC(c->imgq8_all.ensure(plane * N));
       HIPC(c->imgq16_all.ensure(plane * N));
+      HIPC(c->imgqp_all.ensure(pplane * N));
       k_build_quad8<<<qg, qb, 0, c->stream>>>(c->img_plain[i].p, c->imgq8_all.p + plane * i,
                                               c->imgq16_all.p + plane * i, W, H);
+      k_build_pair16<<<pg, qb, 0, c->stream>>>(c->img_plain[i].p, c->imgqp_all.p + pplane * i, W, H);
       B.img8 = (const uint8_t*)c->imgq8_all.p;
       B.img8_view = (uint32_t)(plane * 4);
       B.img16 = (const uint8_t*)c->imgq16_all.p;
       B.img16_view = (uint32_t)(plane * 8);
+      B.imgp = (const uint8_t*)c->imgqp_all.p;
+      B.imgp_view = (uint32_t)(pplane * 4);
     } else {
       HIPC(c->imgq[i].ensure((size_t)(W + 2) * (H + 2)));
       k_build_quad<<<qg, qb, 0, c->stream>>>(c->img_plain[i].p, c->imgq[i].p, W, H);

@@ -40,6 +40,7 @@ struct DevBufs {
   // all views in one allocation, view v at byte offset v * view bytes (< 4 GiB: 32-bit offsets)
   const uint8_t* img8; uint32_t img8_view;
   const uint8_t* img16; uint32_t img16_view;
+  const uint8_t* imgp; uint32_t imgp_view;   // TEX_P16 column pairs, row stride W + 3
   const float* depth[DPE_MAX_IMAGES];
   const float* ref;
   float4* planes; float4* planes_snap; float4* fit_plane;
@@ -305,15 +306,33 @@ DEV float sample_quad(const float4* __restrict__ q, int W, int H, float sx, floa
 //     fx equals the reference's fma(fx/256, b-a, a) bit for bit (the products are the same real
 //     number), and each row interpolation is one v_fma_mix_f32 on the loaded halves: 7 fewer
 //     VALU ops per tap than TEX_U8 for twice the bytes.
-enum { TEX_F32 = 0, TEX_U8 = 1, TEX_F16 = 2 };
+//   TEX_P16: 4 B column pairs, f16 (g(X-1, Y-1), g(X-1, Y)) at (X, Y), row stride W + 3: the quad
+//     texel (X, Y) is the 8 B at pair X (a, c) and pair X+1 (b, d), read with one unaligned 8-B
+//     load; the row differences are one packed f16 subtraction (exact: integers <= 255), so each row
+//     interpolation is again one v_fma_mix_f32, now with fx/256 (exact) times (b-a): 2 more VALU ops
+//     per tap than TEX_F16 for half the footprint (and a layout whose windows copy as plain rows).
+enum { TEX_F32 = 0, TEX_U8 = 1, TEX_F16 = 2, TEX_P16 = 3 };
 typedef _Float16 h2v __attribute__((ext_vector_type(2)));
-template <int T> DEV const uint8_t* tex_base(const DevBufs& B) { return T == TEX_F16 ? B.img16 : B.img8; }
-template <int T> DEV uint32_t tex_view(const DevBufs& B) { return T == TEX_F16 ? B.img16_view : B.img8_view; }
+typedef uint2 uint2_a4 __attribute__((aligned(4)));
+template <int T> DEV const uint8_t* tex_base(const DevBufs& B) {
+  return T == TEX_F16 ? B.img16 : (T == TEX_P16 ? B.imgp : B.img8);
+}
+template <int T> DEV uint32_t tex_view(const DevBufs& B) {
+  return T == TEX_F16 ? B.img16_view : (T == TEX_P16 ? B.imgp_view : B.img8_view);
+}
 template <int T> constexpr uint32_t tex_bytes() { return T == TEX_F16 ? 8u : 4u; }
+template <int T> DEV uint32_t tex_stride(int W) { return (uint32_t)(W + (T == TEX_P16 ? 3 : 2)); }
 // the two row interpolations (r0 at y0, r1 at y1) of the texel at `p` for the raw x fraction fx
 template <int T>
 DEV void texel_rows(const uint8_t* p, float fx, float& r0, float& r1) {
-  if constexpr (T == TEX_F16) {
+  if constexpr (T == TEX_P16) {
+    const uint2 t = *(const uint2_a4*)p;                 // (a, c), (b, d)
+    const h2v df = __builtin_bit_cast(h2v, t.y) - __builtin_bit_cast(h2v, t.x);
+    const uint32_t d = __builtin_bit_cast(uint32_t, df);
+    const float ax = fx * 0.00390625f;
+    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(r0) : "v"(ax), "v"(d), "v"(t.x));
+    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[0,1,1] op_sel_hi:[0,1,1]" : "=v"(r1) : "v"(ax), "v"(d), "v"(t.x));
+  } else if constexpr (T == TEX_F16) {
     // v_fma_mix_f32 is fma(fx, (float)half, (float)half) with one rounding; the compiler only forms
     // it under f32 denormal flushing, which cannot matter here (|fx*d| >= 2^-8 or 0, a integer)
     const uint2 t = *(const uint2*)p;
@@ -337,7 +356,7 @@ DEV float sample_quad8(const uint8_t* __restrict__ q, int W, int H, float sx, fl
   const int uy = (int)__builtin_fmaf(yb, 256.0f, 256.5f);
   const float ay = (float)(uy & 255) * 0.00390625f;
   float r0, r1;
-  texel_rows<T>(q + (size_t)((uy >> 8) * (W + 2) + (ux >> 8)) * tex_bytes<T>(), (float)(ux & 255), r0, r1);
+  texel_rows<T>(q + (size_t)((uy >> 8) * tex_stride<T>(W) + (ux >> 8)) * tex_bytes<T>(), (float)(ux & 255), r0, r1);
   return __builtin_fmaf(ay, r1 - r0, r0);
 }
 // Minimum waves per SIMD the tap-heavy kernels are compiled for (register cap 512 / waves).
@@ -400,7 +419,7 @@ DEV float tap_u8_fast(const DevBufs& B, uint32_t vofs, uint32_t stride, f2v lim,
 #endif
   const uint8_t* p = tex_base<T>(B) + (vofs + (__umul24(uy >> 8, stride) + (ux >> 8)) * tex_bytes<T>());
   const float ay = (float)(uy & 255u) * 0.00390625f;
-  if constexpr (T == TEX_F16) {
+  if constexpr (T == TEX_F16 || T == TEX_P16) {
     float r0, r1;
     texel_rows<T>(p, (float)(ux & 255u), r0, r1);
     return __builtin_fmaf(ay, r1 - r0, r0);
@@ -417,6 +436,9 @@ DEV float tap_u8_fast(const DevBufs& B, uint32_t vofs, uint32_t stride, f2v lim,
 // Two taps of one patch row (columns yf.x, yf.y) with the projection, reciprocal refinement and
 // the vertical interpolation packed across the two taps; per element the same operations as
 // tap_u8_fast, so each result is bit-identical to it.
+#ifndef DPE_EXP_CHEAP
+#define DPE_EXP_CHEAP 0
+#endif
 #ifndef DPE_TAP_PAIR
 #define DPE_TAP_PAIR 1
 #endif
@@ -427,7 +449,11 @@ DEV f2v tap2_at(const uint8_t* base, uint32_t vofs, uint32_t stride, f2v lim, co
   const f2v qy = fma2(f2s(h[4]), yf, f2s(bxy.y));
   const f2v qz = fma2(f2s(h[7]), yf, f2s(bz));
   const f2v r = (f2v){__builtin_amdgcn_rcpf(qz.x), __builtin_amdgcn_rcpf(qz.y)};
+#if DPE_EXP_CHEAP   // timing experiment only (not bit-exact): no Newton step
+  const f2v iz = r;
+#else
   const f2v iz = fma2(fma2(-qz, r, f2s(1.0f)), r, r);
+#endif
   const f2v sx = qx * iz, sy = qy * iz;
   const uint32_t mx = (uint32_t)lim.x * 256u + 256u, my = (uint32_t)lim.y * 256u + 256u;
   const uint32_t ux0 = fixed_coord<IN>(sx.x, mx), ux1 = fixed_coord<IN>(sx.y, mx);

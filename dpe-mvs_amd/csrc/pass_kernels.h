@@ -743,6 +743,16 @@ __global__ void k_build_quad8(const float* __restrict__ img, uint32_t* __restric
   const h2v df = (h2v){(_Float16)((b - a) * 0.00390625f), (_Float16)((d - c) * 0.00390625f)};
   q16[o] = make_uint2(__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, df));
 }
+// TEX_P16 column pairs (pass_common.h): (g(X-1, Y-1), g(X-1, Y)) as f16, X in [0, W+2], Y in [0, H+1]
+__global__ void k_build_pair16(const float* __restrict__ img, uint32_t* __restrict__ qp, int W, int H) {
+  const int X = blockIdx.x * blockDim.x + threadIdx.x;
+  const int Y = blockIdx.y * blockDim.y + threadIdx.y;
+  if (X > W + 2 || Y > H + 1) return;
+  auto cl = [](int v, int n) { return v < 0 ? 0 : (v > n - 1 ? n - 1 : v); };
+  const int x0 = cl(X - 1, W), y0 = cl(Y - 1, H), y1 = cl(Y, H);
+  const h2v pr = (h2v){(_Float16)img[y0 * W + x0], (_Float16)img[y1 * W + x0]};
+  qp[(size_t)Y * (W + 3) + X] = __builtin_bit_cast(uint32_t, pr);
+}
 // padded quad-texel image (see pass_common.h)
 __global__ void k_build_quad(const float* __restrict__ img, float4* __restrict__ q, int W, int H) {
   const int X = blockIdx.x * blockDim.x + threadIdx.x;

@@ -109,7 +109,7 @@ DEV void lds_taps(const float* pw, int px, int py, const PassConst& pc, const De
   const int W = pc.W, Hh = pc.H;
   if constexpr (U8 != TEX_F32 && FAST && DPE_PACKED_TAP) {
     taps36_at<U8, IN>(pw, px, py, (f2v){(float)W, (float)Hh}, tex_base<U8>(B), (uint32_t)v * tex_view<U8>(B),
-                      (uint32_t)(W + 2), H, acc);
+                      tex_stride<U8>(W), H, acc);
   } else {
     float s_src = 0, s_ss = 0, s_rs = 0;
 #pragma unroll
@@ -147,7 +147,7 @@ DEV void lds_row(const float* pw, int px, int py, const PassConst& pc, const Dev
   const int W = pc.W, Hh = pc.H;
   const float x = (float)(px - 5 + 2 * a);
   if constexpr (U8 != TEX_F32 && FAST && DPE_PACKED_TAP) {
-    const uint32_t vofs = (uint32_t)v * tex_view<U8>(B), stride = (uint32_t)(W + 2);
+    const uint32_t vofs = (uint32_t)v * tex_view<U8>(B), stride = tex_stride<U8>(W);
     const f2v lim = (f2v){(float)W, (float)Hh};
     const f2v* wp = (const f2v*)pw;
     const f2v bxy = fma2((f2v){H.h[0], H.h[3]}, f2s(x), (f2v){H.h[2], H.h[5]});

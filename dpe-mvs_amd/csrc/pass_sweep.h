@@ -699,7 +699,7 @@ DEV void tab_taps(const PassConst& pc, const DevBufs& B, int v, const Homog& H, 
   const int n = NN > 0 ? NN : n_rt;
   const f2v* wp = (const f2v*)tw;            // (w, w*grey) pairs
   if constexpr (U8 != TEX_F32 && FAST && DPE_PACKED_TAP) {
-    const uint32_t vofs = (uint32_t)v * tex_view<U8>(B), stride = (uint32_t)(W + 2);
+    const uint32_t vofs = (uint32_t)v * tex_view<U8>(B), stride = tex_stride<U8>(W);
     const f2v lim = (f2v){(float)W, (float)Hh};
     f2v s_sr = f2s(0.0f);
     float s_ss = 0;

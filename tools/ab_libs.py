@@ -18,6 +18,7 @@ p = bench.workload_params(_abi, 10)
 inp = synthetic.pass_input(sc, p, depths=synthetic.src_depths(sc))
 st = synthetic.gt_state(sc)
 libs = sys.argv[1:]
+NOCHECK = os.environ.get("AB_NOCHECK") == "1"   # timing-only variants (e.g. stubbed phases)
 ctxs = []
 for path in libs:
     lib = native.load_library(path)
@@ -32,10 +33,11 @@ for rnd in range(3):
     for path, lib, ctx, bufs in ctxs:
         assert lib.dpe_pm_execute(ctx, None) == 0
         assert lib.dpe_pm_fetch(ctx, C.byref(bufs.st)) == 0
-        out = bufs.planes.tobytes()
+        out = b''.join(a.tobytes() for a in (bufs.planes, bufs.weak, bufs.sel, bufs.costs))
         if ref is None:
             ref = out
-        assert out == ref, f"{path}: output differs from {libs[0]}"
+        if not NOCHECK:
+            assert out == ref, f"{path}: output differs from {libs[0]}"
         buf = (C.c_float * 9)()
         lib.dpe_pm_last_timings(ctx, buf, 9)
         res[path].append([float(x) for x in buf])
@@ -53,7 +55,8 @@ for rnd in range(3):
         assert lib.dpe_pm_fetch(ctx, C.byref(bufs.st)) == 0
         torch.cuda.synchronize()
         wall[path].append((time.perf_counter() - t0) / 5 * 1e3)
-        assert bufs.planes.tobytes() == ref, f"{path}: untimed output differs from {libs[0]}"
+        if not NOCHECK:
+            assert b''.join(a.tobytes() for a in (bufs.planes, bufs.weak, bufs.sel, bufs.costs)) == ref, f"{path}: untimed output differs from {libs[0]}"
 names = ["total"] + native.CLASSES
 for path in libs:
     best = min(res[path], key=lambda t: t[0])
