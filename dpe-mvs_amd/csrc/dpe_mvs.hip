@@ -568,6 +568,7 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   HIPC(hipMemsetAsync(B.radius, 0, L * sizeof(int), s));
 
   const dim3 fb(16, 16), fg((W + 15) / 16, (H + 15) / 16);
+  const dim3 rb(16, kRansacThreads / 16), rg((W + 15) / 16, (H + rb.y - 1) / rb.y);
   const dim3 hb(32, 4), hg((((W + 1) / 2) + 31) / 32, (pc.half_rows + 3) / 4);
 
   DevBufs Bc;
@@ -655,7 +656,7 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
     }
     HIPC(hipGetLastError());
     Bc = begin(DPE_CLASS_RANSAC);
-    k_ransac_fit<<<fg, fb, 0, s>>>(dpc, Bc, it);
+    k_ransac_fit<<<rg, rb, 0, s>>>(dpc, Bc, it);
     end();
     for (int colour = 0; colour < 2; ++colour) {
       Bc = begin(DPE_CLASS_WEAK);
@@ -675,7 +676,7 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   }
   Bc = begin(DPE_CLASS_FILTER);
   k_depth_normal<<<fg, fb, 0, s>>>(dpc, Bc);
-  for (int colour = 0; colour < 2; ++colour) k_filter<<<hg, hb, 0, s>>>(dpc, Bc, colour);
+  for (int colour = 0; colour < 2; ++colour) k_filter<<<hg, hb, 0, s>>>(dpc, Bc, colour);   // hb: 32 x 4 = kFilterThreads
   end();
   Bc = begin(DPE_CLASS_DEPTH_TO_WEAK);
   if (c->img8) k_depth_to_weak<kTexD2W><<<(unsigned)((L + 3) / 4), 256, 0, s>>>(dpc, Bc);

@@ -389,14 +389,18 @@ DEV f2v fma2(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
 #endif
 // IN: the caller has proven s <= lim for this tap (patch_inside), so the min is the identity and is
 // skipped (the saturating conversion alone handles the low side).
+// The upper clamp is taken on the float before the conversion (v_min_f32, full rate, instead of
+// v_min_u32 after it, half rate): min(trunc(u), umax) == trunc(min(u, umax)) for every u that is
+// not NaN (umax is an integer below 2^24; +-inf saturate the same way), and on the taps' fast path
+// (rcp_range_ok) s = q * iz is never NaN.
 template <bool IN = false>
 DEV uint32_t fixed_coord(float s, uint32_t umax) {
 #if DPE_SAT_CLAMP
-  const float u = __builtin_fmaf(s, 256.0f, 256.5f);
+  float u = __builtin_fmaf(s, 256.0f, 256.5f);
+  if constexpr (!IN) u = __builtin_fminf(u, (float)umax);
   uint32_t r;
   asm("v_cvt_u32_f32 %0, %1" : "=v"(r) : "v"(u));
-  if constexpr (IN) return r;
-  return min(r, umax);
+  return r;
 #else
   const float lim = (float)((umax - 256u) >> 8);
   return (uint32_t)(int)__builtin_fmaf(__builtin_amdgcn_fmed3f(s, -1.0f, lim), 256.0f, 256.5f);

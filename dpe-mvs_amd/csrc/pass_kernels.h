@@ -536,7 +536,8 @@ __global__ void __launch_bounds__(256) k_random_init(const PassConst* __restrict
 }
 
 // ------------------------------------------------------------------------------ RANSACToGetFitPlane
-__global__ void __launch_bounds__(256) k_ransac_fit(const PassConst* __restrict__ pcp, DevBufs B, int iter) {   // DPE.cu:2891-3124
+constexpr int kRansacThreads = 128;   // 16 x 8 workgroups: 28 KB of LDS each
+__global__ void __launch_bounds__(kRansacThreads) k_ransac_fit(const PassConst* __restrict__ pcp, DevBufs B, int iter) {   // DPE.cu:2891-3124
   const PassConst& pc = *pcp;
   PIX2D_FULL();
   const int W = pc.W;
@@ -552,7 +553,13 @@ __global__ void __launch_bounds__(256) k_ransac_fit(const PassConst* __restrict_
       if (rp < cv) edge_limit = false;
     }
   }
-  short2 sp[8]; float3 sp3[8]; float3 spn[8];
+  // support points in LDS (thread index fastest): the random draws index them, which a register
+  // array cannot do without scratch memory
+  __shared__ short2 s_sp[8][kRansacThreads];
+  __shared__ float3 s_sp3[8][kRansacThreads], s_spn[8][kRansacThreads];
+  const int tid = threadIdx.y * blockDim.x + threadIdx.x;
+  struct Col2 { short2* p; DEV short2& operator[](int i) const { return p[i * kRansacThreads]; } } sp{&s_sp[0][tid]};
+  struct Col3 { float3* p; DEV float3& operator[](int i) const { return p[i * kRansacThreads]; } } sp3{&s_sp3[0][tid]}, spn{&s_spn[0][tid]};
   int sc = 0;
   float X[3];
   const short2* nb = B.nb + (size_t)center * 9;
@@ -574,14 +581,15 @@ __global__ void __launch_bounds__(256) k_ransac_fit(const PassConst* __restrict_
   float4 best = make_float4(0, 0, 0, 0);
   bool has_best = false, has_strong_plane = false;
   bool must_in_triangle = (pc.P.use_label && B.label[center] > 0 && edge_limit) ? false : true;
-  uint8_t tested[8] = {0, 0, 0, 0, 0, 0, 0, 0}, crosses[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  // edge_test[8][8] (DPE.cu:2960) as two 64-bit matrices, bit a * 8 + b
+  uint64_t tested = 0, crosses = 0;
   auto edge_pair = [&](int a, int b) -> bool {
-    if (!((tested[a] >> b) & 1)) {
+    if (!((tested >> (a * 8 + b)) & 1ull)) {
       const bool c = bresenham(pc, B, sp[a].x, sp[a].y, sp[b].x, sp[b].y);
-      tested[a] |= 1 << b; tested[b] |= 1 << a;
-      if (c) { crosses[a] |= 1 << b; crosses[b] |= 1 << a; }
+      tested |= (1ull << (a * 8 + b)) | (1ull << (b * 8 + a));
+      if (c) crosses |= (1ull << (a * 8 + b)) | (1ull << (b * 8 + a));
     }
-    return (crosses[a] >> b) & 1;
+    return (crosses >> (a * 8 + b)) & 1ull;
   };
   while (iteration--) {
     const int a = (int)(rng_u32(rs) % (uint32_t)sc);
@@ -696,13 +704,20 @@ __global__ void k_depth_normal(const PassConst* __restrict__ pcp, DevBufs B) {  
 }
 
 // ------------------------------------------------------------------------------ CheckerboardFilterStrong
-__global__ void k_filter(const PassConst* __restrict__ pcp, DevBufs B, int colour) {   // DPE.cu:1957-2101
+// The up-to-21 candidates live in LDS, thread index fastest (conflict-free), so the insertion sort
+// indexes them without scratch memory.  Launched with 128-thread (32 x 4) workgroups.
+constexpr int kFilterThreads = 128;
+__global__ void __launch_bounds__(kFilterThreads) k_filter(const PassConst* __restrict__ pcp, DevBufs B, int colour) {   // DPE.cu:1957-2101
+  __shared__ float s_filter[21][kFilterThreads];
   const PassConst& pc = *pcp;
   PIX2D_HALF();
   const int W = pc.W, H = pc.H;
   if (B.weak[center] == DPE_WEAK) return;
   const float4* P = B.planes;
-  float filter[21];
+  struct Col {
+    float* p;
+    DEV float& operator[](int i) const { return p[i * kFilterThreads]; }
+  } filter{&s_filter[0][threadIdx.y * blockDim.x + threadIdx.x]};
   int n = 0;
   filter[n++] = P[center].w;
   if (B.costs[center] < 0.001f) return;
