@@ -43,6 +43,7 @@ class DpePipelineOptions(C.Structure):
         ("keep_intermediate", C.c_bool),
         ("fusion_runner", C.c_void_p), ("fusion_user", C.c_void_p),
         ("max_iterations", C.c_int), ("photometric_only", C.c_bool),
+        ("allgather_device", C.c_void_p), ("allgather_device_user", C.c_void_p),
     ]
 
 
@@ -244,6 +245,34 @@ def _torch_allgather(dist):
     return ALLGATHER_FN(cb)
 
 
+ALLGATHER_DEV_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p)
+
+
+class _DeviceArray:
+    """A device buffer of the library as a torch tensor view (__cuda_array_interface__, no copy)."""
+
+    def __init__(self, ptr: int, n: int):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": "<f4", "data": (ptr, False), "version": 3}
+
+
+def _torch_allgather_device(dist):
+    """Device all-gather hook (dpe_allgather_dev_fn) over torch.distributed "nccl" (= RCCL): the
+    depth maps go from the library's HBM buffers to the other ranks' without a host copy."""
+    import torch
+    world = dist.get_world_size()
+
+    def cb(_user, send, count, recv):
+        try:
+            s = torch.as_tensor(_DeviceArray(send, count), device="cuda")
+            r = torch.as_tensor(_DeviceArray(recv, world * count), device="cuda")
+            dist.all_gather_into_tensor(r, s)
+            torch.cuda.synchronize()
+            return 0
+        except Exception:   # noqa: BLE001 -- reported to the C++ side as a failed collective
+            return -1
+    return ALLGATHER_DEV_FN(cb)
+
+
 def run_dpe_pipeline(dense_folder: str, gpu_index: int = 0, verbose: bool = True, fusion: bool = False,
                      viz: bool = False, depth: bool = True, normal: bool = False, weak: bool = False,
                      edge: bool = False, schedule: str = "reference", dist=None, runner=None,
@@ -270,6 +299,10 @@ def run_dpe_pipeline(dense_folder: str, gpu_index: int = 0, verbose: bool = True
         cb = _torch_allgather(dist)
         keep.append(cb)
         o.allgather = cb
+        if dist.get_backend() == "nccl" and runner is None:
+            dcb = _torch_allgather_device(dist)
+            keep.append(dcb)
+            o.allgather_device = C.cast(dcb, C.c_void_p)
     if runner is not None:
         o.runner = C.cast(runner[0], C.c_void_p)
         o.runner_user = C.cast(runner[1], C.c_void_p) if runner[1] is not None else None

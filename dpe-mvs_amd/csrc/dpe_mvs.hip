@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <map>
 #include <vector>
 
 #include "pass_kernels.h"
@@ -95,8 +96,25 @@ struct CachedImage {
   void release() { plain.release(); q8.release(); q16.release(); qp.release(); qf.release(); }
 };
 
+// Per-image pipeline state kept in HBM between passes (the reference's depths.dmb / normals.dmb /
+// weak.bin / selected_views.bin round trip, main.cpp:439-446 -> DPE.cpp:826-911).
+struct ResState {
+  int w = 0, h = 0;
+  bool full = false;          // planes / weak / sel of a pass of this image; false: depth only (imported)
+  DevArr<float4> planes;      // (world normal xyz, depth) after the ProcessProblem epilogue
+  DevArr<uint8_t> weak;
+  DevArr<uint32_t> sel;
+  DevArr<float> snap;         // depth snapshot for the Jacobi schedule (dpe_state_snapshot)
+  int snap_w = 0, snap_h = 0;
+  bool has_snap = false;
+  void release() { planes.release(); weak.release(); sel.release(); snap.release(); }
+};
+
 struct DpeContext {
   int device = 0;
+  std::map<int, ResState*> rstore;
+  DevArr<float> xbuf[2];             // dpe_device_buffer: exchange buffers of the multi-rank schedule
+  bool snap_mode = false;            // stage_resident reads source depths from the Jacobi snapshots
   std::vector<CachedImage*> icache;
   uint64_t icache_clock = 0;
   hipStream_t stream = nullptr;
@@ -257,6 +275,9 @@ void dpe_destroy(DpeContext* c) {
   c->weak.release(); c->weak_rel.release(); c->vw.release();
   c->nb.release(); c->nearest.release(); c->edge_neigh.release(); c->lab_bound.release();
   c->radius.release();
+  for (auto& kv : c->rstore) { kv.second->release(); delete kv.second; }
+  c->rstore.clear();
+  c->xbuf[0].release(); c->xbuf[1].release();
   c->cnt.release();
   c->tab_right.release(); c->tab_down.release();
   c->lists.release(); c->row_counts.release(); c->list_totals.release();
@@ -320,11 +341,76 @@ static void compute_pass_constants(PassConst& pc) {
   pc.half_rows = std::min(pc.H, 2 * 16 * (((pc.H / 2) + 15) / 16));
 }
 
+// where a stage takes the initial state and the source depths from: host buffers (dpe_pm_stage) or
+// the resident store (dpe_pm_stage_resident)
+struct StageSrc {
+  const DpePassState* st = nullptr;   // host initial state
+  const ResState* prior = nullptr;    // resident initial state (nullptr: none, FIRST_INIT)
+  const ResState* dep[DPE_MAX_IMAGES] = {};   // resident source depths (index 1..N-1)
+  bool dep_snap = false;              // read the depths' Jacobi snapshots
+};
+static int stage_impl(DpeContext* c, const DpePassInput* in, const StageSrc& src);
+
 extern "C" int dpe_pm_stage(DpeContext* c, const DpePassInput* in, const DpePassState* st) {
   g_err.clear();
   if (!c || !in || !st || !in->images || !in->cams || !st->planes || !st->weak_info || !st->selected_views) {
     g_err = "dpe_pm_stage: null argument"; return DPE_ERR_ARG;
   }
+  if (in->params.geom_consistency) {
+    if (!in->depths) { g_err = "dpe_pm_stage: geom_consistency needs depths"; return DPE_ERR_ARG; }
+    for (int i = 1; i < in->num_images; ++i) if (!in->depths[i]) { g_err = "dpe_pm_stage: missing source depth"; return DPE_ERR_ARG; }
+  }
+  StageSrc src;
+  src.st = st;
+  return stage_impl(c, in, src);
+}
+
+template <class T>
+__global__ void k_rescale_nearest(const T* __restrict__ src, int w, int h, T* __restrict__ dst, int nw, int nh, T zero) {
+  // RescaleMatToTargetSize (DPE.cpp:1146-1165) with its swapped factors, as host rescale_nearest
+  const int c = blockIdx.x * blockDim.x + threadIdx.x, r = blockIdx.y * blockDim.y + threadIdx.y;
+  if (c >= nw || r >= nh) return;
+  const float scale_x = nw / (float)w, scale_y = nh / (float)h;
+  const int o_r = (int)(r / scale_x), o_c = (int)(c / scale_y);
+  dst[(size_t)r * nw + c] = (o_r < 0 || o_c < 0 || o_r >= h || o_c >= w) ? zero : src[(size_t)o_r * w + o_c];
+}
+__global__ void k_rescale_depth(const float4* __restrict__ src, int w, int h, float* __restrict__ dst, int nw, int nh) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x, r = blockIdx.y * blockDim.y + threadIdx.y;
+  if (c >= nw || r >= nh) return;
+  const float scale_x = nw / (float)w, scale_y = nh / (float)h;
+  const int o_r = (int)(r / scale_x), o_c = (int)(c / scale_y);
+  dst[(size_t)r * nw + c] = (o_r < 0 || o_c < 0 || o_r >= h || o_c >= w) ? 0.0f : src[(size_t)o_r * w + o_c].w;
+}
+
+extern "C" int dpe_pm_stage_resident(DpeContext* c, const DpePassInput* in, int prior_id) {
+  g_err.clear();
+  if (!c || !in || !in->images || !in->cams) { g_err = "dpe_pm_stage_resident: null argument"; return DPE_ERR_ARG; }
+  const DpePatchMatchParams& P = in->params;
+  StageSrc src;
+  auto find = [&](int id) -> ResState* { auto it = c->rstore.find(id); return it == c->rstore.end() ? nullptr : it->second; };
+  if (P.state != DPE_FIRST_INIT || P.use_APD) {
+    src.prior = find(prior_id);
+    if (!src.prior || !src.prior->full) {
+      g_err = "dpe_pm_stage_resident: no resident state of image " + std::to_string(prior_id); return DPE_ERR_STATE;
+    }
+  }
+  if (P.geom_consistency) {
+    if (!in->image_ids) { g_err = "dpe_pm_stage_resident: geom_consistency needs image_ids"; return DPE_ERR_ARG; }
+    for (int i = 1; i < in->num_images && i < DPE_MAX_IMAGES; ++i) {
+      src.dep[i] = find(in->image_ids[i]);
+      if (!src.dep[i]) { g_err = "no depth map of source image " + std::to_string(in->image_ids[i]); return DPE_ERR_STATE; }
+    }
+    src.dep_snap = c->snap_mode;
+    if (src.dep_snap)
+      for (int i = 1; i < in->num_images && i < DPE_MAX_IMAGES; ++i)
+        if (!src.dep[i]->has_snap) { g_err = "no depth snapshot of source image " + std::to_string(in->image_ids[i]); return DPE_ERR_STATE; }
+  }
+  return stage_impl(c, in, src);
+}
+
+static int stage_impl(DpeContext* c, const DpePassInput* in, const StageSrc& src) {
+  g_err.clear();
+  const DpePassState* st = src.st;
   if (in->num_images > DPE_MAX_IMAGES) { g_err = "dpe_pm_stage: num_images > 32 (DPE.cpp:762)"; return DPE_ERR_TOO_MANY; }
   if (in->num_images < 2 || in->width <= 0 || in->height <= 0) { g_err = "dpe_pm_stage: bad shape"; return DPE_ERR_ARG; }
   if (in->width > 32000 || in->height > 32000) { g_err = "dpe_pm_stage: image too large for short2 coordinates"; return DPE_ERR_ARG; }
@@ -332,10 +418,6 @@ extern "C" int dpe_pm_stage(DpeContext* c, const DpePassInput* in, const DpePass
   if (P.rotate_time < 1 || P.rotate_time > 4) { g_err = "dpe_pm_stage: rotate_time must be in [1,4]"; return DPE_ERR_ARG; }
   if (P.strong_increment <= 0 || P.weak_increment <= 0) { g_err = "dpe_pm_stage: increments must be > 0"; return DPE_ERR_ARG; }
   for (int i = 0; i < in->num_images; ++i) if (!in->images[i]) { g_err = "dpe_pm_stage: missing image"; return DPE_ERR_ARG; }
-  if (P.geom_consistency) {
-    if (!in->depths) { g_err = "dpe_pm_stage: geom_consistency needs depths"; return DPE_ERR_ARG; }
-    for (int i = 1; i < in->num_images; ++i) if (!in->depths[i]) { g_err = "dpe_pm_stage: missing source depth"; return DPE_ERR_ARG; }
-  }
   if ((P.use_edge || P.use_limit) && (!in->edge || !in->edge_low_res || in->low_width <= 0 || in->low_height <= 0)) {
     g_err = "dpe_pm_stage: use_edge/use_limit need edge and edge_low_res"; return DPE_ERR_ARG;
   }
@@ -457,10 +539,20 @@ extern "C" int dpe_pm_stage(DpeContext* c, const DpePassInput* in, const DpePass
     HIPC(hipGetLastError());
   }
   if (!in->image_ids) B.ref = c->img_plain[0].p;
+  const dim3 rb2(32, 8), rg2((W + 31) / 32, (H + 7) / 8);
   if (P.geom_consistency) {
     for (int i = 1; i < N; ++i) {
       HIPC(c->depth[i].ensure(L));
-      HIPC(hipMemcpyAsync(c->depth[i].p, in->depths[i], L * sizeof(float), hipMemcpyHostToDevice, c->stream));
+      if (st) {
+        HIPC(hipMemcpyAsync(c->depth[i].p, in->depths[i], L * sizeof(float), hipMemcpyHostToDevice, c->stream));
+      } else {
+        const ResState* r = src.dep[i];
+        if (src.dep_snap)
+          k_rescale_nearest<float><<<rg2, rb2, 0, c->stream>>>(r->snap.p, r->snap_w, r->snap_h, c->depth[i].p, W, H, 0.0f);
+        else
+          k_rescale_depth<<<rg2, rb2, 0, c->stream>>>(r->planes.p, r->w, r->h, c->depth[i].p, W, H);
+        HIPC(hipGetLastError());
+      }
       B.depth[i] = c->depth[i].p;
     }
   }
@@ -479,10 +571,24 @@ extern "C" int dpe_pm_stage(DpeContext* c, const DpePassInput* in, const DpePass
     B.label = c->label.p;
   }
   HIPC(c->planes0.ensure(L)); HIPC(c->weak0.ensure(L)); HIPC(c->sel0.ensure(L));
-  HIPC(hipMemcpyAsync(c->planes0.p, st->planes, L * sizeof(float4), hipMemcpyHostToDevice, c->stream));
-  if (P.use_APD) HIPC(hipMemcpyAsync(c->weak0.p, st->weak_info, L, hipMemcpyHostToDevice, c->stream));
-  else HIPC(hipMemsetAsync(c->weak0.p, DPE_STRONG, L, c->stream));   // DPE.cpp:873-881
-  HIPC(hipMemcpyAsync(c->sel0.p, st->selected_views, L * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+  if (st) {
+    HIPC(hipMemcpyAsync(c->planes0.p, st->planes, L * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+    if (P.use_APD) HIPC(hipMemcpyAsync(c->weak0.p, st->weak_info, L, hipMemcpyHostToDevice, c->stream));
+    else HIPC(hipMemsetAsync(c->weak0.p, DPE_STRONG, L, c->stream));   // DPE.cpp:873-881
+    HIPC(hipMemcpyAsync(c->sel0.p, st->selected_views, L * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+  } else {   // InuputInitialization's prior (DPE.cpp:845-911) from the resident state, rescaled on device
+    const ResState* r = src.prior;
+    if (P.state != DPE_FIRST_INIT) {
+      k_rescale_nearest<float4><<<rg2, rb2, 0, c->stream>>>(r->planes.p, r->w, r->h, c->planes0.p, W, H, make_float4(0, 0, 0, 0));
+      k_rescale_nearest<uint32_t><<<rg2, rb2, 0, c->stream>>>(r->sel.p, r->w, r->h, c->sel0.p, W, H, 0u);
+    } else {
+      HIPC(hipMemsetAsync(c->planes0.p, 0, L * sizeof(float4), c->stream));
+      HIPC(hipMemsetAsync(c->sel0.p, 0, L * sizeof(uint32_t), c->stream));
+    }
+    if (P.use_APD) k_rescale_nearest<uint8_t><<<rg2, rb2, 0, c->stream>>>(r->weak.p, r->w, r->h, c->weak0.p, W, H, (uint8_t)0);
+    else HIPC(hipMemsetAsync(c->weak0.p, DPE_STRONG, L, c->stream));
+    HIPC(hipGetLastError());
+  }
   HIPC(c->planes.ensure(L)); HIPC(c->planes_snap.ensure(L)); HIPC(c->fit_plane.ensure(L));
   HIPC(c->costs.ensure(L)); HIPC(c->costs_snap.ensure(L)); HIPC(c->complex_.ensure(L));
   HIPC(c->sel.ensure(L)); HIPC(c->sel_snap.ensure(L));
@@ -765,6 +871,171 @@ extern "C" int dpe_pm_export_depth(DpeContext* c, float* dev_dst, void* stream_)
   k_export_depth<<<(unsigned)((L + 255) / 256), 256, 0, s>>>(c->bufs.planes, dev_dst, L);
   HIPC(hipGetLastError());
   return DPE_OK;
+}
+
+// ------------------------------------------------------------------------------ resident state
+// ProcessProblem's epilogue (main.cpp:423-437) on the pass outputs, into the image's resident state
+__global__ void k_state_save(const float4* __restrict__ planes, const uint8_t* __restrict__ weak,
+                             const uint32_t* __restrict__ sel, float dmin, float dmax, float4* __restrict__ op,
+                             uint8_t* __restrict__ ow, uint32_t* __restrict__ os, size_t L) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= L) return;
+  float4 p = planes[i];
+  uint8_t w = weak[i];
+  if (p.w < dmin || p.w > dmax) { p.w = 0.0f; w = DPE_UNKNOWN; }
+  op[i] = p; ow[i] = w; os[i] = sel[i];
+}
+__global__ void k_depth_of(const float4* __restrict__ p, float* __restrict__ d, size_t L) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < L) d[i] = p[i].w;
+}
+__global__ void k_depth_into(const float* __restrict__ d, float4* __restrict__ p, size_t L) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < L) p[i].w = d[i];
+}
+
+static ResState* state_slot(DpeContext* c, int id) {
+  auto it = c->rstore.find(id);
+  if (it != c->rstore.end()) return it->second;
+  ResState* r = new ResState();
+  c->rstore[id] = r;
+  return r;
+}
+
+extern "C" int dpe_state_save(DpeContext* c, int image_id) {
+  g_err.clear();
+  if (!c) { g_err = "dpe_state_save: null context"; return DPE_ERR_ARG; }
+  if (!c->staged) { g_err = "dpe_state_save: nothing staged"; return DPE_ERR_STATE; }
+  HIPC(hipSetDevice(c->device));
+  const int W = c->hc.W, H = c->hc.H;
+  const size_t L = (size_t)W * H;
+  if (c->pending) HIPC(hipStreamWaitEvent(c->stream, c->ev_done, 0));   // after the pass that wrote the outputs
+  ResState* r = state_slot(c, image_id);
+  HIPC(r->planes.ensure(L)); HIPC(r->weak.ensure(L)); HIPC(r->sel.ensure(L));
+  r->w = W; r->h = H; r->full = true;
+  k_state_save<<<(unsigned)((L + 255) / 256), 256, 0, c->stream>>>(c->bufs.planes, c->bufs.weak, c->bufs.sel, c->hc.P.depth_min,
+                                                                  c->hc.P.depth_max, r->planes.p, r->weak.p, r->sel.p, L);
+  HIPC(hipGetLastError());
+  HIPC(hipEventRecord(c->ev_done, c->stream));   // the next execute / stage waits for the save too
+  c->pending = true;
+  return DPE_OK;
+}
+
+extern "C" int dpe_state_fetch(DpeContext* c, int image_id, int* w, int* h, float* depth, float* normal, uint8_t* weak,
+                               uint32_t* sel) {
+  g_err.clear();
+  if (!c) { g_err = "dpe_state_fetch: null context"; return DPE_ERR_ARG; }
+  auto it = c->rstore.find(image_id);
+  if (it == c->rstore.end()) { g_err = "dpe_state_fetch: no state of image " + std::to_string(image_id); return DPE_ERR_STATE; }
+  ResState* r = it->second;
+  if (w) *w = r->w;
+  if (h) *h = r->h;
+  const size_t L = (size_t)r->w * r->h;
+  HIPC(hipSetDevice(c->device));
+  HIPC(wait_pending(c));
+  HIPC(hipStreamSynchronize(c->stream));
+  if (depth || normal) {
+    std::vector<float4> p(L);
+    HIPC(hipMemcpy(p.data(), r->planes.p, L * sizeof(float4), hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < L; ++i) {
+      if (depth) depth[i] = p[i].w;
+      if (normal) { normal[3 * i] = p[i].x; normal[3 * i + 1] = p[i].y; normal[3 * i + 2] = p[i].z; }
+    }
+  }
+  if (weak || sel) {
+    if (!r->full) { g_err = "dpe_state_fetch: image " + std::to_string(image_id) + " holds a depth map only"; return DPE_ERR_STATE; }
+    if (weak) HIPC(hipMemcpy(weak, r->weak.p, L, hipMemcpyDeviceToHost));
+    if (sel) HIPC(hipMemcpy(sel, r->sel.p, L * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  }
+  return DPE_OK;
+}
+
+extern "C" int dpe_state_snapshot(DpeContext* c) {
+  g_err.clear();
+  if (!c) { g_err = "dpe_state_snapshot: null context"; return DPE_ERR_ARG; }
+  HIPC(hipSetDevice(c->device));
+  if (c->pending) HIPC(hipStreamWaitEvent(c->stream, c->ev_done, 0));
+  for (auto& kv : c->rstore) {
+    ResState* r = kv.second;
+    const size_t L = (size_t)r->w * r->h;
+    HIPC(r->snap.ensure(L));
+    k_depth_of<<<(unsigned)((L + 255) / 256), 256, 0, c->stream>>>(r->planes.p, r->snap.p, L);
+    r->snap_w = r->w; r->snap_h = r->h;
+    r->has_snap = true;
+  }
+  HIPC(hipGetLastError());
+  HIPC(hipEventRecord(c->ev_done, c->stream));
+  c->pending = true;
+  c->snap_mode = true;
+  return DPE_OK;
+}
+
+extern "C" int dpe_state_export_depth(DpeContext* c, int image_id, float* dev_dst, void* stream_) {
+  g_err.clear();
+  if (!c || !dev_dst) { g_err = "dpe_state_export_depth: null argument"; return DPE_ERR_ARG; }
+  auto it = c->rstore.find(image_id);
+  if (it == c->rstore.end()) { g_err = "dpe_state_export_depth: no state of image " + std::to_string(image_id); return DPE_ERR_STATE; }
+  HIPC(hipSetDevice(c->device));
+  hipStream_t s = stream_ ? (hipStream_t)stream_ : c->stream;
+  if (c->pending) HIPC(hipStreamWaitEvent(s, c->ev_done, 0));
+  const size_t L = (size_t)it->second->w * it->second->h;
+  k_depth_of<<<(unsigned)((L + 255) / 256), 256, 0, s>>>(it->second->planes.p, dev_dst, L);
+  HIPC(hipGetLastError());
+  return DPE_OK;
+}
+
+extern "C" int dpe_state_import_depth(DpeContext* c, int image_id, int w, int h, const float* dev_src, void* stream_) {
+  g_err.clear();
+  if (!c || !dev_src || w <= 0 || h <= 0) { g_err = "dpe_state_import_depth: bad argument"; return DPE_ERR_ARG; }
+  HIPC(hipSetDevice(c->device));
+  hipStream_t s = stream_ ? (hipStream_t)stream_ : c->stream;
+  if (c->pending) HIPC(hipStreamWaitEvent(s, c->ev_done, 0));   // an execute may still read this state's depth
+  ResState* r = state_slot(c, image_id);
+  const size_t L = (size_t)w * h;
+  if (r->w != w || r->h != h) {
+    HIPC(r->planes.ensure(L));
+    HIPC(hipMemsetAsync(r->planes.p, 0, L * sizeof(float4), s));
+    r->w = w; r->h = h; r->full = false;
+  }
+  k_depth_into<<<(unsigned)((L + 255) / 256), 256, 0, s>>>(dev_src, r->planes.p, L);
+  HIPC(hipGetLastError());
+  if (s != c->stream) {   // later stages on the context stream read it
+    HIPC(hipEventRecord(c->ev_done, s));
+    c->pending = true;
+  }
+  return DPE_OK;
+}
+
+extern "C" float* dpe_device_buffer(DpeContext* c, int slot, size_t count) {
+  g_err.clear();
+  if (!c || slot < 0 || slot > 1) { g_err = "dpe_device_buffer: bad argument"; return nullptr; }
+  if (hipSetDevice(c->device) != hipSuccess) { g_err = "dpe_device_buffer: hipSetDevice"; return nullptr; }
+  if (c->xbuf[slot].n < count) {
+    if (wait_pending(c) != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess) { g_err = "dpe_device_buffer: sync"; return nullptr; }
+    if (c->xbuf[slot].ensure(count) != hipSuccess) { g_err = "dpe_device_buffer: hipMalloc"; return nullptr; }
+  }
+  return c->xbuf[slot].p;
+}
+
+extern "C" int dpe_device_copy(DpeContext* c, void* dst, const void* src, size_t bytes, int kind) {
+  g_err.clear();
+  if (!c || !dst || !src || kind < 0 || kind > 2) { g_err = "dpe_device_copy: bad argument"; return DPE_ERR_ARG; }
+  HIPC(hipSetDevice(c->device));
+  HIPC(wait_pending(c));
+  HIPC(hipStreamSynchronize(c->stream));
+  const hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice : (kind == 1 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice);
+  HIPC(hipMemcpy(dst, src, bytes, k));
+  return DPE_OK;
+}
+
+extern "C" void dpe_state_clear(DpeContext* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  (void)wait_pending(c);
+  (void)hipStreamSynchronize(c->stream);
+  for (auto& kv : c->rstore) { kv.second->release(); delete kv.second; }
+  c->rstore.clear();
+  c->snap_mode = false;
 }
 
 extern "C" int dpe_fusion_stage(DpeContext* c, const DpeFusionView* views, int n) {

@@ -51,6 +51,13 @@ int rccl_allgather(void* user, const float* send, size_t count, float* recv) {
   return hipStreamSynchronize(r->stream) == hipSuccess ? 0 : -1;
 }
 
+// device buffers on both sides: the depth maps go from HBM to HBM over xGMI with no host copy
+int rccl_allgather_dev(void* user, const float* dsend, size_t count, float* drecv) {
+  Rccl* r = static_cast<Rccl*>(user);
+  if (ncclAllGather(dsend, drecv, count, ncclFloat, r->comm, r->stream) != ncclSuccess) return -1;
+  return hipStreamSynchronize(r->stream) == hipSuccess ? 0 : -1;
+}
+
 bool send_all(int fd, const void* p, size_t n) {
   const char* c = static_cast<const char*>(p);
   while (n) {
@@ -155,8 +162,10 @@ int main(int argc, char** argv) {
       std::fprintf(stderr, "RCCL initialisation failed\n");
       return EXIT_FAILURE;
     }
-    o.allgather = rccl_allgather;
+    o.allgather = rccl_allgather;          // host buffers (runner hooks, fusion's one-off exchange)
     o.allgather_user = &rccl;
+    o.allgather_device = rccl_allgather_dev;   // the per-pass depth maps, HBM to HBM
+    o.allgather_device_user = &rccl;
   }
   const int rc = dpe_run_pipeline(argv[1], &o);
   if (rc != 0) std::fprintf(stderr, "DPE pipeline failed: %s\n", dpe_pipeline_last_error());

@@ -199,6 +199,36 @@ int native_fusion(void* user, const DpeFusionView* views, int n, int ref, const 
   return dpe_fusion_candidates(f->ctx, ref, src, ns, idx, val);
 }
 
+// the per-pass intermediate maps of the reference (main.cpp:439-446)
+bool write_state_maps(const Problem& p, const ImageState& s, std::string& err) {
+  const int W = s.w, H = s.h;
+  const size_t L = (size_t)W * H;
+  Mat m;
+  m.create(H, W, CV_32FC1); std::memcpy(m.data.data(), s.depth.data(), L * 4);
+  if (!write_bin_mat((fs::path(p.result_folder) / "depths.dmb").string(), m, err)) return false;
+  m.create(H, W, CV_32FC3); std::memcpy(m.data.data(), s.normal.data(), L * 12);
+  if (!write_bin_mat((fs::path(p.result_folder) / "normals.dmb").string(), m, err)) return false;
+  m.create(H, W, CV_8UC1); std::memcpy(m.data.data(), s.weak.data(), L);
+  if (!write_bin_mat((fs::path(p.result_folder) / "weak.bin").string(), m, err)) return false;
+  m.create(H, W, CV_32SC1); std::memcpy(m.data.data(), s.sel.data(), L * 4);
+  if (!write_bin_mat((fs::path(p.result_folder) / "selected_views.bin").string(), m, err)) return false;
+  return true;
+}
+
+// host copy of an image's HBM-resident state (depth_only: a state imported from another rank)
+bool fetch_state(DpeContext* ctx, int id, ImageState& s, std::string& err, bool depth_only = false) {
+  int w = 0, h = 0;
+  if (dpe_state_fetch(ctx, id, &w, &h, nullptr, nullptr, nullptr, nullptr) != 0) { err = dpe_last_error(); return false; }
+  const size_t L = (size_t)w * h;
+  s.w = w; s.h = h;
+  s.depth.resize(L);
+  if (!depth_only) { s.normal.resize(L * 3); s.weak.resize(L); s.sel.resize(L); }
+  const int rc = dpe_state_fetch(ctx, id, &w, &h, s.depth.data(), depth_only ? nullptr : s.normal.data(),
+                                 depth_only ? nullptr : s.weak.data(), depth_only ? nullptr : s.sel.data());
+  if (rc != 0) { err = dpe_last_error(); return false; }
+  return true;
+}
+
 // InuputInitialization + SupportInitialization (DPE.cpp:733-914, 1025-1052), the pass, the epilogue
 bool process_problem(Problem& p, ImageCache& cache, std::map<int, ImageState>& states,
                      const std::map<int, DepthMap>& depth_src, const DpePipelineOptions& opt, Runner& run,
@@ -231,9 +261,12 @@ bool process_problem(Problem& p, ImageCache& cache, std::map<int, ImageState>& s
   P.depth_min = cams[0].depth_min * 0.6f;
   P.depth_max = cams[0].depth_max * 1.2f;
   P.num_images = (int)ids.size();
+  // with the default runner the state stays in HBM (dpe_state_save / dpe_pm_stage_resident): the
+  // prior, the source depths and the epilogue are all on the device, nothing is copied back per pass
+  const bool resident = run.ctx != nullptr;
   std::vector<std::vector<float>> dep_store;
   std::vector<const float*> depths(ids.size(), nullptr);
-  if (P.geom_consistency) {
+  if (P.geom_consistency && !resident) {
     dep_store.reserve(ids.size());
     for (size_t k = 1; k < ids.size(); ++k) {
       auto it = depth_src.find(ids[k]);
@@ -242,15 +275,17 @@ bool process_problem(Problem& p, ImageCache& cache, std::map<int, ImageState>& s
       depths[k] = dep_store.back().data();
     }
   }
-  const ImageState* prev = states.count(p.ref_image_id) ? &states.at(p.ref_image_id) : nullptr;
-  std::vector<float> planes(L * 4, 0.0f);
-  std::vector<uint8_t> weak(L, DPE_STRONG);
-  std::vector<uint32_t> sel(L, 0u);
-  if (P.use_APD) {
+  const ImageState* prev = (!resident && states.count(p.ref_image_id)) ? &states.at(p.ref_image_id) : nullptr;
+  std::vector<float> planes(resident ? 0 : L * 4, 0.0f);
+  std::vector<uint8_t> weak(resident ? 0 : L, DPE_STRONG);
+  std::vector<uint32_t> sel(resident ? 0 : L, 0u);
+  if (resident) {
+    // nothing to build on the host
+  } else if (P.use_APD) {
     if (!prev) { err = "Can't find weak info of image " + std::to_string(p.ref_image_id); return false; }
     weak = rescaled(prev->weak, prev->w, prev->h, W, H);
   }
-  if (P.state != DPE_FIRST_INIT) {
+  if (!resident && P.state != DPE_FIRST_INIT) {
     if (!prev) { err = "no prior depth/normal of image " + std::to_string(p.ref_image_id); return false; }
     const std::vector<float> d = rescaled(prev->depth, prev->w, prev->h, W, H);
     const std::vector<float> n = rescaled(prev->normal, prev->w, prev->h, W, H, 3);
@@ -265,7 +300,7 @@ bool process_problem(Problem& p, ImageCache& cache, std::map<int, ImageState>& s
   in.width = W; in.height = H; in.num_images = (int)ids.size();
   in.images = images.data();
   in.cams = cams.data();
-  in.depths = P.geom_consistency ? depths.data() : nullptr;
+  in.depths = (P.geom_consistency && !resident) ? depths.data() : nullptr;
   Mat edge, edge_low, label;
   if (P.use_edge || P.use_limit) {
     const int s = scale_index(p.scale_size);
@@ -286,6 +321,18 @@ bool process_problem(Problem& p, ImageCache& cache, std::map<int, ImageState>& s
   in.seed = opt.base_seed ^ ((uint64_t)p.ref_image_id * 0x9E3779B97F4A7C15ull);
   in.pass_salt = (uint32_t)p.iteration;
   in.image_ids = ids.data();        // pyramid levels stay in HBM across passes (keyed by id and size)
+  if (resident) {
+    int rc = dpe_pm_stage_resident(run.ctx, &in, p.ref_image_id);
+    if (rc == 0) rc = dpe_pm_execute(run.ctx, nullptr);
+    if (rc == 0) rc = dpe_state_save(run.ctx, p.ref_image_id);
+    if (rc != 0) { err = "PatchMatch pass failed (" + std::to_string(rc) + "): " + dpe_last_error(); return false; }
+    if (opt.keep_intermediate) {
+      ImageState s;
+      if (!fetch_state(run.ctx, p.ref_image_id, s, err)) return false;
+      if (!write_state_maps(p, s, err)) return false;
+    }
+    return true;
+  }
   std::vector<float> costs(L);
   DpePassState st{planes.data(), weak.data(), sel.data(), costs.data()};
   const int rc = run.fn(run.user, &in, &st);
@@ -303,17 +350,7 @@ bool process_problem(Problem& p, ImageCache& cache, std::map<int, ImageState>& s
     s.depth[i] = d;
     s.normal[3 * i + 0] = planes[4 * i + 0]; s.normal[3 * i + 1] = planes[4 * i + 1]; s.normal[3 * i + 2] = planes[4 * i + 2];
   }
-  if (opt.keep_intermediate) {
-    Mat m;
-    m.create(H, W, CV_32FC1); std::memcpy(m.data.data(), s.depth.data(), L * 4);
-    if (!write_bin_mat((fs::path(p.result_folder) / "depths.dmb").string(), m, err)) return false;
-    m.create(H, W, CV_32FC3); std::memcpy(m.data.data(), s.normal.data(), L * 12);
-    if (!write_bin_mat((fs::path(p.result_folder) / "normals.dmb").string(), m, err)) return false;
-    m.create(H, W, CV_8UC1); std::memcpy(m.data.data(), s.weak.data(), L);
-    if (!write_bin_mat((fs::path(p.result_folder) / "weak.bin").string(), m, err)) return false;
-    m.create(H, W, CV_32SC1); std::memcpy(m.data.data(), s.sel.data(), L * 4);
-    if (!write_bin_mat((fs::path(p.result_folder) / "selected_views.bin").string(), m, err)) return false;
-  }
+  if (opt.keep_intermediate && !write_state_maps(p, s, err)) return false;
   states[p.ref_image_id] = std::move(s);
   return true;
 }
@@ -456,9 +493,11 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
   std::map<int, ImageState> states;
   std::map<int, DepthMap> depth_cur;
   int iteration_index = 0;
+  const bool resident = runner.ctx != nullptr;
   for (int i = 0; i < round_num; ++i) {
     for (int j = -1; j < 3; ++j) {
-      const std::map<int, DepthMap> snapshot = jacobi ? depth_cur : std::map<int, DepthMap>{};
+      if (resident && jacobi && !failed && dpe_state_snapshot(runner.ctx) != 0) fail(dpe_last_error());
+      const std::map<int, DepthMap> snapshot = (jacobi && !resident) ? depth_cur : std::map<int, DepthMap>{};
       const auto& depth_src = jacobi ? snapshot : depth_cur;
       // pass size: ImageCache::level's rounding of the first image (CheckImages: all the same size)
       const int scale = (int)std::pow(2, round_num - 1 - i);
@@ -475,11 +514,50 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
         if (opt.photometric_only) p.params.geom_consistency = false;
         std::string perr;
         if (!process_problem(p, cache, states, depth_src, opt, runner, perr)) { fail(perr); break; }
-        const ImageState& s = states[p.ref_image_id];
-        depth_cur[p.ref_image_id] = DepthMap{s.w, s.h, s.depth};
+        if (!resident) {
+          const ImageState& s = states[p.ref_image_id];
+          depth_cur[p.ref_image_id] = DepthMap{s.w, s.h, s.depth};
+        }
       }
       if (world == 1 && failed) { err = first_err; return 1; }
-      if (world > 1) {   // all-gather of the depth maps (the pass's only cross-image data)
+      if (world > 1 && resident) {   // all-gather of the depth maps from / into the HBM-resident states
+        size_t nmax = 0;
+        for (auto& b : blocks) nmax = std::max(nmax, b.size());
+        const size_t per = (size_t)pw * ph, cnt = nmax * per + 1;   // + the status float
+        float* dsend = dpe_device_buffer(runner.ctx, 0, cnt);
+        float* drecv = dsend ? dpe_device_buffer(runner.ctx, 1, cnt * world) : nullptr;
+        if (!drecv) { err = dpe_last_error(); return 1; }
+        for (size_t k = 0; !failed && k < blocks[rank].size(); ++k)
+          if (dpe_state_export_depth(runner.ctx, problems[blocks[rank][k]].ref_image_id, dsend + k * per, nullptr) != 0)
+            fail(dpe_last_error());
+        const float flag = failed ? 1.0f : 0.0f;
+        if (dpe_device_copy(runner.ctx, dsend + nmax * per, &flag, sizeof(float), 0) != 0) { err = dpe_last_error(); return 1; }
+        std::vector<float> status(world);
+        if (opt.allgather_device) {
+          if (opt.allgather_device(opt.allgather_device_user, dsend, cnt, drecv) != 0) { err = "all-gather failed"; return 1; }
+        } else {   // host hook: one device -> host -> device hop of the packed maps
+          std::vector<float> hs(cnt), hr(cnt * world);
+          if (dpe_device_copy(runner.ctx, hs.data(), dsend, cnt * sizeof(float), 1) != 0) { err = dpe_last_error(); return 1; }
+          if (opt.allgather(opt.allgather_user, hs.data(), cnt, hr.data()) != 0) { err = "all-gather failed"; return 1; }
+          if (dpe_device_copy(runner.ctx, drecv, hr.data(), hr.size() * sizeof(float), 0) != 0) { err = dpe_last_error(); return 1; }
+        }
+        int bad = -1;
+        for (int r = 0; r < world; ++r) {
+          if (dpe_device_copy(runner.ctx, &status[r], drecv + (size_t)r * cnt + nmax * per, sizeof(float), 1) != 0) {
+            err = dpe_last_error(); return 1;
+          }
+          if (bad < 0 && status[r] != 0.0f) bad = r;
+        }
+        if (bad >= 0) { err = bad == rank ? first_err : "rank " + std::to_string(bad) + " failed"; return 1; }
+        for (int r = 0; r < world; ++r) {
+          if (r == rank) continue;
+          for (size_t k = 0; k < blocks[r].size(); ++k)
+            if (dpe_state_import_depth(runner.ctx, problems[blocks[r][k]].ref_image_id, pw, ph,
+                                       drecv + (size_t)r * cnt + k * per, nullptr) != 0) {
+              err = dpe_last_error(); return 1;
+            }
+        }
+      } else if (world > 1) {   // all-gather of the depth maps (the pass's only cross-image data)
         size_t nmax = 0;
         for (auto& b : blocks) nmax = std::max(nmax, b.size());
         const size_t per = (size_t)pw * ph;
@@ -499,7 +577,13 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
       iteration_index++;
     }
   }
+  if (resident && !failed)   // the final states come back from HBM once
+    for (int pi : blocks[rank]) {
+      std::string ferr;
+      if (!fetch_state(runner.ctx, problems[pi].ref_image_id, states[problems[pi].ref_image_id], ferr)) { fail(ferr); break; }
+    }
   for (int pi : blocks[rank]) {
+    if (failed) break;
     const Problem& p = problems[pi];
     std::string werr;
     if (!write_outputs(p, states[p.ref_image_id], opt, werr)) { fail(werr); break; }
@@ -528,7 +612,13 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
           const float* src = recv.data() + ((size_t)r * nmax + k) * per * 4;
           ImageState st;
           st.w = s0.w; st.h = s0.h;
-          st.depth = depth_cur[id].d;
+          if (resident) {
+            ImageState d;
+            if (!fetch_state(runner.ctx, id, d, err, true)) return 1;
+            st.depth = std::move(d.depth);
+          } else {
+            st.depth = depth_cur[id].d;
+          }
           st.normal.assign(src, src + 3 * per);
           st.weak.resize(per);
           for (size_t i = 0; i < per; ++i) st.weak[i] = (uint8_t)src[3 * per + i];

@@ -44,6 +44,10 @@ extern "C" {
 typedef int (*dpe_pass_runner_fn)(void* user, const DpePassInput* in, const DpePassState* state);
 /* All-gather of `count` floats per rank into recv[world * count], rank-major.  0 = success. */
 typedef int (*dpe_allgather_fn)(void* user, const float* send, size_t count, float* recv);
+/* The same all-gather on DEVICE buffers of the pipeline's GPU (RCCL over xGMI in the CLI); the hook
+ * returns once recv is complete.  With the default runner the depth maps then go from each rank's
+ * HBM-resident state to the others' without a host copy. */
+typedef int (*dpe_allgather_dev_fn)(void* user, const float* dev_send, size_t count, float* dev_recv);
 
 /* Fusion projection tests of one reference view: same contract as dpe_fusion_candidates
  * (include/dpe_mvs.h) over the given views (the default runs the HIP kernel on gpu_index). */
@@ -67,6 +71,8 @@ typedef struct DpePipelineOptions {
   int max_iterations;       /* PatchMatch iterations per pass; 0 = the reference's 3 (main.cpp:527, 554) */
   bool photometric_only;    /* geom_consistency = false on every pass (BASELINE config 2; the
                                reference always runs its geometric passes, main.cpp:549) */
+  dpe_allgather_dev_fn allgather_device; void* allgather_device_user;   /* optional (see above); with the
+                               default runner it is used instead of `allgather` for the depth maps */
 } DpePipelineOptions;
 
 void dpe_pipeline_default_options(DpePipelineOptions* opt);

@@ -180,6 +180,42 @@ void* dpe_pm_device_planes(DpeContext* ctx);
 /* Copies depth (planes.w) into a caller device buffer f32 [H][W] on `stream`. */
 int dpe_pm_export_depth(DpeContext* ctx, float* dev_dst, void* stream);
 
+/*
+ * HBM-resident pipeline state: the reference writes each image's depths.dmb / normals.dmb / weak.bin /
+ * selected_views.bin after a pass (main.cpp:439-446) and its next pass, or a neighbour's geometric
+ * term, reads them back (DPE.cpp:826-911).  Here they stay on the device, keyed by image id.
+ *
+ * dpe_state_save:      after dpe_pm_execute, applies ProcessProblem's epilogue (main.cpp:423-437: depth
+ *                      outside [params.depth_min, depth_max] -> 0 and UNKNOWN) on the device and keeps
+ *                      (world normal, depth, weak, selected views) as image_id's state.
+ * dpe_pm_stage_resident: dpe_pm_stage whose initial state (planes unless FIRST_INIT, weak when use_APD,
+ *                      selected views unless FIRST_INIT) comes from prior_id's state, and whose source depths
+ *                      (geom_consistency) come from the states of in->image_ids[1..]: each rescaled on the
+ *                      device with RescaleMatToTargetSize's nearest rule (DPE.cpp:1146-1165), exactly as the
+ *                      host path rescales them.  in->depths is ignored; in->image_ids is required for geom.
+ * dpe_state_snapshot:  copies every state's depth into its snapshot and makes later resident stages read
+ *                      source depths from the snapshots (the Jacobi schedule: every pass of a round sees the
+ *                      previous round's depths).
+ * dpe_state_fetch:     host copies of a state (any output pointer may be NULL); w, h receive its size.
+ * dpe_state_export_depth / dpe_state_import_depth: the depth map of a state to / from a caller device
+ *                      buffer f32 [h][w] on `stream` (the multi-rank all-gather; an imported id without a
+ *                      pass of its own holds a depth map only).
+ * dpe_state_clear:     frees every state.
+ */
+int dpe_state_save(DpeContext* ctx, int image_id);
+int dpe_pm_stage_resident(DpeContext* ctx, const DpePassInput* in, int prior_id);
+int dpe_state_snapshot(DpeContext* ctx);
+int dpe_state_fetch(DpeContext* ctx, int image_id, int* w, int* h, float* depth, float* normal, uint8_t* weak,
+                    uint32_t* selected_views);
+int dpe_state_export_depth(DpeContext* ctx, int image_id, float* dev_dst, void* stream);
+int dpe_state_import_depth(DpeContext* ctx, int image_id, int w, int h, const float* dev_src, void* stream);
+void dpe_state_clear(DpeContext* ctx);
+/* Context-owned device scratch of `count` floats (slot 0 or 1; grows, kept until dpe_destroy) and a
+ * synchronous copy (kind 0 host->device, 1 device->host, 2 device->device) after all work of the
+ * context: the exchange buffers of the multi-rank schedule without HIP in the caller. */
+float* dpe_device_buffer(DpeContext* ctx, int slot, size_t count);
+int dpe_device_copy(DpeContext* ctx, void* dst, const void* src, size_t bytes, int kind);
+
 /* Kernel classes of one pass, for timing and work accounting. */
 enum {
   DPE_CLASS_SETUP = 0,        /* GenEdgeInform, FindNearestStrongPoint, GenNeighbours, NeigbourUpdate */
