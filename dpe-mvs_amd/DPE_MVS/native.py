@@ -20,6 +20,9 @@ EXPORTED = [
     "dpe_pm_execute", "dpe_pm_fetch", "dpe_pm_run", "dpe_pm_device_planes", "dpe_pm_export_depth",
     "dpe_pm_last_timings", "dpe_set_timing", "dpe_set_counting", "dpe_pm_last_counts",
     "dpe_fusion_stage", "dpe_fusion_candidates",
+    "dpe_pm_stage_resident", "dpe_state_save", "dpe_state_snapshot", "dpe_state_fetch", "dpe_state_export_depth",
+    "dpe_state_import_depth", "dpe_state_clear", "dpe_device_buffer", "dpe_device_copy",
+    "dpe_resize_linear", "dpe_resize_u8", "dpe_canny", "dpe_roberts_threshold",
 ]
 
 CLASSES = ["setup", "init", "strong", "ransac", "weak", "filter", "depth_to_weak", "local_refine"]
@@ -60,6 +63,12 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.dpe_fusion_stage.restype = C.c_int
     lib.dpe_fusion_candidates.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
     lib.dpe_fusion_candidates.restype = C.c_int
+    lib.dpe_resize_linear.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int]
+    lib.dpe_resize_u8.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int]
+    lib.dpe_canny.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_double, C.c_void_p]
+    lib.dpe_roberts_threshold.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
+    for fn in ("dpe_resize_linear", "dpe_resize_u8", "dpe_canny", "dpe_roberts_threshold"):
+        getattr(lib, fn).restype = C.c_int
     return lib
 
 
@@ -107,6 +116,35 @@ class PatchMatchContext:
             self.close()
         except Exception:
             pass
+
+    # EdgeSegment's data-parallel stages (include/dpe_mvs.h; bit-identical to host/edges.cpp)
+    def resize_linear(self, img: np.ndarray, nw: int, nh: int) -> np.ndarray:
+        src = np.ascontiguousarray(img, np.float32)
+        out = np.empty((nh, nw), np.float32)
+        _check(_LIB.dpe_resize_linear(self._ctx, src.ctypes.data, src.shape[1], src.shape[0], out.ctypes.data, nw, nh),
+               "dpe_resize_linear")
+        return out
+
+    def resize_u8(self, img: np.ndarray, nw: int, nh: int) -> np.ndarray:
+        src = np.ascontiguousarray(img, np.uint8)
+        out = np.empty((nh, nw), np.uint8)
+        _check(_LIB.dpe_resize_u8(self._ctx, src.ctypes.data, src.shape[1], src.shape[0], out.ctypes.data, nw, nh),
+               "dpe_resize_u8")
+        return out
+
+    def canny(self, img: np.ndarray, low: float, high: float) -> np.ndarray:
+        src = np.ascontiguousarray(img, np.uint8)
+        out = np.empty_like(src)
+        _check(_LIB.dpe_canny(self._ctx, src.ctypes.data, src.shape[1], src.shape[0], float(low), float(high),
+                              out.ctypes.data), "dpe_canny")
+        return out
+
+    def roberts_threshold(self, img: np.ndarray, thr: int) -> np.ndarray:
+        src = np.ascontiguousarray(img, np.uint8)
+        out = np.empty_like(src)
+        _check(_LIB.dpe_roberts_threshold(self._ctx, src.ctypes.data, src.shape[1], src.shape[0], int(thr), out.ctypes.data),
+               "dpe_roberts_threshold")
+        return out
 
     def set_timing(self, on: bool):
         _LIB.dpe_set_timing(self._ctx, 1 if on else 0)

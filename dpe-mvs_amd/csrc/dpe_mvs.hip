@@ -21,6 +21,7 @@
 #include "pass_refine.h"
 #include "pass_fusion.h"
 #include "pass_sweep.h"
+#include "pass_edges.h"
 
 using namespace dpe;
 
@@ -114,6 +115,13 @@ struct DpeContext {
   int device = 0;
   std::map<int, ResState*> rstore;
   DevArr<float> xbuf[2];             // dpe_device_buffer: exchange buffers of the multi-rank schedule
+  // EdgeSegment stages (dpe_canny / dpe_resize_* / dpe_roberts_threshold): scratch
+  DevArr<uint8_t> e_a, e_b, e_map;
+  DevArr<float> e_fa, e_fb;
+  DevArr<int> e_rows, e_mag, e_itab;
+  DevArr<int16_t> e_dx, e_dy;
+  DevArr<float> e_ftab;
+  DevArr<short> e_stab;
   bool snap_mode = false;            // stage_resident reads source depths from the Jacobi snapshots
   std::vector<CachedImage*> icache;
   uint64_t icache_clock = 0;
@@ -278,6 +286,9 @@ void dpe_destroy(DpeContext* c) {
   for (auto& kv : c->rstore) { kv.second->release(); delete kv.second; }
   c->rstore.clear();
   c->xbuf[0].release(); c->xbuf[1].release();
+  c->e_a.release(); c->e_b.release(); c->e_map.release(); c->e_fa.release(); c->e_fb.release();
+  c->e_rows.release(); c->e_mag.release(); c->e_itab.release(); c->e_dx.release(); c->e_dy.release();
+  c->e_ftab.release(); c->e_stab.release();
   c->cnt.release();
   c->tab_right.release(); c->tab_down.release();
   c->lists.release(); c->row_counts.release(); c->list_totals.release();
@@ -1025,6 +1036,167 @@ extern "C" int dpe_device_copy(DpeContext* c, void* dst, const void* src, size_t
   HIPC(hipStreamSynchronize(c->stream));
   const hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice : (kind == 1 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice);
   HIPC(hipMemcpy(dst, src, bytes, k));
+  return DPE_OK;
+}
+
+// ------------------------------------------------------------------------------ EdgeSegment stages
+namespace {
+// cv::resize INTER_LINEAR CV_32F taps (host/hostio.cpp linear_taps)
+void f32_taps(int n_src, int n_dst, int* s0, int* s1, float* a0, float* a1) {
+  const double scale = 1.0 / ((double)n_dst / n_src);
+  for (int d = 0; d < n_dst; ++d) {
+    float f = (float)((d + 0.5) * scale - 0.5);
+    int sidx = (int)std::floor(f);
+    f -= (float)sidx;
+    if (sidx < 0) { f = 0; sidx = 0; }
+    if (sidx >= n_src - 1) { f = 0; sidx = n_src - 1; }
+    s0[d] = sidx; s1[d] = std::min(sidx + 1, n_src - 1);
+    a0[d] = 1.0f - f; a1[d] = f;
+  }
+}
+// cv::resize INTER_LINEAR CV_8U taps (host/edges.cpp lin_tab): 11-bit weights, cvRound half to even
+int u8_taps(int ssize, int dsize, int* ofs, short* a) {
+  const double scale = 1.0 / ((double)dsize / ssize);
+  int xmax = dsize;
+  for (int d = 0; d < dsize; ++d) {
+    float f = (float)((d + 0.5) * scale - 0.5);
+    int sidx = (int)std::floor(f);
+    f -= (float)sidx;
+    if (sidx < 0) { f = 0; sidx = 0; }
+    if (sidx + 1 >= ssize) {
+      xmax = std::min(xmax, d);
+      if (sidx >= ssize - 1) { f = 0; sidx = ssize - 1; }
+    }
+    ofs[d] = sidx;
+    const float c0 = 1.0f - f, c1 = f;
+    a[2 * d] = (short)std::min(32767, std::max(-32768, (int)std::nearbyint(c0 * 2048.0f)));
+    a[2 * d + 1] = (short)std::min(32767, std::max(-32768, (int)std::nearbyint(c1 * 2048.0f)));
+  }
+  return xmax;
+}
+}  // namespace
+
+extern "C" int dpe_resize_linear(DpeContext* c, const float* src, int w, int h, float* dst, int nw, int nh) {
+  g_err.clear();
+  if (!c || !src || !dst || w < 1 || h < 1 || nw < 1 || nh < 1) { g_err = "dpe_resize_linear: bad argument"; return DPE_ERR_ARG; }
+  if (w == nw && h == nh) { std::memcpy(dst, src, sizeof(float) * (size_t)w * h); return DPE_OK; }
+  HIPC(hipSetDevice(c->device));
+  std::vector<int> it(2 * (size_t)(nw + nh));
+  std::vector<float> ft(2 * (size_t)(nw + nh));
+  f32_taps(w, nw, it.data(), it.data() + nw, ft.data(), ft.data() + nw);
+  f32_taps(h, nh, it.data() + 2 * nw, it.data() + 2 * nw + nh, ft.data() + 2 * nw, ft.data() + 2 * nw + nh);
+  HIPC(c->e_fa.ensure((size_t)w * h)); HIPC(c->e_fb.ensure((size_t)nw * nh));
+  HIPC(c->e_rows.ensure((size_t)h * nw));   // f32 rows stored in the int scratch (same size)
+  HIPC(c->e_itab.ensure(it.size())); HIPC(c->e_ftab.ensure(ft.size()));
+  HIPC(hipMemcpyAsync(c->e_fa.p, src, sizeof(float) * (size_t)w * h, hipMemcpyHostToDevice, c->stream));
+  HIPC(hipMemcpyAsync(c->e_itab.p, it.data(), it.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
+  HIPC(hipMemcpyAsync(c->e_ftab.p, ft.data(), ft.size() * sizeof(float), hipMemcpyHostToDevice, c->stream));
+  float* rows = (float*)c->e_rows.p;
+  const dim3 b(32, 8);
+  k_resize_linear_h<<<dim3((nw + 31) / 32, (h + 7) / 8), b, 0, c->stream>>>(c->e_fa.p, w, h, c->e_itab.p, c->e_itab.p + nw,
+                                                                            c->e_ftab.p, c->e_ftab.p + nw, rows, nw);
+  k_resize_linear_v<<<dim3((nw + 31) / 32, (nh + 7) / 8), b, 0, c->stream>>>(rows, nw, c->e_itab.p + 2 * nw,
+                                                                             c->e_itab.p + 2 * nw + nh, c->e_ftab.p + 2 * nw,
+                                                                             c->e_ftab.p + 2 * nw + nh, c->e_fb.p, nh);
+  HIPC(hipGetLastError());
+  HIPC(hipMemcpyAsync(dst, c->e_fb.p, sizeof(float) * (size_t)nw * nh, hipMemcpyDeviceToHost, c->stream));
+  HIPC(hipStreamSynchronize(c->stream));
+  return DPE_OK;
+}
+
+// device-to-device core of dpe_resize_u8 (src / dst in the context's scratch)
+static int resize_u8_dev(DpeContext* c, const uint8_t* dsrc, int w, int h, uint8_t* ddst, int nw, int nh) {
+  const dim3 b(32, 8);
+  if (w == nw && h == nh) { HIPC(hipMemcpyAsync(ddst, dsrc, (size_t)w * h, hipMemcpyDeviceToDevice, c->stream)); return DPE_OK; }
+  const double scale_x = 1.0 / ((double)nw / w), scale_y = 1.0 / ((double)nh / h);
+  const int isx = (int)std::lround(scale_x), isy = (int)std::lround(scale_y);
+  const bool area_fast = std::fabs(scale_x - isx) < 2.220446049250313e-16 && std::fabs(scale_y - isy) < 2.220446049250313e-16;
+  if (area_fast && isx == 2 && isy == 2) {   // INTER_LINEAR at exactly 1/2 = INTER_AREA's fast path
+    k_resize_u8_half<<<dim3((nw + 31) / 32, (nh + 7) / 8), b, 0, c->stream>>>(dsrc, w, ddst, nw, nh);
+    HIPC(hipGetLastError());
+    return DPE_OK;
+  }
+  std::vector<int> ofs((size_t)nw + nh);
+  std::vector<short> a(2 * ((size_t)nw + nh));
+  const int xmax = u8_taps(w, nw, ofs.data(), a.data());
+  (void)u8_taps(h, nh, ofs.data() + nw, a.data() + 2 * nw);
+  int xv = 0;                                 // VResizeLinear: 16-lane, then 8-lane vector blocks
+  for (; xv <= nw - 16; xv += 16) {}
+  for (; xv < nw - 8; xv += 8) {}
+  HIPC(c->e_rows.ensure((size_t)h * nw)); HIPC(c->e_itab.ensure(ofs.size())); HIPC(c->e_stab.ensure(a.size()));
+  HIPC(hipMemcpyAsync(c->e_itab.p, ofs.data(), ofs.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
+  HIPC(hipMemcpyAsync(c->e_stab.p, a.data(), a.size() * sizeof(short), hipMemcpyHostToDevice, c->stream));
+  k_resize_u8_h<<<dim3((nw + 31) / 32, (h + 7) / 8), b, 0, c->stream>>>(dsrc, w, h, c->e_itab.p, c->e_stab.p, xmax,
+                                                                        c->e_rows.p, nw);
+  k_resize_u8_v<<<dim3((nw + 31) / 32, (nh + 7) / 8), b, 0, c->stream>>>(c->e_rows.p, h, nw, c->e_itab.p + nw,
+                                                                         c->e_stab.p + 2 * nw, xv, ddst, nh);
+  HIPC(hipGetLastError());
+  return DPE_OK;
+}
+
+extern "C" int dpe_resize_u8(DpeContext* c, const uint8_t* src, int w, int h, uint8_t* dst, int nw, int nh) {
+  g_err.clear();
+  if (!c || !src || !dst || w < 1 || h < 1 || nw < 1 || nh < 1) { g_err = "dpe_resize_u8: bad argument"; return DPE_ERR_ARG; }
+  HIPC(hipSetDevice(c->device));
+  HIPC(c->e_a.ensure((size_t)w * h)); HIPC(c->e_b.ensure((size_t)nw * nh));
+  HIPC(hipMemcpyAsync(c->e_a.p, src, (size_t)w * h, hipMemcpyHostToDevice, c->stream));
+  const int r = resize_u8_dev(c, c->e_a.p, w, h, c->e_b.p, nw, nh);
+  if (r != DPE_OK) return r;
+  HIPC(hipMemcpyAsync(dst, c->e_b.p, (size_t)nw * nh, hipMemcpyDeviceToHost, c->stream));
+  HIPC(hipStreamSynchronize(c->stream));
+  return DPE_OK;
+}
+
+extern "C" int dpe_roberts_threshold(DpeContext* c, const uint8_t* src, int w, int h, int thr, uint8_t* dst) {
+  g_err.clear();
+  if (!c || !src || !dst || w < 1 || h < 1) { g_err = "dpe_roberts_threshold: bad argument"; return DPE_ERR_ARG; }
+  HIPC(hipSetDevice(c->device));
+  HIPC(c->e_a.ensure((size_t)w * h)); HIPC(c->e_b.ensure((size_t)w * h));
+  HIPC(hipMemcpyAsync(c->e_a.p, src, (size_t)w * h, hipMemcpyHostToDevice, c->stream));
+  k_roberts_threshold<<<dim3((w + 31) / 32, (h + 7) / 8), dim3(32, 8), 0, c->stream>>>(c->e_a.p, w, h, thr, c->e_b.p);
+  HIPC(hipGetLastError());
+  HIPC(hipMemcpyAsync(dst, c->e_b.p, (size_t)w * h, hipMemcpyDeviceToHost, c->stream));
+  HIPC(hipStreamSynchronize(c->stream));
+  return DPE_OK;
+}
+
+extern "C" int dpe_canny(DpeContext* c, const uint8_t* src, int w, int h, double low_thresh, double high_thresh, uint8_t* dst) {
+  g_err.clear();
+  if (!c || !src || !dst || w < 1 || h < 1) { g_err = "dpe_canny: bad argument"; return DPE_ERR_ARG; }
+  HIPC(hipSetDevice(c->device));
+  if (low_thresh > high_thresh) std::swap(low_thresh, high_thresh);   // canny.cpp threshold handling
+  low_thresh = std::min(32767.0, low_thresh);
+  high_thresh = std::min(32767.0, high_thresh);
+  if (low_thresh > 0) low_thresh *= low_thresh;
+  if (high_thresh > 0) high_thresh *= high_thresh;
+  const int low = (int)std::floor(low_thresh), high = (int)std::floor(high_thresh);
+  const int ms = w + 2;
+  const size_t L = (size_t)w * h, M = (size_t)ms * (h + 2);
+  HIPC(c->e_a.ensure(L)); HIPC(c->e_dx.ensure(L)); HIPC(c->e_dy.ensure(L)); HIPC(c->e_mag.ensure(M)); HIPC(c->e_map.ensure(M));
+  HIPC(hipMemcpyAsync(c->e_a.p, src, L, hipMemcpyHostToDevice, c->stream));
+  const dim3 b(32, 8), g((ms + 31) / 32, (h + 2 + 7) / 8);
+  k_canny_sobel<<<g, b, 0, c->stream>>>(c->e_a.p, w, h, c->e_dx.p, c->e_dy.p, c->e_mag.p);
+  k_canny_nms<<<g, b, 0, c->stream>>>(c->e_dx.p, c->e_dy.p, c->e_mag.p, w, h, low, high, c->e_map.p);
+  HIPC(hipGetLastError());
+  std::vector<uint8_t> map(M);
+  HIPC(hipMemcpyAsync(map.data(), c->e_map.p, M, hipMemcpyDeviceToHost, c->stream));
+  HIPC(hipStreamSynchronize(c->stream));
+  // hysteresis: 8-connected growth through candidates from every strong candidate (any order: the
+  // closure is the same set)
+  std::vector<size_t> stack;
+  stack.reserve(L / 8 + 16);
+  for (size_t i = 0; i < M; ++i) if (map[i] == 2) stack.push_back(i);
+  const long off[8] = {-ms - 1, -ms, -ms + 1, -1, 1, ms - 1, ms, ms + 1};
+  while (!stack.empty()) {
+    const size_t i = stack.back();
+    stack.pop_back();
+    for (long o : off) {
+      const size_t j = (size_t)((long)i + o);
+      if (!map[j]) { map[j] = 2; stack.push_back(j); }
+    }
+  }
+  for (int y = 0; y < h; ++y)
+    for (int x = 0; x < w; ++x) dst[(size_t)y * w + x] = map[(size_t)(y + 1) * ms + x + 1] == 2 ? 255 : 0;
   return DPE_OK;
 }
 

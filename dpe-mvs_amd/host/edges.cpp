@@ -377,10 +377,38 @@ void fix_frame(uint8_t* d, int cols, int rows) {
 }
 }  // namespace
 
+namespace {
+// the data-parallel stages on the device when one is given (bit-identical), else on the host
+bool stage_resize_u8(const EdgeDevice* dev, const uint8_t* src, int w, int h, uint8_t* dst, int nw, int nh, std::string& err) {
+  if (!dev || !dev->ctx) { resize_u8(src, w, h, dst, nw, nh); return true; }
+  std::lock_guard<std::mutex> lk(*dev->mu);
+  if (dpe_resize_u8(dev->ctx, src, w, h, dst, nw, nh) != 0) { err = dpe_last_error(); return false; }
+  return true;
+}
+bool stage_canny(const EdgeDevice* dev, const uint8_t* src, int w, int h, double low, double high, uint8_t* dst, std::string& err) {
+  if (!dev || !dev->ctx) { canny_l2(src, w, h, low, high, dst); return true; }
+  std::lock_guard<std::mutex> lk(*dev->mu);
+  if (dpe_canny(dev->ctx, src, w, h, low, high, dst) != 0) { err = dpe_last_error(); return false; }
+  return true;
+}
+bool stage_roberts_threshold(const EdgeDevice* dev, const uint8_t* src, int w, int h, int thr, uint8_t* dst, std::string& err) {
+  if (!dev || !dev->ctx) { roberts(src, w, h, dst); threshold_binary(dst, (size_t)w * h, thr); return true; }
+  std::lock_guard<std::mutex> lk(*dev->mu);
+  if (dpe_roberts_threshold(dev->ctx, src, w, h, thr, dst) != 0) { err = dpe_last_error(); return false; }
+  return true;
+}
+bool stage_resize_linear(const EdgeDevice* dev, const float* src, int w, int h, float* dst, int nw, int nh, std::string& err) {
+  if (!dev || !dev->ctx) { resize_linear(src, w, h, dst, nw, nh); return true; }
+  std::lock_guard<std::mutex> lk(*dev->mu);
+  if (dpe_resize_linear(dev->ctx, src, w, h, dst, nw, nh) != 0) { err = dpe_last_error(); return false; }
+  return true;
+}
+}  // namespace
+
 // EdgeSegment (DPE.cpp:129-291) for mode 0 (edges: CV_8UC1 0/255) and mode 1 (labels: CV_32SC1,
 // -1 = small region, 0 = boundary, > 0 region).
 bool edge_segment(int scale, const uint8_t* src, int cols, int rows, int mode, bool use_canny, bool high_res, Mat& out,
-                  std::string& err) {
+                  std::string& err, const EdgeDevice* dev) {
   if (cols < 4 || rows < 4) { err = "EdgeSegment: image too small"; return false; }
   const int robthr = high_res ? 4 : 6;
   const int weak_tex_num = (int)(1.0 * rows * cols / (1024 << scale << scale));
@@ -391,19 +419,18 @@ bool edge_segment(int scale, const uint8_t* src, int cols, int rows, int mode, b
     int w = cols, h = rows;
     if (high_res) {
       std::vector<uint8_t> t((size_t)(w / 2) * (h / 2));
-      resize_u8(down.data(), w, h, t.data(), w / 2, h / 2);
+      if (!stage_resize_u8(dev, down.data(), w, h, t.data(), w / 2, h / 2, err)) return false;
       down.swap(t); w /= 2; h /= 2;
     }
     {
       std::vector<uint8_t> t((size_t)(w / 2) * (h / 2));
-      resize_u8(down.data(), w, h, t.data(), w / 2, h / 2);
+      if (!stage_resize_u8(dev, down.data(), w, h, t.data(), w / 2, h / 2, err)) return false;
       down.swap(t); w /= 2; h /= 2;
     }
     const int mn = std::min(w, h);
     const int houthr = (int)(mn / 30.0), min_line_length = (int)(mn / 30.0), max_line_gap = (int)(mn / 30.0);
     dst.resize((size_t)w * h);
-    roberts(down.data(), w, h, dst.data());
-    threshold_binary(dst.data(), dst.size(), robthr);
+    if (!stage_roberts_threshold(dev, down.data(), w, h, robthr, dst.data(), err)) return false;
     std::vector<int> lab0((size_t)w * h);
     std::vector<int> cnt0;
     connect(dst.data(), w, h, lab0.data(), cnt0);
@@ -436,7 +463,7 @@ bool edge_segment(int scale, const uint8_t* src, int cols, int rows, int mode, b
     const float sigma = 0.67f;
     const int t1 = (int)((1 - sigma) * (float)median_val), t2 = median_val;
     dst.resize((size_t)cols * rows);
-    canny_l2(src, cols, rows, t1, t2, dst.data());
+    if (!stage_canny(dev, src, cols, rows, t1, t2, dst.data(), err)) return false;
     dw = cols; dh = rows;
   }
   int ow, oh;
@@ -446,7 +473,7 @@ bool edge_segment(int scale, const uint8_t* src, int cols, int rows, int mode, b
     ow = (int)std::round(cols * factor); oh = (int)std::round(rows * factor);
   }
   std::vector<uint8_t> rs((size_t)ow * oh);
-  resize_u8(dst.data(), dw, dh, rs.data(), ow, oh);
+  if (!stage_resize_u8(dev, dst.data(), dw, dh, rs.data(), ow, oh, err)) return false;
   threshold_binary(rs.data(), rs.size(), robthr);
   fix_frame(rs.data(), ow, oh);
   if (mode == 0) {
@@ -466,7 +493,7 @@ bool edge_segment(int scale, const uint8_t* src, int cols, int rows, int mode, b
 // GetProblemEdges (main.cpp:331-388): edges_<s>.dmb from the scaled image (32-bit float resize,
 // then round to 8 bits), labels_<s>.dmb from the full-resolution image; files that exist are kept.
 bool get_problem_edges(const GrayImage& full, int scale_size, const std::string& result_folder, bool use_edge,
-                       bool use_label, bool high_res, std::string& err) {
+                       bool use_label, bool high_res, std::string& err, const EdgeDevice* dev) {
   int scale = 0;
   while ((1 << scale) < scale_size) scale++;
   const fs::path rf(result_folder);
@@ -478,11 +505,11 @@ bool get_problem_edges(const GrayImage& full, int scale_size, const std::string&
       const float factor = 1.0f / (float)scale_size;
       const int nw = (int)std::round(full.w * factor), nh = (int)std::round(full.h * factor);
       std::vector<float> f(full.px.begin(), full.px.end()), g((size_t)nw * nh);
-      resize_linear(f.data(), full.w, full.h, g.data(), nw, nh);
+      if (!stage_resize_linear(dev, f.data(), full.w, full.h, g.data(), nw, nh, err)) return false;
       std::vector<uint8_t> s(g.size());
       for (size_t i = 0; i < g.size(); ++i) s[i] = sat_u8(cv_round(g[i]));
       Mat m;
-      if (!edge_segment(scale, s.data(), nw, nh, 0, true, high_res, m, err)) return false;
+      if (!edge_segment(scale, s.data(), nw, nh, 0, true, high_res, m, err, dev)) return false;
       if (!write_bin_mat(ep.string(), m, err)) return false;
     }
   }
@@ -490,7 +517,7 @@ bool get_problem_edges(const GrayImage& full, int scale_size, const std::string&
     const fs::path lp = rf / ("labels_" + std::to_string(scale) + ".dmb");
     if (!fs::exists(lp)) {
       Mat m;
-      if (!edge_segment(scale, full.px.data(), full.w, full.h, 1, false, high_res, m, err)) return false;
+      if (!edge_segment(scale, full.px.data(), full.w, full.h, 1, false, high_res, m, err, dev)) return false;
       if (!write_bin_mat(lp.string(), m, err)) return false;
     }
   }

@@ -3,6 +3,7 @@
 #pragma once
 #include <array>
 #include <cstdint>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -57,10 +58,17 @@ void connect(const uint8_t* img, int w, int h, int* label, std::vector<int>& lab
 void draw_line(uint8_t* img, int w, int h, int x0, int y0, int x1, int y1, uint8_t value);
 void hough_lines_p(const uint8_t* img, int w, int h, double rho, double theta, int threshold, double min_len,
                    double max_gap, std::vector<std::array<int, 4>>& lines);
+// The device for EdgeSegment's data-parallel stages (dpe_resize_linear / dpe_resize_u8 / dpe_canny /
+// dpe_roberts_threshold, bit-identical to the host functions above): one context shared by the host
+// threads behind `mu`.  ctx == nullptr: every stage on the host.
+struct EdgeDevice {
+  DpeContext* ctx = nullptr;
+  std::mutex* mu = nullptr;
+};
 bool edge_segment(int scale, const uint8_t* src, int cols, int rows, int mode, bool use_canny, bool high_res, Mat& out,
-                  std::string& err);
+                  std::string& err, const EdgeDevice* dev = nullptr);
 bool get_problem_edges(const GrayImage& full, int scale_size, const std::string& result_folder, bool use_edge,
-                       bool use_label, bool high_res, std::string& err);
+                       bool use_label, bool high_res, std::string& err, const EdgeDevice* dev = nullptr);
 
 // fusion.cpp: RunFusion (DPE.cpp:1220-1370) / ExportPointCloud (DPE.cpp:532-572)
 struct FusionView {

@@ -29,6 +29,7 @@
 #include <fstream>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <sstream>
 #include <thread>
 
@@ -105,6 +106,27 @@ class ImageCache {
     }
     w = it->second.w; h = it->second.h;
     return &it->second.px;
+  }
+  // decodes the images not cached yet on `nt` host threads (independent files; same pixels as full())
+  bool prefetch(const std::vector<int>& ids, int nt, std::string& err) {
+    std::vector<int> todo;
+    for (int id : ids)
+      if (!full_.count(id) && std::find(todo.begin(), todo.end(), id) == todo.end()) todo.push_back(id);
+    std::vector<GrayImage> g(todo.size());
+    std::vector<std::string> e(todo.size());
+    nt = std::max(1, std::min<int>(nt, (int)todo.size()));
+    std::vector<std::thread> pool;
+    for (int t = 0; t < nt; ++t)
+      pool.emplace_back([&, t]() {
+        for (size_t k = t; k < todo.size(); k += nt)
+          read_gray((fs::path(folder_) / "images" / (fmt_index(todo[k]) + ".jpg")).string(), g[k], e[k]);
+      });
+    for (auto& th : pool) th.join();
+    for (size_t k = 0; k < todo.size(); ++k) {
+      if (!e[k].empty()) { err = e[k]; return false; }
+      full_.emplace(todo[k], Level{g[k].w, g[k].h, std::vector<float>(g[k].px.begin(), g[k].px.end())});
+    }
+    return true;
   }
   const std::vector<float>* level(int idx, int scale, int& w, int& h, std::string& err) {
     int fw, fh;
@@ -397,6 +419,16 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
   std::vector<Problem> problems;
   if (!generate_sample_list(dense, problems, err)) return 1;
   ImageCache cache(dense);
+  {   // every image of the run decoded once, on the host threads
+    std::vector<int> ids;
+    for (const Problem& p : problems) {
+      ids.push_back(p.ref_image_id);
+      for (int s : p.src_image_ids) ids.push_back(s);
+    }
+    const int nt = (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
+    std::string perr;
+    if (!cache.prefetch(ids, nt, perr)) { err = "Images may error, check it! " + perr; std::fprintf(stderr, "Images may error, check it!\n"); return 1; }
+  }
   {   // CheckImages (main.cpp:310-329)
     int w0 = 0, h0 = 0;
     bool ok = !problems.empty();
@@ -473,6 +505,10 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
     }
     const int nt = (int)std::max<size_t>(1, std::min<size_t>({grey.size(), (size_t)16,
                                                               (size_t)std::max(1u, std::thread::hardware_concurrency())}));
+    // the data-parallel stages (resize, Sobel / NMS, Roberts) on the runner's GPU, the scan-order and
+    // RNG-order parts (hysteresis walk, Connect, HoughLinesP) on the host threads
+    std::mutex edge_mu;
+    EdgeDevice edev{runner.ctx, &edge_mu};
     std::vector<std::string> terr(nt);
     std::vector<std::thread> pool;
     for (int t = 0; t < nt; ++t)
@@ -481,7 +517,7 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
           const Problem& p = problems[blocks[rank][k]];
           for (int i = 0; i < round_num && terr[t].empty(); ++i)
             if (!get_problem_edges(grey[k], (int)std::pow(2, round_num - 1 - i), p.result_folder, p.params.use_edge,
-                                   p.params.use_label, p.params.high_res_img, terr[t]) && terr[t].empty())
+                                   p.params.use_label, p.params.high_res_img, terr[t], &edev) && terr[t].empty())
               terr[t] = "EdgeSegment failed";
         }
       });

@@ -216,6 +216,24 @@ void dpe_state_clear(DpeContext* ctx);
 float* dpe_device_buffer(DpeContext* ctx, int slot, size_t count);
 int dpe_device_copy(DpeContext* ctx, void* dst, const void* src, size_t bytes, int kind);
 
+/*
+ * EdgeSegment's data-parallel stages on the device (DPE.cpp:129-291 calls them through OpenCV; the
+ * host restatement is host/edges.cpp, and these are bit-identical to it).  HOST buffers, synchronous,
+ * on the context's stream (use one context per thread, or serialise the calls).
+ *   dpe_resize_linear      cv::resize(INTER_LINEAR) of CV_32FC1             == dpe_host_resize_linear
+ *   dpe_resize_u8          cv::resize(INTER_LINEAR) of CV_8UC1 (INTER_AREA fast path at exactly 1/2)
+ *                                                                          == dpe_host_resize_u8
+ *   dpe_canny              cv::Canny(L2gradient, aperture 3): Sobel, magnitude, non-maximum
+ *                          suppression and the strong candidates on the device, the 8-connected
+ *                          hysteresis walk on the host                      == dpe_host_canny
+ *   dpe_roberts_threshold  Roberts (DPE.cpp:9-25) + cv::threshold(thr, 255, THRESH_BINARY)
+ * Connect (DPE.cpp:27-127) and HoughLinesP are scan-order / RNG-order dependent and stay on the host.
+ */
+int dpe_resize_linear(DpeContext* ctx, const float* src, int w, int h, float* dst, int nw, int nh);
+int dpe_resize_u8(DpeContext* ctx, const uint8_t* src, int w, int h, uint8_t* dst, int nw, int nh);
+int dpe_canny(DpeContext* ctx, const uint8_t* src, int w, int h, double low, double high, uint8_t* dst);
+int dpe_roberts_threshold(DpeContext* ctx, const uint8_t* src, int w, int h, int thr, uint8_t* dst);
+
 /* Kernel classes of one pass, for timing and work accounting. */
 enum {
   DPE_CLASS_SETUP = 0,        /* GenEdgeInform, FindNearestStrongPoint, GenNeighbours, NeigbourUpdate */
