@@ -9,6 +9,7 @@
 //   * cuRAND states (48 B/px + curand_init) are replaced by counter-based Philox;
 //   * errors are return codes (no exit()).
 #include <hip/hip_runtime.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -56,6 +57,15 @@ static constexpr int kTexD2W = DPE_TEX_D2W, kTexLR = DPE_TEX_LR;
 namespace {
 
 thread_local std::string g_err;
+
+// roctx ranges (SURVEY.md §5 tracing): host-side enqueue regions of the pass, visible in
+// `rocprofv3 --marker-trace` beside the kernel trace
+struct Range {
+  explicit Range(const char* m) { roctxRangePushA(m); }
+  ~Range() { roctxRangePop(); }
+  Range(const Range&) = delete;
+  Range& operator=(const Range&) = delete;
+};
 
 #define HIPC(expr)                                                                  \
   do {                                                                              \
@@ -421,6 +431,7 @@ extern "C" int dpe_pm_stage_resident(DpeContext* c, const DpePassInput* in, int 
 
 static int stage_impl(DpeContext* c, const DpePassInput* in, const StageSrc& src) {
   g_err.clear();
+  Range range_(src.st ? "dpe_pm_stage" : "dpe_pm_stage_resident");
   const DpePassState* st = src.st;
   if (in->num_images > DPE_MAX_IMAGES) { g_err = "dpe_pm_stage: num_images > 32 (DPE.cpp:762)"; return DPE_ERR_TOO_MANY; }
   if (in->num_images < 2 || in->width <= 0 || in->height <= 0) { g_err = "dpe_pm_stage: bad shape"; return DPE_ERR_ARG; }
@@ -624,6 +635,7 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   g_err.clear();
   if (!c) { g_err = "dpe_pm_execute: null context"; return DPE_ERR_ARG; }
   if (!c->staged) { g_err = "dpe_pm_execute: call dpe_pm_stage first"; return DPE_ERR_STATE; }
+  Range range_("dpe_pm_execute");
   HIPC(hipSetDevice(c->device));
   hipStream_t s = stream_ ? (hipStream_t)stream_ : c->stream;
   // a previous execute, possibly on another stream, still uses the working buffers this one resets
@@ -659,14 +671,20 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   int nev = 0;
   std::vector<int> ev_class(timing ? max_slots : 0);
   for (int k = 0; k <= DPE_NUM_CLASSES; ++k) c->launches[k] = 0;
+  static const char* const kClassName[DPE_NUM_CLASSES] = {"setup", "init", "strong", "ransac", "weak", "filter",
+                                                           "depth_to_weak", "local_refine"};
   auto begin = [&](int cls) -> DevBufs {
+    roctxRangePushA(kClassName[cls]);
     DevBufs Bc = B;
     if (c->counting) Bc.cnt = c->cnt.p + 4 * cls;
     c->launches[cls]++;
     if (timing && nev < max_slots) { ev_class[nev] = cls; (void)hipEventRecord(c->ev[2 * nev], s); }
     return Bc;
   };
-  auto end = [&]() { if (timing && nev < max_slots) { (void)hipEventRecord(c->ev[2 * nev + 1], s); nev++; } };
+  auto end = [&]() {
+    if (timing && nev < max_slots) { (void)hipEventRecord(c->ev[2 * nev + 1], s); nev++; }
+    roctxRangePop();
+  };
 
   if (timing) (void)hipEventRecord(c->ev_start, s);
   // initial state (the reference uploads it in CudaSpaceInitialization, DPE.cpp:964-1015)
@@ -846,6 +864,7 @@ extern "C" int dpe_pm_fetch(DpeContext* c, const DpePassState* st) {
   if (!c || !st) { g_err = "dpe_pm_fetch: null argument"; return DPE_ERR_ARG; }
   if (!c->staged) { g_err = "dpe_pm_fetch: nothing staged"; return DPE_ERR_STATE; }
   HIPC(hipSetDevice(c->device));
+  Range range_("dpe_pm_fetch");
   const size_t L = (size_t)c->hc.W * c->hc.H;
   HIPC(wait_pending(c));
   HIPC(hipStreamSynchronize(c->stream));
@@ -918,6 +937,7 @@ extern "C" int dpe_state_save(DpeContext* c, int image_id) {
   if (!c) { g_err = "dpe_state_save: null context"; return DPE_ERR_ARG; }
   if (!c->staged) { g_err = "dpe_state_save: nothing staged"; return DPE_ERR_STATE; }
   HIPC(hipSetDevice(c->device));
+  Range range_("dpe_state_save");
   const int W = c->hc.W, H = c->hc.H;
   const size_t L = (size_t)W * H;
   if (c->pending) HIPC(hipStreamWaitEvent(c->stream, c->ev_done, 0));   // after the pass that wrote the outputs
@@ -1164,6 +1184,7 @@ extern "C" int dpe_canny(DpeContext* c, const uint8_t* src, int w, int h, double
   g_err.clear();
   if (!c || !src || !dst || w < 1 || h < 1) { g_err = "dpe_canny: bad argument"; return DPE_ERR_ARG; }
   HIPC(hipSetDevice(c->device));
+  Range range_("dpe_canny");
   if (low_thresh > high_thresh) std::swap(low_thresh, high_thresh);   // canny.cpp threshold handling
   low_thresh = std::min(32767.0, low_thresh);
   high_thresh = std::min(32767.0, high_thresh);

@@ -21,6 +21,8 @@
 // viz medium results (ignored).
 #include "host.h"
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -492,6 +494,7 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
     std::printf("There are %d resolution stages for coarse-to-fine processing!\n", round_num);
     std::printf("Iteration nums: %d\n", round_num * 4);
   }
+  roctxRangePushA("GetProblemEdges");
   {   // GetProblemEdges for every scale of the schedule (main.cpp:494-501); images are independent,
       // so a pool of host threads takes them round-robin (the decode cache is filled first)
     std::vector<GrayImage> grey(blocks[rank].size());
@@ -523,6 +526,7 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
       });
     for (auto& th : pool) th.join();
     for (auto& e : terr) if (!e.empty()) { fail(e); break; }
+    roctxRangePop();
     if (world == 1 && failed) return 1;
   }
   for (auto& p : problems) p.params.max_scale_size = std::max(1, (int)std::pow(2, round_num - 1));
@@ -549,7 +553,12 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
         if (opt.max_iterations > 0) p.params.max_iterations = opt.max_iterations;
         if (opt.photometric_only) p.params.geom_consistency = false;
         std::string perr;
-        if (!process_problem(p, cache, states, depth_src, opt, runner, perr)) { fail(perr); break; }
+        const std::string rname = "ProcessProblem round " + std::to_string(i) + " pass " + std::to_string(j + 1) +
+                                  " image " + std::to_string(p.ref_image_id);
+        roctxRangePushA(rname.c_str());
+        const bool ok = process_problem(p, cache, states, depth_src, opt, runner, perr);
+        roctxRangePop();
+        if (!ok) { fail(perr); break; }
         if (!resident) {
           const ImageState& s = states[p.ref_image_id];
           depth_cur[p.ref_image_id] = DepthMap{s.w, s.h, s.depth};
