@@ -827,6 +827,7 @@ template <int U8, int C>
 __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassConst* __restrict__ pcp, DevBufs B, int iter,
                                                    const int* __restrict__ list, const int* __restrict__ nlist_p) {
   extern __shared__ float4 lds4[];
+  static_assert(C == 16 || C == 32, "the per-pixel phases give lanes 0..8 the patch sums and lanes 8..15 the alias rows");
   constexpr int P = 64 / C;
   const PassConst& pc = *pcp;
   const int nlist = *nlist_p;

@@ -7,7 +7,7 @@ pids=()
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -w $flags -shared \
-    -o lib/variants/$name.so csrc/dpe_mvs.hip &
+    -o lib/variants/$name.so csrc/dpe_mvs.hip -L/opt/rocm/lib -lrocprofiler-sdk-roctx -Wl,-rpath,/opt/rocm/lib &
   pids+=($!)
 done
 rc=0
