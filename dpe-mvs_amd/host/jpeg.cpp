@@ -104,7 +104,7 @@ void idct_islow(const int* coef /* dequantised, natural order */, uint8_t* out, 
   for (int c = 0; c < 8; ++c) {                     // pass 1: columns
     const int* in = coef + c;
     if (in[8] == 0 && in[16] == 0 && in[24] == 0 && in[32] == 0 && in[40] == 0 && in[48] == 0 && in[56] == 0) {
-      const int64_t dc = (int64_t)in[0] << PASS1_BITS;
+      const int64_t dc = (int64_t)in[0] * (1 << PASS1_BITS);   // LEFT_SHIFT as a multiply: no UB on negatives
       for (int r = 0; r < 8; ++r) ws[r * 8 + c] = dc;
       continue;
     }
@@ -113,8 +113,8 @@ void idct_islow(const int* coef /* dequantised, natural order */, uint8_t* out, 
     int64_t tmp2 = z1 + z3 * (-F_1_847759065);
     int64_t tmp3 = z1 + z2 * F_0_765366865;
     z2 = in[0]; z3 = in[32];
-    int64_t tmp0 = (z2 + z3) << CONST_BITS;
-    int64_t tmp1 = (z2 - z3) << CONST_BITS;
+    int64_t tmp0 = (z2 + z3) * ((int64_t)1 << CONST_BITS);
+    int64_t tmp1 = (z2 - z3) * ((int64_t)1 << CONST_BITS);
     const int64_t tmp10 = tmp0 + tmp3, tmp13 = tmp0 - tmp3, tmp11 = tmp1 + tmp2, tmp12 = tmp1 - tmp2;
     tmp0 = in[56]; tmp1 = in[40]; tmp2 = in[24]; tmp3 = in[8];
     z1 = tmp0 + tmp3; z2 = tmp1 + tmp2; z3 = tmp0 + tmp2;
@@ -143,8 +143,8 @@ void idct_islow(const int* coef /* dequantised, natural order */, uint8_t* out, 
     int64_t z1 = (z2 + z3) * F_0_541196100;
     int64_t tmp2 = z1 + z3 * (-F_1_847759065);
     int64_t tmp3 = z1 + z2 * F_0_765366865;
-    int64_t tmp0 = (w[0] + w[4]) << CONST_BITS;
-    int64_t tmp1 = (w[0] - w[4]) << CONST_BITS;
+    int64_t tmp0 = (w[0] + w[4]) * ((int64_t)1 << CONST_BITS);
+    int64_t tmp1 = (w[0] - w[4]) * ((int64_t)1 << CONST_BITS);
     const int64_t tmp10 = tmp0 + tmp3, tmp13 = tmp0 - tmp3, tmp11 = tmp1 + tmp2, tmp12 = tmp1 - tmp2;
     tmp0 = w[7]; tmp1 = w[5]; tmp2 = w[3]; tmp3 = w[1];
     z1 = tmp0 + tmp3; z2 = tmp1 + tmp2; z3 = tmp0 + tmp2;
