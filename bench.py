@@ -149,10 +149,16 @@ def end_to_end(local_rank: int, n_images: int, W: int, H: int, scene=None) -> di
         t0 = time.perf_counter()
         dpe_mvs(d, local_rank, False, False, False, True, False, False, False)
         dt = time.perf_counter() - t0
+        import ctypes
+        from DPE_MVS import pipeline
+        phases = (ctypes.c_double * 5)()
+        pipeline.lib().dpe_pipeline_last_timings(phases, 5)
     finally:
         shutil.rmtree(d, ignore_errors=True)
     return {"images": n_images, "width": W, "height": H, "src_views": min(9, n_images - 1), "passes_per_image": 8,
             "wall_s": round(dt, 3), "mpix_s": round(n_images * W * H / dt / 1e6, 4),
+            "phases_s": {"decode": round(phases[1], 3), "edge_segment_prepass": round(phases[2], 3),
+                         "passes": round(phases[3], 3), "outputs": round(phases[4], 3)},
             "note": "dpe_mvs() wall clock incl. JPEG decode, EdgeSegment, host I/O; value is per-pass HBM-resident"}
 
 

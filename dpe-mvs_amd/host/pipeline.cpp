@@ -24,6 +24,7 @@
 #include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -42,6 +43,9 @@ namespace {
 
 thread_local std::string g_err;
 const char* kOutName = "DPE";
+// wall seconds of the last run's phases: total, decode, GetProblemEdges pre-pass, passes, outputs + fusion
+double g_times[5] = {0, 0, 0, 0, 0};
+double now_s() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
 
 struct Problem {   // main.h:108-118
   int index = 0, ref_image_id = 0;
@@ -411,6 +415,8 @@ bool write_outputs(const Problem& p, const ImageState& s, const DpePipelineOptio
 int run(const char* dense_folder, const DpePipelineOptions& opt) {
   std::string& err = g_err;
   err.clear();
+  const double t_start = now_s();
+  for (double& t : g_times) t = 0.0;
   const int world = std::max(1, opt.world_size), rank = opt.rank;
   if (world > 1 && !opt.allgather) { err = "world_size > 1 needs an all-gather"; return 1; }
   if (rank < 0 || rank >= world) { err = "bad rank"; return 1; }
@@ -421,6 +427,7 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
   std::vector<Problem> problems;
   if (!generate_sample_list(dense, problems, err)) return 1;
   ImageCache cache(dense);
+  double t_mark = now_s();
   {   // every image of the run decoded once, on the host threads
     std::vector<int> ids;
     for (const Problem& p : problems) {
@@ -494,6 +501,8 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
     std::printf("There are %d resolution stages for coarse-to-fine processing!\n", round_num);
     std::printf("Iteration nums: %d\n", round_num * 4);
   }
+  g_times[1] = now_s() - t_mark;
+  t_mark = now_s();
   roctxRangePushA("GetProblemEdges");
   {   // GetProblemEdges for every scale of the schedule (main.cpp:494-501); images are independent,
       // so a pool of host threads takes them round-robin (the decode cache is filled first)
@@ -529,6 +538,8 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
     roctxRangePop();
     if (world == 1 && failed) return 1;
   }
+  g_times[2] = now_s() - t_mark;
+  t_mark = now_s();
   for (auto& p : problems) p.params.max_scale_size = std::max(1, (int)std::pow(2, round_num - 1));
   std::map<int, ImageState> states;
   std::map<int, DepthMap> depth_cur;
@@ -622,6 +633,8 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
       iteration_index++;
     }
   }
+  g_times[3] = now_s() - t_mark;
+  t_mark = now_s();
   if (resident && !failed)   // the final states come back from HBM once
     for (int pi : blocks[rank]) {
       std::string ferr;
@@ -738,6 +751,8 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
         fs::remove(fs::path(problems[pi].result_folder) / ("labels_" + std::to_string(j) + ".dmb"), ec2);
       }
   if (opt.verbose && rank == 0) std::printf("All done\n");
+  g_times[4] = now_s() - t_mark;
+  g_times[0] = now_s() - t_start;
   return 0;
 }
 
@@ -768,5 +783,11 @@ int dpe_run_pipeline(const char* dense_folder, const DpePipelineOptions* opt) {
 }
 
 const char* dpe_pipeline_last_error(void) { return dpe_host::g_err.c_str(); }
+
+int dpe_pipeline_last_timings(double* out, int n) {
+  int k = 0;
+  for (; k < n && k < 5; ++k) out[k] = dpe_host::g_times[k];
+  return k;
+}
 
 }  // extern "C"

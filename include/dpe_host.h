@@ -79,6 +79,10 @@ void dpe_pipeline_default_options(DpePipelineOptions* opt);
 /* RunDPEPipeline: 0 on success, nonzero on failure (message in dpe_pipeline_last_error()). */
 int dpe_run_pipeline(const char* dense_folder, const DpePipelineOptions* opt);
 const char* dpe_pipeline_last_error(void);
+/* Wall seconds of the last successful dpe_run_pipeline on this process: [0] total, [1] image decode,
+ * [2] the GetProblemEdges pre-pass (EdgeSegment), [3] the passes, [4] outputs + fusion.  Returns the
+ * number of entries written (<= n, at most 5). */
+int dpe_pipeline_last_timings(double* out, int n);
 
 /* Grey-level decode of a JPEG (baseline/extended, luma plane) or binary PGM.  Writes up to `cap`
  * bytes into `out` (pass NULL/0 to query the size) and the size into *w, *h.  0 on success. */
