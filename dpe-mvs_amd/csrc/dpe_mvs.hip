@@ -23,6 +23,7 @@
 #include "pass_fusion.h"
 #include "pass_sweep.h"
 #include "pass_edges.h"
+#include "tap_launch.h"
 
 using namespace dpe;
 
@@ -31,28 +32,6 @@ static const int kDefaultXcdRows = 1;
 #define DPE_WEAK_LANES 16
 #endif
 static constexpr int kWeakLanes = DPE_WEAK_LANES;   // lanes per weak pixel in k_weak_coop (16 or 32)
-// source-image layout of each kernel for 8-bit grey-level images (pass_common.h TEX_*): TEX_F16
-// issues fewer VALU ops per tap, TEX_U8 touches half the bytes (better for scattered gathers),
-// TEX_P16 is in between (half the bytes, 2 more ops per tap than TEX_F16, one unaligned 8-B load).
-// A/B on the bench pass (two runs): P16 strong -0.85 / -0.32 ms; DepthToWeak -0.9 / +0.9 (noise),
-// LocalRefine +0.2 / -0.2, weak +3 (the 8-B unaligned gathers of its scattered patches cost more)
-#ifndef DPE_TEX_STRONG
-#define DPE_TEX_STRONG TEX_P16
-#endif
-#ifndef DPE_TEX_WEAK
-#define DPE_TEX_WEAK TEX_U8
-#endif
-#ifndef DPE_TEX_D2W
-#define DPE_TEX_D2W TEX_F16
-#endif
-#ifndef DPE_TEX_LR
-#define DPE_TEX_LR TEX_F16
-#endif
-#ifndef DPE_TEX_INIT
-#define DPE_TEX_INIT TEX_F16
-#endif
-static constexpr int kTexInit = DPE_TEX_INIT, kTexStrong = DPE_TEX_STRONG, kTexWeak = DPE_TEX_WEAK;
-static constexpr int kTexD2W = DPE_TEX_D2W, kTexLR = DPE_TEX_LR;
 
 namespace {
 
@@ -764,13 +743,7 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
     const int P = edge ? 4 : 8, C = edge ? 16 : 8;
     const size_t lds = (size_t)4 * strong_lds_per_wave(P, C, nv) * sizeof(float);
     const unsigned grid = (unsigned)((L / 2 + 1 + 4 * P - 1) / (4 * P));
-    if (edge) {
-      if (c->img8) k_strong_coop<kTexStrong, true><<<grid, 256, lds, s>>>(dpc, Bs, it, lst, cnt);
-      else k_strong_coop<TEX_F32, true><<<grid, 256, lds, s>>>(dpc, Bs, it, lst, cnt);
-    } else {
-      if (c->img8) k_strong_coop<kTexStrong, false><<<grid, 256, lds, s>>>(dpc, Bs, it, lst, cnt);
-      else k_strong_coop<TEX_F32, false><<<grid, 256, lds, s>>>(dpc, Bs, it, lst, cnt);
-    }
+    launch_strong(edge, c->img8, grid, lds, s, dpc, Bs, it, lst, cnt);
   };
   for (int it = 0; it < pc.P.max_iterations; ++it) {
     for (int colour = 0; colour < 2; ++colour) {
@@ -814,16 +787,10 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   for (int colour = 0; colour < 2; ++colour) k_filter<<<hg, hb, 0, s>>>(dpc, Bc, colour);   // hb: 32 x 4 = kFilterThreads
   end();
   Bc = begin(DPE_CLASS_DEPTH_TO_WEAK);
-  if (c->img8) k_depth_to_weak<kTexD2W><<<(unsigned)((L + 3) / 4), 256, 0, s>>>(dpc, Bc);
-  else k_depth_to_weak<TEX_F32><<<(unsigned)((L + 3) / 4), 256, 0, s>>>(dpc, Bc);
+  launch_depth_to_weak(c->img8, (long)L, s, dpc, Bc);
   end();
   Bc = begin(DPE_CLASS_LOCAL_REFINE);
-  {
-    const unsigned g = (unsigned)((L + 4 * kLrPix - 1) / (4 * kLrPix));
-    const size_t lds = (size_t)4 * kLrPix * 12 * nv * 2 * sizeof(float);
-    if (c->img8) k_local_refine_jobs<kTexLR><<<g, 256, lds, s>>>(dpc, Bc);
-    else k_local_refine_jobs<TEX_F32><<<g, 256, lds, s>>>(dpc, Bc);
-  }
+  launch_local_refine(c->img8, (long)L, nv, s, dpc, Bc);
   end();
   HIPC(hipGetLastError());
   if (timing && nev > 0) {

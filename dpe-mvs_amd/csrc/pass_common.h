@@ -359,6 +359,10 @@ DEV float sample_quad8(const uint8_t* __restrict__ q, int W, int H, float sx, fl
   texel_rows<T>(q + (size_t)((uy >> 8) * tex_stride<T>(W) + (ux >> 8)) * tex_bytes<T>(), (float)(ux & 255), r0, r1);
   return __builtin_fmaf(ay, r1 - r0, r0);
 }
+// The default 36-tap patch (strong radius 5, increment 2) that the tabulated fast paths serve.
+#ifndef DPE_FAST_PATCH
+#define DPE_FAST_PATCH(pc) ((pc).P.strong_radius == 5 && (pc).P.strong_increment == 2)
+#endif
 // Minimum waves per SIMD the tap-heavy kernels are compiled for (register cap 512 / waves).
 #ifndef DPE_TAP_WAVES
 #define DPE_TAP_WAVES 4

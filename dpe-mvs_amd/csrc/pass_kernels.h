@@ -481,7 +481,7 @@ __global__ void __launch_bounds__(256) k_random_init(const PassConst* __restrict
   PIX2D_FULL();
   const DpeCamera& c0 = pc.cams[0];
   const int N = pc.N;
-  const bool fast = pc.P.strong_radius == 5 && pc.P.strong_increment == 2;
+  const bool fast = DPE_FAST_PATCH(pc);
   Patch36 P;
   if (fast) make_patch36(P, pc, B, x, y); else { P.px = x; P.py = y; }
   if (pc.P.state == DPE_FIRST_INIT) {

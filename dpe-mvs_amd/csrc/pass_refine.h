@@ -304,7 +304,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_depth_to_weak(const Pass
   if (valid == 0) { if (lane == 0) B.weak[center] = DPE_UNKNOWN; return; }
   base_line /= valid;
   const float disp = c0.K[0] * base_line / od;
-  const bool fast = pc.P.strong_radius == 5 && pc.P.strong_increment == 2;
+  const bool fast = DPE_FAST_PATCH(pc);
   float* pw = s_patch[wave];
   if (fast) patch_lds_build<64>(pw, pc, B, x, y, lane);
   wave_sync();
@@ -378,7 +378,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_local_refine_jobs(const 
   const long base = ((long)xcd_remap(blockIdx.x, gridDim.x, B.xcd_rows * 16 * ((pc.W + 15) / 16)) * 4 + wave) * kLrPix;
   if (base >= L) return;                          // wave-uniform
   const DpeCamera& c0 = pc.cams[0];
-  const bool fast = pc.P.strong_radius == 5 && pc.P.strong_increment == 2;
+  const bool fast = DPE_FAST_PATCH(pc);
   const uint32_t vmask = (pc.N - 1) >= 32 ? 0xFFFFFFFFu : ((1u << (pc.N - 1)) - 1u);
   const int nv = pc.N - 1;
   float* res = s_dyn + (size_t)wave * kLrPix * 12 * nv * 2;   // res[((p * 12 + h) * nv + k) * 2 + {0, 1}]
@@ -494,6 +494,8 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_local_refine_jobs(const 
   if ((double)(t[11] - min_cost) > 0.1) B.planes[pix].w = best_depth;
 }
 
+// (non-template kernels: defined only in the translation unit that launches them, dpe_mvs.hip)
+#ifndef DPE_TAP_TU
 // ------------------------------------------------------------------------------ FindNearestStrongPoint
 // Ring search r = 0..100 (DPE.cu:2855-2889) in O(1) per ring with two tables:
 //   next_right[y*W + x] = smallest x' >= x with weak(x', y) == STRONG (W if none)
@@ -556,5 +558,7 @@ __global__ void k_find_nearest_strong(const PassConst* __restrict__ pcp, DevBufs
   }
   B.nearest[center] = res;
 }
+
+#endif  // DPE_TAP_TU
 
 }  // namespace dpe

@@ -356,7 +356,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_strong_coop(const PassCo
 
   const float* __restrict__ costs_s = B.costs_snap;
   const float4* __restrict__ planes_s = B.planes_snap;
-  const bool fast = pc.P.strong_radius == 5 && pc.P.strong_increment == 2;
+  const bool fast = DPE_FAST_PATCH(pc);
   bool on_edge = false;
   PHASE_BEGIN();
   // ---- phase 1: reference patch + candidate scans

@@ -1,0 +1,43 @@
+// tap_launch.hip — launches of the strong sweep, DepthToWeak and LocalRefine, compiled as their own
+// translation unit with LLVM's occupancy-first iterative scheduler
+// (-mllvm -amdgpu-sched-strategy=iterative-maxocc, see the Makefile).
+//
+// A scheduler is chosen per compilation, so the kernels that gain from it live here.  At the
+// 4 waves/SIMD of __launch_bounds__(256, DPE_TAP_WAVES) the default scheduler hoists the gathers of
+// the unrolled 36-tap loop until it needs more than 128 VGPRs and spills (strong 56, DepthToWeak
+// 68, LocalRefine 36 B/lane of scratch, whose stores reach HBM); the iterative scheduler fits the
+// same code in 106-110 VGPRs with no scratch.  Interleaved A/B on the bench pass (bit-identical
+// outputs): strong -0.4 / -0.6 ms, DepthToWeak -0.6 / -0.6 ms, LocalRefine +0.05 ms.  The weak
+// sweep is slower under it (+1.2 ms, more scratch) and stays in dpe_mvs.hip with the default.
+#define DPE_TAP_TU 1
+#include "tap_launch.h"
+#include "pass_refine.h"
+#include "pass_sweep.h"
+
+namespace dpe {
+
+void launch_strong(bool edge, bool img8, unsigned grid, size_t lds, hipStream_t s, const PassConst* dpc,
+                   const DevBufs& B, int it, const int* list, const int* count) {
+  if (edge) {
+    if (img8) k_strong_coop<kTexStrong, true><<<grid, 256, lds, s>>>(dpc, B, it, list, count);
+    else k_strong_coop<TEX_F32, true><<<grid, 256, lds, s>>>(dpc, B, it, list, count);
+  } else {
+    if (img8) k_strong_coop<kTexStrong, false><<<grid, 256, lds, s>>>(dpc, B, it, list, count);
+    else k_strong_coop<TEX_F32, false><<<grid, 256, lds, s>>>(dpc, B, it, list, count);
+  }
+}
+
+void launch_depth_to_weak(bool img8, long L, hipStream_t s, const PassConst* dpc, const DevBufs& B) {
+  const unsigned g = (unsigned)((L + 3) / 4);
+  if (img8) k_depth_to_weak<kTexD2W><<<g, 256, 0, s>>>(dpc, B);
+  else k_depth_to_weak<TEX_F32><<<g, 256, 0, s>>>(dpc, B);
+}
+
+void launch_local_refine(bool img8, long L, int nv, hipStream_t s, const PassConst* dpc, const DevBufs& B) {
+  const unsigned g = (unsigned)((L + 4 * kLrPix - 1) / (4 * kLrPix));
+  const size_t lds = (size_t)4 * kLrPix * 12 * nv * 2 * sizeof(float);
+  if (img8) k_local_refine_jobs<kTexLR><<<g, 256, lds, s>>>(dpc, B);
+  else k_local_refine_jobs<TEX_F32><<<g, 256, lds, s>>>(dpc, B);
+}
+
+}  // namespace dpe

@@ -1,13 +1,26 @@
 #!/bin/bash
 # Build A/B variants of lib/libdpe_mvs.so into dpe-mvs_amd/lib/variants/<name>.so (in parallel).
 # Usage: tools/build_variants.sh "name:-DFLAG=1 -DOTHER=2" "base:" ...
+# The flags apply to both translation units; TAP_SCHED (env) overrides the scheduler of
+# csrc/tap_launch.hip (default: the Makefile's iterative-maxocc).
 cd "$(dirname "$0")/../dpe-mvs_amd" || exit 1
-mkdir -p lib/variants
+mkdir -p lib/variants obj/variants
+TAP_SCHED=${TAP_SCHED--mllvm -amdgpu-sched-strategy=iterative-maxocc}
+HF="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -w"
+build() {
+  local name=$1 flags=$2
+  /opt/rocm/bin/hipcc $HF $flags -c -o obj/variants/$name.main.o csrc/dpe_mvs.hip &
+  local a=$!
+  /opt/rocm/bin/hipcc $HF $flags $TAP_SCHED -c -o obj/variants/$name.tap.o csrc/tap_launch.hip &
+  local b=$!
+  wait $a && wait $b || return 1
+  /opt/rocm/bin/hipcc $HF -shared -o lib/variants/$name.so obj/variants/$name.main.o obj/variants/$name.tap.o \
+    -L/opt/rocm/lib -lrocprofiler-sdk-roctx -Wl,-rpath,/opt/rocm/lib
+}
 pids=()
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -w $flags -shared \
-    -o lib/variants/$name.so csrc/dpe_mvs.hip -L/opt/rocm/lib -lrocprofiler-sdk-roctx -Wl,-rpath,/opt/rocm/lib &
+  build "$name" "$flags" &
   pids+=($!)
 done
 rc=0

@@ -1,14 +1,17 @@
 #!/usr/bin/env python3
-"""Per-kernel register / scratch / occupancy table of lib/libdpe_mvs.so's source
-(hipcc -Rpass-analysis=kernel-resource-usage).  Usage: python tools/ru.py [extra hipcc flags...]"""
+"""Per-kernel register / scratch / occupancy table of lib/libdpe_mvs.so's two translation units
+(hipcc -Rpass-analysis=kernel-resource-usage; csrc/tap_launch.hip with the Makefile's scheduler).
+Usage: python tools/ru.py [extra hipcc flags...]"""
 import re
 import subprocess
 import sys
 
 ROOT = __file__.rsplit("/tools/", 1)[0]
-cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
-       "-Rpass-analysis=kernel-resource-usage", "-c", "-o", "/tmp/dpe_ru.o", ROOT + "/dpe-mvs_amd/csrc/dpe_mvs.hip"] + sys.argv[1:]
-out = subprocess.run(cmd, capture_output=True, text=True).stderr
+base = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
+        "-Rpass-analysis=kernel-resource-usage", "-c", "-o", "/tmp/dpe_ru.o"]
+out = subprocess.run(base + [ROOT + "/dpe-mvs_amd/csrc/dpe_mvs.hip"] + sys.argv[1:], capture_output=True, text=True).stderr
+out += subprocess.run(base + ["-mllvm", "-amdgpu-sched-strategy=iterative-maxocc", ROOT + "/dpe-mvs_amd/csrc/tap_launch.hip"]
+                      + sys.argv[1:], capture_output=True, text=True).stderr
 rows, cur = [], None
 for line in out.splitlines():
     m = re.search(r"remark:\s+(Function Name|VGPRs|AGPRs|ScratchSize \[bytes/lane\]|Occupancy \[waves/SIMD\]|LDS Size \[bytes/block\]): (\S+)", line)
