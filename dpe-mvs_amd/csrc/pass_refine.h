@@ -200,6 +200,16 @@ DEV void lds_row(const float* pw, int px, int py, const PassConst& pc, const Dev
 #ifndef DPE_CLAMP_ELIDE
 #define DPE_CLAMP_ELIDE 1
 #endif
+#ifndef DPE_ELIDE_UNIFORM
+#define DPE_ELIDE_UNIFORM 1
+#endif
+// clamp-free tap loop in the strong sweep's pools and LocalRefine (A/B knobs)
+#ifndef DPE_STRONG_ELIDE
+#define DPE_STRONG_ELIDE false
+#endif
+#ifndef DPE_LR_ELIDE
+#define DPE_LR_ELIDE false
+#endif
 template <int U8, bool ELIDE = false>
 DEV float ncc_old_lds(const float* pw, float s_ref, float s_rr, float s_w, int px, int py, const PassConst& pc,
                       const DevBufs& B, int v, const float4& pl) {
@@ -209,7 +219,16 @@ DEV float ncc_old_lds(const float* pw, float s_ref, float s_rr, float s_w, int p
   float a[3];
   if (rcp_range_ok(H, (float)(px - 5), (float)(px + 5), (float)(py - 5), (float)(py + 5))) {
 #if DPE_CLAMP_ELIDE
-    if (ELIDE && patch_inside(H, (float)(px - 5), (float)(px + 5), (float)(py - 5), (float)(py + 5), pc.W, pc.H))
+    // wave-uniform choice: the clamped loop gives the same bits for patches inside the image, so a
+    // wave whose lanes disagree runs that loop once instead of both loops under partial masks
+    bool in = false;
+    if constexpr (ELIDE) {
+      in = patch_inside(H, (float)(px - 5), (float)(px + 5), (float)(py - 5), (float)(py + 5), pc.W, pc.H);
+#if DPE_ELIDE_UNIFORM
+      in = __all(in);
+#endif
+    }
+    if (in)
       lds_taps<U8, true, true>(pw, px, py, pc, B, v, H, a);
     else
 #endif
@@ -456,7 +475,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_local_refine_jobs(const 
     const float4 tp = s_hyp[wave][p][h];
     const float* sm = s_sum[wave][p];
     float* rr = res + ((p * 12 + h) * nv + k) * 2;
-    rr[0] = ncc_old_any<U8>(fast, s_patch[wave][p], sm[0], sm[1], sm[2], jx, jy, pc, B, si, tp);
+    rr[0] = ncc_old_any<U8, DPE_LR_ELIDE>(fast, s_patch[wave][p], sm[0], sm[1], sm[2], jx, jy, pc, B, si, tp);
     if (pc.P.geom_consistency) rr[1] = geom_cost_at(pc, B, jx, jy, si, s_fw[wave][p][h]);
   }
   wave_sync();

@@ -451,7 +451,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_strong_coop(const PassCo
       const float4 pl = cpl_all[q * (C + 1) + slot];
       const float* sm = sums_all + q * 4;
       cost_all[(q * (C + 1) + slot) * nv + v - 1] =
-          ncc_old_any<U8>(fast, pw_all + q * 108, sm[0], sm[1], sm[2], qx, qy, pc, B, v, pl);
+          ncc_old_any<U8, DPE_STRONG_ELIDE>(fast, pw_all + q * 108, sm[0], sm[1], sm[2], qx, qy, pc, B, v, pl);
     }
     if (split) {
       float* tb = wl + strong_lds_per_wave(P, C, nv) - kTailJobs * 18;   // [job][row][3]
@@ -636,7 +636,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_strong_coop(const PassCo
       const int h = r % 5, k = r / 5;                      // the 5 hypotheses of one view adjacent
       const int cq = list[wbase + q];
       const float* sm = sums_all + q * 4;
-      ref_all[(q * 5 + h) * nv + k] = ncc_old_any<U8>(fast, pw_all + q * 108, sm[0], sm[1], sm[2], cq % W, cq / W, pc,
+      ref_all[(q * 5 + h) * nv + k] = ncc_old_any<U8, DPE_STRONG_ELIDE>(fast, pw_all + q * 108, sm[0], sm[1], sm[2], cq % W, cq / W, pc,
                                                       B, iq[C + 16 + k] + 1, hyp_all[q * 5 + h]);
     }
   }

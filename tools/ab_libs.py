@@ -29,7 +29,7 @@ for path in libs:
     ctxs.append((path, lib, ctx, bufs))
 res = {path: [] for path in libs}
 ref = None
-for rnd in range(3):
+for rnd in range(int(os.environ.get("AB_ROUNDS", "3"))):
     for path, lib, ctx, bufs in ctxs:
         assert lib.dpe_pm_execute(ctx, None) == 0
         assert lib.dpe_pm_fetch(ctx, C.byref(bufs.st)) == 0
@@ -46,7 +46,7 @@ import time  # noqa: E402
 wall = {path: [] for path in libs}
 for path, lib, ctx, bufs in ctxs:
     lib.dpe_set_timing(ctx, 0)
-for rnd in range(3):
+for rnd in range(int(os.environ.get("AB_ROUNDS", "3"))):
     for path, lib, ctx, bufs in ctxs:
         torch.cuda.synchronize()
         t0 = time.perf_counter()
