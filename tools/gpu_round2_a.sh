@@ -2,7 +2,7 @@
 cd "$GRAFT_REPO_ROOT"
 export PYTHONUNBUFFERED=1
 mkdir -p gpurun_out
-timeout -k 10 1140 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 900 --timeout-method thread --durations=0 > gpurun_out/r2_gputest.log 2>&1
+timeout -k 10 1140 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 900 --timeout-method thread --durations=0 > gpurun_out/${1:-r2}_gputest.log 2>&1
 rc=$?
-echo "pytest rc=$rc" >> gpurun_out/r2_gputest.log
+echo "pytest rc=$rc" >> gpurun_out/${1:-r2}_gputest.log
 exit $rc
