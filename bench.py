@@ -328,7 +328,9 @@ def main():
         "config": {"workload": f"DTU-like {Wd}x{Hd}, 9 src views, full-res REFINE_ITER pass + geometric consistency "
                                "(BASELINE configs[2])",
                    "width": Wd, "height": Hd, "num_images": NV_, "max_iterations": 3,
-                   "parallelism": f"reference-image sharding x{world}" + (" + RCCL depth all-gather" if world > 1 else "")},
+                   "parallelism": f"reference-image sharding x{world}" + (
+                       (" + RCCL depth all-gather" if dist.get_backend() == "nccl" else f" + {dist.get_backend()} depth "
+                        "all-gather (rehearsal)") if world > 1 else "")},
         "roofline": {
             "bound": "valu",
             "kernel": f"k_{dom}",
