@@ -220,3 +220,41 @@ def test_zero_iterations_joins_the_aux_stream(ctx):
     st = synthetic.gt_state(sc)
     inp = synthetic.pass_input(sc, p, depths=synthetic.src_depths(sc))
     assert_same(ctx.run(inp, st), oracle.run_pass(inp, st), "max_iterations 0")
+
+
+def _random_case(seed):
+    """A seeded random pass configuration: size, views, pass type and the schedule's switches
+    (rotate_time, labels, edge limit, radius map, resolution class, iterations, peak radius,
+    RANSAC threshold, candidate scheme, geometric consistency, NCC-New patch)."""
+    r = np.random.default_rng(1000 + seed)
+    W, H, N = int(r.integers(24, 161)), int(r.integers(24, 121)), int(r.integers(2, 11))
+    p = _abi.default_params()
+    p.max_iterations = int(r.integers(1, 4))
+    kind = ("first", "refine_init", "refine_iter")[int(r.integers(0, 3))]
+    if kind == "first":
+        p.state = _abi.FIRST_INIT; p.use_APD = False; p.use_edge = False; p.geom_consistency = False
+    else:
+        p.state = _abi.REFINE_INIT if kind == "refine_init" else _abi.REFINE_ITER
+        p.geom_consistency = kind == "refine_iter" and bool(r.integers(0, 2))
+        apd = bool(r.integers(0, 4))                      # 1 in 4: the ACMH scheme
+        p.use_APD = apd; p.use_edge = apd
+        p.rotate_time = int((1, 2, 4)[int(r.integers(0, 3))])
+        p.ransac_threshold = float(np.float32(r.uniform(0.005, 0.01)))
+        p.weak_peak_radius = int(r.integers(2, 7))
+        p.use_label = bool(r.integers(0, 2)); p.use_limit = bool(r.integers(0, 4))
+        p.use_radius = bool(r.integers(0, 4)); p.high_res_img = bool(r.integers(0, 2))
+        if r.integers(0, 4) == 0:                         # untabulated NCC-New neighbour patches
+            p.weak_radius = int(r.integers(3, 7)); p.weak_increment = int(r.integers(2, 4))
+    return W, H, N, kind, p
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_gpu_matches_oracle_random_configs(ctx, seed):
+    W, H, N, kind, p = _random_case(seed)
+    sc = synthetic.make_scene(W, H, N, seed=synthetic.SCENE_SEED + seed)
+    st = synthetic.first_init_state(sc) if kind == "first" else synthetic.gt_state(sc, seed=seed)
+    inp = synthetic.pass_input(sc, p, depths=synthetic.src_depths(sc) if p.geom_consistency else None, seed=seed + 3)
+    what = f"seed {seed}: {W}x{H}x{N} {kind} it={p.max_iterations} rot={p.rotate_time} apd={p.use_APD} " \
+           f"geom={p.geom_consistency} label={p.use_label} limit={p.use_limit} radius={p.use_radius} " \
+           f"hires={p.high_res_img} weak={p.weak_radius}/{p.weak_increment}"
+    assert_same(ctx.run(inp, st), oracle.run_pass(inp, st), what)
