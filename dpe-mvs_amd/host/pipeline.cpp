@@ -640,11 +640,20 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
       std::string ferr;
       if (!fetch_state(runner.ctx, problems[pi].ref_image_id, states[problems[pi].ref_image_id], ferr)) { fail(ferr); break; }
     }
-  for (int pi : blocks[rank]) {
-    if (failed) break;
-    const Problem& p = problems[pi];
-    std::string werr;
-    if (!write_outputs(p, states[p.ref_image_id], opt, werr)) { fail(werr); break; }
+  if (!failed) {   // each image's .npy files on their own host thread (independent files)
+    const auto& blk = blocks[rank];
+    const int nt = (int)std::min<size_t>(blk.size(), std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency())));
+    std::vector<std::string> werr(blk.size());
+    std::vector<std::thread> pool;
+    for (int t = 0; t < nt; ++t)
+      pool.emplace_back([&, t]() {
+        for (size_t k = t; k < blk.size(); k += nt) {
+          const Problem& p = problems[blk[k]];
+          if (!write_outputs(p, states.at(p.ref_image_id), opt, werr[k]) && werr[k].empty()) werr[k] = "write failed";
+        }
+      });
+    for (auto& th : pool) th.join();
+    for (auto& e : werr) if (!e.empty()) { fail(e); break; }
   }
   if (failed && !(world > 1 && opt.fusion)) { err = first_err; return 1; }   // else reported at the exchange
   if (opt.fusion) {   // RunFusion (main.cpp:578-580)
