@@ -198,6 +198,9 @@ void dpe_params_default(DpePatchMatchParams* p) {   // main.h:78-106
 
 const char* dpe_last_error(void) { return g_err.c_str(); }
 
+#ifndef DPE_FORK_AFTER_INIT
+#define DPE_FORK_AFTER_INIT 1
+#endif
 DpeContext* dpe_create(int device) {
   g_err.clear();
   int n = 0;
@@ -717,17 +720,29 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
     k_list_count<0><<<(pc.half_rows + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p);
     k_list_scan<0><<<1, 256, 0, s>>>(dpc, c->row_counts.p, c->list_totals.p);
     k_list_fill<0><<<(pc.half_rows + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p, c->lists.p, list_stride);
-    HIPC(hipEventRecord(c->ev_fork, s));
-    HIPC(hipStreamWaitEvent(a, c->ev_fork, 0));
   }
-  k_gen_neighbours<<<(unsigned)((L + 255) / 256), 256, 0, a>>>(dpc, Bc, weak_list, c->list_totals.p + 4);
-  k_neighbour_update<<<fg, fb, 0, a>>>(dpc, Bc);
-  if (overlap) {
-    k_list_count<2><<<(pc.half_rows + 3) / 4, 256, 0, a>>>(dpc, Bc, c->row_counts.p);
-    k_list_scan<2><<<1, 64, 0, a>>>(dpc, c->row_counts.p, c->list_totals.p + 5);
-    k_list_fill<2><<<(pc.half_rows + 3) / 4, 256, 0, a>>>(dpc, Bc, c->row_counts.p, failed_list, list_stride);
-    HIPC(hipEventRecord(c->ev_join, a));
-  } else {
+  // GenNeighbours + NeigbourUpdate (+ the failed-pixel list on the aux stream).  Forked after
+  // RandomInitialization: launched beside it, GenNeighbours' ~4.7 K long waves (all resident at once)
+  // starved it of registers (0.86 -> 8.5 ms in a kernel trace of the overlapped pass)
+  const DevBufs Bgn = Bc;
+  auto launch_gn = [&]() -> int {
+    if (overlap) {
+      HIPC(hipEventRecord(c->ev_fork, s));
+      HIPC(hipStreamWaitEvent(a, c->ev_fork, 0));
+    }
+    k_gen_neighbours<<<(unsigned)((L + 255) / 256), 256, 0, a>>>(dpc, Bgn, weak_list, c->list_totals.p + 4);
+    k_neighbour_update<<<fg, fb, 0, a>>>(dpc, Bgn);
+    if (overlap) {
+      k_list_count<2><<<(pc.half_rows + 3) / 4, 256, 0, a>>>(dpc, Bgn, c->row_counts.p);
+      k_list_scan<2><<<1, 64, 0, a>>>(dpc, c->row_counts.p, c->list_totals.p + 5);
+      k_list_fill<2><<<(pc.half_rows + 3) / 4, 256, 0, a>>>(dpc, Bgn, c->row_counts.p, failed_list, list_stride);
+      HIPC(hipEventRecord(c->ev_join, a));
+    }
+    return 0;
+  };
+  const bool gn_after_init = overlap && DPE_FORK_AFTER_INIT;
+  if (!gn_after_init) { const int r = launch_gn(); if (r) return r; }
+  if (!overlap) {
     // per-colour pixel lists of the sweeps (weak_info is fixed from here until DepthToWeak)
     k_list_count<0><<<(pc.half_rows + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p);
     k_list_scan<0><<<1, 256, 0, s>>>(dpc, c->row_counts.p, c->list_totals.p);
@@ -737,6 +752,7 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   Bc = begin(DPE_CLASS_INIT);
   if (c->img8) k_random_init<kTexInit><<<fg, fb, 0, s>>>(dpc, Bc); else k_random_init<TEX_F32><<<fg, fb, 0, s>>>(dpc, Bc);
   end();
+  if (gn_after_init) { const int r = launch_gn(); if (r) return r; }
   HIPC(hipGetLastError());
   auto strong_sweep = [&](const DevBufs& Bs, int it, const int* lst, const int* cnt) {
     const bool edge = pc.P.use_edge;
