@@ -116,7 +116,7 @@ struct DpeContext {
   uint64_t icache_clock = 0;
   hipStream_t stream = nullptr;
   hipStream_t aux = nullptr;         // GenNeighbours beside the first strong half-sweep
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_ei = nullptr;
   hipEvent_t ev_done = nullptr;      // end of the last dpe_pm_execute's work on its stream
   bool pending = false;              // ev_done recorded and not yet waited for
   bool staged = false;
@@ -198,6 +198,9 @@ void dpe_params_default(DpePatchMatchParams* p) {   // main.h:78-106
 
 const char* dpe_last_error(void) { return g_err.c_str(); }
 
+#ifndef DPE_EARLY_FORK
+#define DPE_EARLY_FORK 1
+#endif
 #ifndef DPE_FORK_AFTER_INIT
 #define DPE_FORK_AFTER_INIT 1
 #endif
@@ -217,12 +220,14 @@ DpeContext* dpe_create(int device) {
   if (hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_ei, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming) != hipSuccess ||
       hipEventCreate(&c->ev_start) != hipSuccess) {
     g_err = "dpe_create: aux stream";
     if (c->ev_start) (void)hipEventDestroy(c->ev_start);
     if (c->ev_done) (void)hipEventDestroy(c->ev_done);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+    if (c->ev_ei) (void)hipEventDestroy(c->ev_ei);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->aux) (void)hipStreamDestroy(c->aux);
     (void)hipStreamDestroy(c->stream);
@@ -285,7 +290,7 @@ void dpe_destroy(DpeContext* c) {
   c->tab_right.release(); c->tab_down.release();
   c->lists.release(); c->row_counts.release(); c->list_totals.release();
   (void)hipStreamSynchronize(c->aux);
-  (void)hipEventDestroy(c->ev_fork); (void)hipEventDestroy(c->ev_join);
+  (void)hipEventDestroy(c->ev_fork); (void)hipEventDestroy(c->ev_join); (void)hipEventDestroy(c->ev_ei);
   (void)hipStreamDestroy(c->aux);
   (void)hipStreamDestroy(c->stream);
   delete c;
@@ -691,18 +696,34 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   DevBufs Bc;
 
   // RunPatchMatch launch sequence (DPE.cu:3150-3226)
-  Bc = begin(DPE_CLASS_SETUP);
-  k_gen_edge_inform<<<fg, fb, 0, s>>>(dpc, Bc);
-  k_strong_tables_rows<<<(H + 63) / 64, 64, 0, s>>>(dpc, Bc, c->tab_right.p);
-  k_strong_tables_cols<<<(W + 63) / 64, 64, 0, s>>>(dpc, Bc, c->tab_down.p);
-  k_find_nearest_strong<<<fg, fb, 0, s>>>(dpc, Bc, c->tab_right.p, c->tab_down.p);
-  // list of all WEAK pixels (list slot 4), then GenNeighbours one thread per WEAK pixel
+  // DPE_OVERLAP=0 keeps one stream (profiling runs whose per-kernel durations must not overlap)
+  static const bool overlap_env = [] { const char* e = getenv("DPE_OVERLAP"); return !(e && atoi(e) == 0); }();
+  // (the join into `s` sits in the first strong half-sweep, so a pass without iterations keeps one stream)
+  const bool overlap = overlap_env && !timing && !c->counting && pc.P.max_iterations >= 1;
   const long list_stride = (long)(L / 2 + 64);
+  // early fork: the whole setup chain (GenEdgeInform .. GenNeighbours) on the aux stream, beside
+  // RandomInitialization; the first strong half-sweep waits for GenEdgeInform's edge rays only
+  const bool early = overlap && DPE_EARLY_FORK;
+  const hipStream_t se = early ? c->aux : s;
+  Bc = begin(DPE_CLASS_SETUP);
+  if (early) {   // pre-GenNeighbours sweep lists (the colour-0 strong list is the one used)
+    k_list_count<0><<<(pc.half_rows + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p);
+    k_list_scan<0><<<1, 256, 0, s>>>(dpc, c->row_counts.p, c->list_totals.p);
+    k_list_fill<0><<<(pc.half_rows + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p, c->lists.p, list_stride);
+    HIPC(hipEventRecord(c->ev_fork, s));
+    HIPC(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
+  }
+  k_gen_edge_inform<<<fg, fb, 0, se>>>(dpc, Bc);
+  if (early) HIPC(hipEventRecord(c->ev_ei, se));
+  k_strong_tables_rows<<<(H + 63) / 64, 64, 0, se>>>(dpc, Bc, c->tab_right.p);
+  k_strong_tables_cols<<<(W + 63) / 64, 64, 0, se>>>(dpc, Bc, c->tab_down.p);
+  k_find_nearest_strong<<<fg, fb, 0, se>>>(dpc, Bc, c->tab_right.p, c->tab_down.p);
+  // list of all WEAK pixels (list slot 4), then GenNeighbours one thread per WEAK pixel
   int* weak_list = c->lists.p + 4 * list_stride;
   int* failed_list = weak_list + L + 64;             // MODE 2 list (slot 5 of list_totals)
-  k_list_count<1><<<(H + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p);
-  k_list_scan<1><<<1, 64, 0, s>>>(dpc, c->row_counts.p, c->list_totals.p + 4);
-  k_list_fill<1><<<(H + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p, weak_list, (long)L);
+  k_list_count<1><<<(H + 3) / 4, 256, 0, se>>>(dpc, Bc, c->row_counts.p + 2 * (size_t)H + 2);
+  k_list_scan<1><<<1, 64, 0, se>>>(dpc, c->row_counts.p + 2 * (size_t)H + 2, c->list_totals.p + 4);
+  k_list_fill<1><<<(H + 3) / 4, 256, 0, se>>>(dpc, Bc, c->row_counts.p + 2 * (size_t)H + 2, weak_list, (long)L);
   // GenNeighbours + NeigbourUpdate only decide which WEAK pixels join the strong lists; nothing the
   // first strong half-sweep (iteration 0, colour 0) or RandomInitialization reads is written by
   // them, and GenNeighbours reads the staged planes, not the ones those two rewrite.  So they run
@@ -711,12 +732,8 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   // same half-sweep (same snapshot) once the streams join.  Pixels of one half-sweep are
   // independent, so this is the reference's order of results.  Timed / counting executes keep
   // one stream (per-class events).
-  // DPE_OVERLAP=0 keeps one stream (profiling runs whose per-kernel durations must not overlap)
-  static const bool overlap_env = [] { const char* e = getenv("DPE_OVERLAP"); return !(e && atoi(e) == 0); }();
-  // (the join into `s` sits in the first strong half-sweep, so a pass without iterations keeps one stream)
-  const bool overlap = overlap_env && !timing && !c->counting && pc.P.max_iterations >= 1;
   hipStream_t a = overlap ? c->aux : s;
-  if (overlap) {   // pre-GenNeighbours sweep lists (the colour-0 strong list is the one used)
+  if (overlap && !early) {   // pre-GenNeighbours sweep lists (the colour-0 strong list is the one used)
     k_list_count<0><<<(pc.half_rows + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p);
     k_list_scan<0><<<1, 256, 0, s>>>(dpc, c->row_counts.p, c->list_totals.p);
     k_list_fill<0><<<(pc.half_rows + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p, c->lists.p, list_stride);
@@ -726,7 +743,7 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   // starved it of registers (0.86 -> 8.5 ms in a kernel trace of the overlapped pass)
   const DevBufs Bgn = Bc;
   auto launch_gn = [&]() -> int {
-    if (overlap) {
+    if (overlap && !early) {
       HIPC(hipEventRecord(c->ev_fork, s));
       HIPC(hipStreamWaitEvent(a, c->ev_fork, 0));
     }
@@ -740,7 +757,7 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
     }
     return 0;
   };
-  const bool gn_after_init = overlap && DPE_FORK_AFTER_INIT;
+  const bool gn_after_init = overlap && !early && DPE_FORK_AFTER_INIT;
   if (!gn_after_init) { const int r = launch_gn(); if (r) return r; }
   if (!overlap) {
     // per-colour pixel lists of the sweeps (weak_info is fixed from here until DepthToWeak)
@@ -753,6 +770,7 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   if (c->img8) k_random_init<kTexInit><<<fg, fb, 0, s>>>(dpc, Bc); else k_random_init<TEX_F32><<<fg, fb, 0, s>>>(dpc, Bc);
   end();
   if (gn_after_init) { const int r = launch_gn(); if (r) return r; }
+  if (early) HIPC(hipStreamWaitEvent(s, c->ev_ei, 0));   // the strong sweeps read GenEdgeInform's rays
   HIPC(hipGetLastError());
   auto strong_sweep = [&](const DevBufs& Bs, int it, const int* lst, const int* cnt) {
     const bool edge = pc.P.use_edge;
