@@ -738,9 +738,10 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
     k_list_scan<0><<<1, 256, 0, s>>>(dpc, c->row_counts.p, c->list_totals.p);
     k_list_fill<0><<<(pc.half_rows + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p, c->lists.p, list_stride);
   }
-  // GenNeighbours + NeigbourUpdate (+ the failed-pixel list on the aux stream).  Forked after
-  // RandomInitialization: launched beside it, GenNeighbours' ~4.7 K long waves (all resident at once)
-  // starved it of registers (0.86 -> 8.5 ms in a kernel trace of the overlapped pass)
+  // GenNeighbours + NeigbourUpdate (+ the failed-pixel list on the aux stream).  With the early fork
+  // they follow GenEdgeInform and the nearest-strong tables on the aux stream; otherwise they are
+  // forked after RandomInitialization: launched beside it, GenNeighbours' ~4.7 K long waves (all
+  // resident at once) starved it of registers (0.86 -> 8.5 ms in a kernel trace of the overlapped pass)
   const DevBufs Bgn = Bc;
   auto launch_gn = [&]() -> int {
     if (overlap && !early) {
