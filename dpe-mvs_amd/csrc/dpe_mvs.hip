@@ -359,6 +359,13 @@ struct StageSrc {
 };
 static int stage_impl(DpeContext* c, const DpePassInput* in, const StageSrc& src);
 
+#if DPE_LINE_STATS
+extern "C" void dpe_dbg_line_stats_main(unsigned long long out[16], int reset) {
+  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(dpe::g_lstat), sizeof(dpe::g_lstat));
+  if (reset) { unsigned long long z[16] = {}; (void)hipMemcpyToSymbol(HIP_SYMBOL(dpe::g_lstat), z, sizeof(z)); }
+}
+#endif
+
 extern "C" int dpe_pm_stage(DpeContext* c, const DpePassInput* in, const DpePassState* st) {
   g_err.clear();
   if (!c || !in || !st || !in->images || !in->cams || !st->planes || !st->weak_info || !st->selected_views) {
@@ -423,6 +430,8 @@ static int stage_impl(DpeContext* c, const DpePassInput* in, const StageSrc& src
   if (in->num_images > DPE_MAX_IMAGES) { g_err = "dpe_pm_stage: num_images > 32 (DPE.cpp:762)"; return DPE_ERR_TOO_MANY; }
   if (in->num_images < 2 || in->width <= 0 || in->height <= 0) { g_err = "dpe_pm_stage: bad shape"; return DPE_ERR_ARG; }
   if (in->width > 32000 || in->height > 32000) { g_err = "dpe_pm_stage: image too large for short2 coordinates"; return DPE_ERR_ARG; }
+  // tap coordinates on the unit grid of [2^23, 2^24) (pass_common.h kTexMagic): 256 (lim + 1) < 2^22
+  if (in->width > 16000 || in->height > 16000) { g_err = "dpe_pm_stage: image wider or taller than 16000 px"; return DPE_ERR_ARG; }
   const DpePatchMatchParams& P = in->params;
   if (P.rotate_time < 1 || P.rotate_time > 4) { g_err = "dpe_pm_stage: rotate_time must be in [1,4]"; return DPE_ERR_ARG; }
   if (P.strong_increment <= 0 || P.weak_increment <= 0) { g_err = "dpe_pm_stage: increments must be > 0"; return DPE_ERR_ARG; }

@@ -254,8 +254,8 @@ DEV bool rcp_range_ok(const Homog& H, float x0, float x1, float y0, float y1) {
          amax < 1.2676506002282294e+30f;
 }
 
-// True when every tap of the rectangle projects to sx <= W - 1 and sy <= H - 1, so the upper clamp
-// of the fixed-point coordinate (fixed_coord) is the identity for all of them.  Call only after
+// True when every tap of the rectangle projects into [0, W - 1] x [0, H - 1], so the clamp of the
+// fixed-point coordinate (tex_t_fast) is the identity for all of them.  Call only after
 // rcp_range_ok on the same rectangle (qz of one sign, exact reciprocal).  The corners are computed
 // with the taps' own operations; with qz of one sign the exact projective map of the rectangle lies
 // within its corner values, and the computed taps differ from the exact map by < 1e-3 px for any
@@ -272,7 +272,8 @@ DEV bool patch_inside(const Homog& H, float x0, float x1, float y0, float y1, in
     for (int j = 0; j < 2; ++j) {
       const float y = j ? y1 : y0;
       const float iz = d_rcp_fast(__builtin_fmaf(H.h[7], y, bz));
-      ok = ok && (__builtin_fmaf(H.h[1], y, bx) * iz <= lx) && (__builtin_fmaf(H.h[4], y, by) * iz <= ly);   // NaN -> false
+      const float sx = __builtin_fmaf(H.h[1], y, bx) * iz, sy = __builtin_fmaf(H.h[4], y, by) * iz;
+      ok = ok && sx <= lx && sy <= ly && sx >= 0.0f && sy >= 0.0f;   // NaN -> false
     }
   }
   return ok;
@@ -284,14 +285,43 @@ DEV float ref_texel(const float* ref, int W, int H, int x, int y) {
   y = y < 0 ? 0 : (y > H - 1 ? H - 1 : y);
   return ref[y * W + x];
 }
-// Bilinear sample with 8-bit weights on the padded quad image (see oracle OracleSample).
-DEV float sample_quad(const float4* __restrict__ q, int W, int H, float sx, float sy) {
-  const float xb = __builtin_fminf(__builtin_fmaxf(sx, -1.0f), (float)W);
-  const float yb = __builtin_fminf(__builtin_fmaxf(sy, -1.0f), (float)H);
-  const int ux = (int)__builtin_fmaf(xb, 256.0f, 256.5f);
-  const int uy = (int)__builtin_fmaf(yb, 256.0f, 256.5f);
-  const float ax = (float)(ux & 255) * 0.00390625f;
-  const float ay = (float)(uy & 255) * 0.00390625f;
+// ------------------------------------------------------------------------------ tap coordinates
+// The texture unit's coordinate conversion (tex2D(x + 0.5) with linear filtering and clamp
+// addressing, DPE.cpp:927-933), restated (round 3; oracle OracleSampleQ):
+// a tap whose homography rows give (qx, qy, qz) reads the padded quad texel (Ux >> 8, Uy >> 8) with
+// weights (Ux & 255) / 256, (Uy & 255) / 256, where
+//     U = clamp(RN_even(Q * iz + 256), 0, 256 * lim + 256),   Q = 256 q (exact),  iz = RN(1 / qz)
+// i.e. the coordinate s + 1 = q / qz + 1 in 1/256 units rounded to nearest ONCE.  The rows are
+// pre-scaled by 256 (power of two: exact), and t = fma(Q, iz, 1.5·2^23 + 256) lands on the unit grid
+// of [2^23, 2^24), so t's encoding minus that of 1.5·2^23 is U: one FMA per coordinate (round 2 used
+// trunc(fma(q·iz, 256, 256.5)): a multiply, an FMA, a clamp and a half-rate conversion).  The clamp
+// is taken on t (monotone; NaN -> the low end), and the bound |256 s + 256| < 2^22 for unclamped taps
+// holds for images narrower than 16383 px (dpe_pm_stage checks).
+constexpr float kTexMagic = 12582912.0f;          // 1.5 * 2^23
+constexpr uint32_t kTexMagicBits = 0x4B400000u;   // its encoding
+constexpr uint32_t kTexMagicHi = 0x4B4000u;       // encoding >> 8: texel index bias of t >> 8
+DEV float tex_tmax(int lim) { return kTexMagic + 256.0f * (float)(lim + 1); }   // t of U = 256 lim + 256
+// clamped t of a tap with scaled row value Q (generic path: NaN -> kTexMagic)
+DEV float tex_t(float Q, float iz, float tmax) {
+  const float t = __builtin_fmaf(Q, iz, kTexMagic + 256.0f);
+  return __builtin_fminf(__builtin_fmaxf(t, kTexMagic), tmax);
+}
+// The taps' numerators Q = 256 q: the column coefficients h1, h4 scaled by 256 here, the row terms
+// (h0 x + h2, h3 x + h5) scaled after their FMA (the oracle's OracleSampleQ caller does the same).
+DEV Homog scale_cols(const Homog& H) {
+  Homog S = H;
+  S.h[1] = H.h[1] * 256.0f;
+  S.h[4] = H.h[4] * 256.0f;
+  return S;
+}
+
+// Bilinear sample with 8-bit weights on the padded quad image (see oracle OracleSampleQ), at the
+// tap with scaled numerators (Qx, Qy) and reciprocal denominator iz.
+DEV float sample_quad(const float4* __restrict__ q, int W, int H, float Qx, float Qy, float iz) {
+  const uint32_t ux = __float_as_uint(tex_t(Qx, iz, tex_tmax(W))) - kTexMagicBits;
+  const uint32_t uy = __float_as_uint(tex_t(Qy, iz, tex_tmax(H))) - kTexMagicBits;
+  const float ax = (float)(ux & 255u) * 0.00390625f;
+  const float ay = (float)(uy & 255u) * 0.00390625f;
   const float4 t = q[(uy >> 8) * (W + 2) + (ux >> 8)];
   const float r0 = __builtin_fmaf(ax, t.y - t.x, t.x);
   const float r1 = __builtin_fmaf(ax, t.w - t.z, t.z);
@@ -349,14 +379,12 @@ DEV void texel_rows(const uint8_t* p, float fx, float& r0, float& r1) {
 }
 // Same sampler on the 8-bit quad texels of one view: identical values to the f32 layout's.
 template <int T>
-DEV float sample_quad8(const uint8_t* __restrict__ q, int W, int H, float sx, float sy) {
-  const float xb = __builtin_fminf(__builtin_fmaxf(sx, -1.0f), (float)W);
-  const float yb = __builtin_fminf(__builtin_fmaxf(sy, -1.0f), (float)H);
-  const int ux = (int)__builtin_fmaf(xb, 256.0f, 256.5f);
-  const int uy = (int)__builtin_fmaf(yb, 256.0f, 256.5f);
-  const float ay = (float)(uy & 255) * 0.00390625f;
+DEV float sample_quad8(const uint8_t* __restrict__ q, int W, int H, float Qx, float Qy, float iz) {
+  const uint32_t ux = __float_as_uint(tex_t(Qx, iz, tex_tmax(W))) - kTexMagicBits;
+  const uint32_t uy = __float_as_uint(tex_t(Qy, iz, tex_tmax(H))) - kTexMagicBits;
+  const float ay = (float)(uy & 255u) * 0.00390625f;
   float r0, r1;
-  texel_rows<T>(q + (size_t)((uy >> 8) * tex_stride<T>(W) + (ux >> 8)) * tex_bytes<T>(), (float)(ux & 255), r0, r1);
+  texel_rows<T>(q + (size_t)((uy >> 8) * tex_stride<T>(W) + (ux >> 8)) * tex_bytes<T>(), (float)(ux & 255u), r0, r1);
   return __builtin_fmaf(ay, r1 - r0, r0);
 }
 // The default 36-tap patch (strong radius 5, increment 2) that the tabulated fast paths serve.
@@ -380,79 +408,104 @@ typedef float f2v __attribute__((ext_vector_type(2)));
 DEV f2v f2s(float a) { return (f2v){a, a}; }
 DEV f2v fma2(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
 
-// One bilinear tap of the 8-bit quad image (layout T) whose byte offset is `vofs`, at the
-// projection of the tap (row terms bxy = (h0 x + h2, h3 x + h5), bz = h6 x + h8; column yf).
-// Bit-identical to sample_quad8(project) when the tap's qz is in d_rcp_fast's exact range
-// (rcp_range_ok), with packed FP32 ops, one med3 per clamp and a 32-bit offset from one base.
-// Fixed-point coordinate of the clamped sample: trunc(fma(clamp(s, -1, lim), 256, 256.5)) computed
-// as min(cvt_u32_sat(fma(s, 256, 256.5)), 256 lim + 256).  Below -1 both give 0 (the saturating
-// conversion maps every u < 1 to 0; u(-1) = 0.5); above lim both give 256 lim + 256; in between
-// the operations are identical.  One VOP2 min replaces the med3 + signed conversion pair.
-#ifndef DPE_SAT_CLAMP
-#define DPE_SAT_CLAMP 1
+// Gather-locality diagnostic (build with -DDPE_LINE_STATS=1; tools/line_stats.py): for every wave
+// gather of a fast-path tap, the number of distinct 128-B lines and 64-B sectors its active lanes
+// touch, summed per texel layout T in a per-translation-unit device array (read back with
+// dpe_dbg_line_stats).  Off in the product.
+#ifndef DPE_LINE_STATS
+#define DPE_LINE_STATS 0
 #endif
-// IN: the caller has proven s <= lim for this tap (patch_inside), so the min is the identity and is
-// skipped (the saturating conversion alone handles the low side).
-// The upper clamp is taken on the float before the conversion (v_min_f32, full rate, instead of
-// v_min_u32 after it, half rate): min(trunc(u), umax) == trunc(min(u, umax)) for every u that is
-// not NaN (umax is an integer below 2^24; +-inf saturate the same way), and on the taps' fast path
-// (rcp_range_ok) s = q * iz is never NaN.
-template <bool IN = false>
-DEV uint32_t fixed_coord(float s, uint32_t umax) {
-#if DPE_SAT_CLAMP
-  float u = __builtin_fmaf(s, 256.0f, 256.5f);
-  if constexpr (!IN) u = __builtin_fminf(u, (float)umax);
-  uint32_t r;
-  asm("v_cvt_u32_f32 %0, %1" : "=v"(r) : "v"(u));
-  return r;
-#else
-  const float lim = (float)((umax - 256u) >> 8);
-  return (uint32_t)(int)__builtin_fmaf(__builtin_amdgcn_fmed3f(s, -1.0f, lim), 256.0f, 256.5f);
-#endif
+#if DPE_LINE_STATS
+static __device__ unsigned long long g_lstat[4][4];   // [T][loads, lines, quad lines, active lanes]
+DEV void line_stat(int T, const void* p) {
+  const uint64_t a = (uint64_t)p;
+  uint64_t rem = __ballot(1);
+  const int first = __builtin_ctzll(rem);
+  const unsigned long long act = __popcll(rem);
+  unsigned long long nl = 0, ns = 0;
+  {   // the texture-address cost: sum over lane quads of the distinct lines each quad touches
+    const int lane = threadIdx.x & 63, q0 = lane & ~3;
+    bool firstl = true;
+    for (int j = 0; j < 4; ++j) {
+      const uint64_t o = __shfl(a >> 7, q0 + j);
+      if (q0 + j < lane && ((rem >> (q0 + j)) & 1) && o == (a >> 7)) firstl = false;
+    }
+    ns = __popcll(__ballot(firstl));
+  }
+  uint64_t r = rem;
+  while (r) {
+    const int l = __builtin_ctzll(r);
+    const uint64_t L = __shfl(a >> 7, l);
+    r &= ~__ballot((a >> 7) == L);
+    ++nl;
+  }
+  if ((int)(threadIdx.x & 63) == first) {
+    atomicAdd(&g_lstat[T][0], 1ull); atomicAdd(&g_lstat[T][1], nl);
+    atomicAdd(&g_lstat[T][2], ns); atomicAdd(&g_lstat[T][3], act);
+  }
 }
+#define LINE_STAT(T, p) line_stat(T, p)
+#else
+#define LINE_STAT(T, p) do {} while (0)
+#endif
+
+// Fast-path tap constants of one (view, homography): the t clamps of the two axes and the view's
+// byte offset biased so that the t encodings index texels directly:
+//   offset = vofs + ((Uy >> 8) * stride + (Ux >> 8)) * bytes
+//          = vadj + ((bits(ty) >> 8) * stride + (bits(tx) >> 8)) * bytes   (mod 2^32)
+// with vadj = vofs - kTexMagicHi * (stride + 1) * bytes (bits(t) >> 8 = kTexMagicHi + (U >> 8) < 2^24,
+// so __umul24 sees the whole operand; the true offset is below 2^32, so the wrap-around cancels).
+DEV f2v tex_tmax2(int W, int H) { return (f2v){tex_tmax(W), tex_tmax(H)}; }
+template <int T> DEV uint32_t tex_vadj(uint32_t vofs, uint32_t stride) {
+  return vofs - kTexMagicHi * (stride + 1u) * tex_bytes<T>();
+}
+// clamped t of the fast path (no NaN there: rcp_range_ok), or unclamped when IN (patch_inside)
+template <bool IN>
+DEV float tex_t_fast(float t, float tmax) {
+  if constexpr (IN) return t;
+  else return __builtin_amdgcn_fmed3f(t, kTexMagic, tmax);
+}
+
+// One bilinear tap of the 8-bit quad image (layout T) at the view offset `vadj` (tex_vadj), from
+// the homography h with scaled column coefficients (scale_cols) and its row terms
+// bxy = 256 (h0 x + h2, h3 x + h5), bz = h6 x + h8; column yf.  Bit-identical to sample_quad8
+// when the tap's qz is in d_rcp_fast's exact range (rcp_range_ok).
 template <int T, bool IN = false>
-DEV float tap_u8_fast(const DevBufs& B, uint32_t vofs, uint32_t stride, f2v lim, const float* h, f2v bxy, float bz,
+DEV float tap_u8_fast(const DevBufs& B, uint32_t vadj, uint32_t stride, f2v tmax, const float* h, f2v bxy, float bz,
                       float yf) {
   const f2v q = fma2((f2v){h[1], h[4]}, f2s(yf), bxy);
   const float iz = d_rcp_fast(__builtin_fmaf(h[7], yf, bz));
-  const f2v sxy = q * f2s(iz);
-#if DPE_SAT_CLAMP
-  const uint32_t ux = fixed_coord<IN>(sxy.x, (uint32_t)lim.x * 256u + 256u);
-  const uint32_t uy = fixed_coord<IN>(sxy.y, (uint32_t)lim.y * 256u + 256u);
-#else
-  const float xb = __builtin_amdgcn_fmed3f(sxy.x, -1.0f, lim.x);
-  const float yb = __builtin_amdgcn_fmed3f(sxy.y, -1.0f, lim.y);
-  const f2v u = fma2((f2v){xb, yb}, f2s(256.0f), f2s(256.5f));
-  const uint32_t ux = (uint32_t)(int)u.x, uy = (uint32_t)(int)u.y;       // >= 0 after the clamp
-#endif
-  const uint8_t* p = tex_base<T>(B) + (vofs + (__umul24(uy >> 8, stride) + (ux >> 8)) * tex_bytes<T>());
+  const f2v t = fma2(q, f2s(iz), f2s(kTexMagic + 256.0f));
+  const uint32_t ux = __float_as_uint(tex_t_fast<IN>(t.x, tmax.x)), uy = __float_as_uint(tex_t_fast<IN>(t.y, tmax.y));
+  const uint8_t* p = tex_base<T>(B) + (vadj + (__umul24(uy >> 8, stride) + (ux >> 8)) * tex_bytes<T>());
+  LINE_STAT(T, p);
   const float ay = (float)(uy & 255u) * 0.00390625f;
   if constexpr (T == TEX_F16 || T == TEX_P16) {
     float r0, r1;
     texel_rows<T>(p, (float)(ux & 255u), r0, r1);
     return __builtin_fmaf(ay, r1 - r0, r0);
   } else {
-    const uint32_t t = *(const uint32_t*)p;
+    const uint32_t tt = *(const uint32_t*)p;
     const float ax = (float)(ux & 255u) * 0.00390625f;
-    const f2v lo = (f2v){(float)(t & 255u), (float)((t >> 16) & 255u)};
-    const f2v hi = (f2v){(float)((t >> 8) & 255u), (float)(t >> 24)};
+    const f2v lo = (f2v){(float)(tt & 255u), (float)((tt >> 16) & 255u)};
+    const f2v hi = (f2v){(float)((tt >> 8) & 255u), (float)(tt >> 24)};
     const f2v r = fma2(f2s(ax), hi - lo, lo);
     return __builtin_fmaf(ay, r.y - r.x, r.x);
   }
 }
 
 // Two taps of one patch row (columns yf.x, yf.y) with the projection, reciprocal refinement and
-// the vertical interpolation packed across the two taps; per element the same operations as
-// tap_u8_fast, so each result is bit-identical to it.
+// the coordinate FMAs packed across the two taps; per element the same operations as tap_u8_fast,
+// so each result is bit-identical to it.
 #ifndef DPE_EXP_CHEAP
 #define DPE_EXP_CHEAP 0
 #endif
 #ifndef DPE_TAP_PAIR
 #define DPE_TAP_PAIR 1
 #endif
-// `base` is the texel array the byte offsets index (tex_base of the layout; vofs selects the view).
+// `base` is the texel array the byte offsets index (tex_base of the layout; vadj selects the view).
 template <int T, bool IN = false>
-DEV f2v tap2_at(const uint8_t* base, uint32_t vofs, uint32_t stride, f2v lim, const float* h, f2v bxy, float bz, f2v yf) {
+DEV f2v tap2_at(const uint8_t* base, uint32_t vadj, uint32_t stride, f2v tmax, const float* h, f2v bxy, float bz, f2v yf) {
   const f2v qx = fma2(f2s(h[1]), yf, f2s(bxy.x));
   const f2v qy = fma2(f2s(h[4]), yf, f2s(bxy.y));
   const f2v qz = fma2(f2s(h[7]), yf, f2s(bz));
@@ -462,12 +515,13 @@ DEV f2v tap2_at(const uint8_t* base, uint32_t vofs, uint32_t stride, f2v lim, co
 #else
   const f2v iz = fma2(fma2(-qz, r, f2s(1.0f)), r, r);
 #endif
-  const f2v sx = qx * iz, sy = qy * iz;
-  const uint32_t mx = (uint32_t)lim.x * 256u + 256u, my = (uint32_t)lim.y * 256u + 256u;
-  const uint32_t ux0 = fixed_coord<IN>(sx.x, mx), ux1 = fixed_coord<IN>(sx.y, mx);
-  const uint32_t uy0 = fixed_coord<IN>(sy.x, my), uy1 = fixed_coord<IN>(sy.y, my);
-  const uint8_t* p0 = base + (vofs + (__umul24(uy0 >> 8, stride) + (ux0 >> 8)) * tex_bytes<T>());
-  const uint8_t* p1 = base + (vofs + (__umul24(uy1 >> 8, stride) + (ux1 >> 8)) * tex_bytes<T>());
+  const f2v tx = fma2(qx, iz, f2s(kTexMagic + 256.0f)), ty = fma2(qy, iz, f2s(kTexMagic + 256.0f));
+  const uint32_t ux0 = __float_as_uint(tex_t_fast<IN>(tx.x, tmax.x)), ux1 = __float_as_uint(tex_t_fast<IN>(tx.y, tmax.x));
+  const uint32_t uy0 = __float_as_uint(tex_t_fast<IN>(ty.x, tmax.y)), uy1 = __float_as_uint(tex_t_fast<IN>(ty.y, tmax.y));
+  const uint8_t* p0 = base + (vadj + (__umul24(uy0 >> 8, stride) + (ux0 >> 8)) * tex_bytes<T>());
+  const uint8_t* p1 = base + (vadj + (__umul24(uy1 >> 8, stride) + (ux1 >> 8)) * tex_bytes<T>());
+  LINE_STAT(T, p0);
+  LINE_STAT(T, p1);
   const f2v ay = (f2v){(float)(uy0 & 255u), (float)(uy1 & 255u)} * f2s(0.00390625f);
   float a0, a1, b0, b1;
   texel_rows<T>(p0, (float)(ux0 & 255u), a0, a1);
@@ -476,13 +530,14 @@ DEV f2v tap2_at(const uint8_t* base, uint32_t vofs, uint32_t stride, f2v lim, co
   return fma2(ay, r1 - r0, r0);
 }
 template <int T, bool IN = false>
-DEV f2v tap2_fast(const DevBufs& B, uint32_t vofs, uint32_t stride, f2v lim, const float* h, f2v bxy, float bz, f2v yf) {
-  return tap2_at<T, IN>(tex_base<T>(B), vofs, stride, lim, h, bxy, bz, yf);
+DEV f2v tap2_fast(const DevBufs& B, uint32_t vadj, uint32_t stride, f2v tmax, const float* h, f2v bxy, float bz, f2v yf) {
+  return tap2_at<T, IN>(tex_base<T>(B), vadj, stride, tmax, h, bxy, bz, yf);
 }
 
-template <int U8> DEV float sample_src(const DevBufs& B, int v, int W, int H, float sx, float sy) {
-  if constexpr (U8 != TEX_F32) return sample_quad8<U8>(tex_base<U8>(B) + (size_t)v * tex_view<U8>(B), W, H, sx, sy);
-  else return sample_quad(B.imgq[v], W, H, sx, sy);
+// Sample of view v at the tap with scaled numerators (Qx, Qy) and reciprocal denominator iz.
+template <int U8> DEV float sample_src(const DevBufs& B, int v, int W, int H, float Qx, float Qy, float iz) {
+  if constexpr (U8 != TEX_F32) return sample_quad8<U8>(tex_base<U8>(B) + (size_t)v * tex_view<U8>(B), W, H, Qx, Qy, iz);
+  else return sample_quad(B.imgq[v], W, H, Qx, Qy, iz);
 }
 
 DEV float depth_texel(const float* d, int W, int H, float x, float y) {   // DPE.cu:936
@@ -527,17 +582,18 @@ DEV float ncc_finalize(float s_ref, float s_rr, float s_w, float s_src, float s_
 // Generic bilateral NCC of one patch, weights computed per tap (NCC-New neighbour patches and
 // non-default radius/increment).  Same arithmetic order as the oracle's PatchNCC.
 template <int U8, bool FAST>
-DEV void generic_taps(const PassConst& pc, const DevBufs& B, int v, const Homog& H, int cx, int cy, float rcp,
+DEV void generic_taps(const PassConst& pc, const DevBufs& B, int v, const Homog& H0, int cx, int cy, float rcp,
                       int radius, int increment, float* acc) {
   const int W = pc.W, Hh = pc.H;
+  const Homog H = scale_cols(H0);
   const float ss = pc.P.sigma_spatial, sc = pc.P.sigma_color;
   float s_ref = 0, s_rr = 0, s_src = 0, s_ss = 0, s_rs = 0, s_w = 0;
   for (int i = -radius; i <= radius; i += increment) {
     float r_ref = 0, r_src = 0, r_rr = 0, r_ss = 0, r_rs = 0, r_w = 0;
     const int x = cx + i;
     const float xf = (float)x;
-    const float bx = __builtin_fmaf(H.h[0], xf, H.h[2]);
-    const float by = __builtin_fmaf(H.h[3], xf, H.h[5]);
+    const float bx = __builtin_fmaf(H.h[0], xf, H.h[2]) * 256.0f;
+    const float by = __builtin_fmaf(H.h[3], xf, H.h[5]) * 256.0f;
     const float bz = __builtin_fmaf(H.h[6], xf, H.h[8]);
     for (int j = -radius; j <= radius; j += increment) {
       const int y = cy + j;
@@ -546,7 +602,7 @@ DEV void generic_taps(const PassConst& pc, const DevBufs& B, int v, const Homog&
       const float qx = __builtin_fmaf(H.h[1], yf, bx);
       const float qy = __builtin_fmaf(H.h[4], yf, by);
       const float iz = rcp_sel<FAST>(__builtin_fmaf(H.h[7], yf, bz));
-      const float sp = sample_src<U8>(B, v, W, Hh, qx * iz, qy * iz);
+      const float sp = sample_src<U8>(B, v, W, Hh, qx, qy, iz);
       const float w = bilateral_weight(i, j, rp, rcp, ss, sc);
       const float wr = w * rp;
       r_ref = r_ref + wr;
@@ -635,14 +691,15 @@ DEV void make_patch36(Patch36& P, const PassConst& pc, const DevBufs& B, int px,
   P.s_ref = s_ref; P.s_rr = s_rr; P.s_w = s_w;
 }
 template <int U8, bool FAST>
-DEV void patch36_taps(const Patch36& P, const PassConst& pc, const DevBufs& B, int v, const Homog& H, float* acc) {
+DEV void patch36_taps(const Patch36& P, const PassConst& pc, const DevBufs& B, int v, const Homog& H0, float* acc) {
   const int W = pc.W, Hh = pc.H;
+  const Homog H = scale_cols(H0);
   float s_src = 0, s_ss = 0, s_rs = 0;
 #pragma unroll
   for (int a = 0; a < 6; ++a) {
     const float x = (float)(P.px - 5 + 2 * a);
-    const float bx = __builtin_fmaf(H.h[0], x, H.h[2]);
-    const float by = __builtin_fmaf(H.h[3], x, H.h[5]);
+    const float bx = __builtin_fmaf(H.h[0], x, H.h[2]) * 256.0f;
+    const float by = __builtin_fmaf(H.h[3], x, H.h[5]) * 256.0f;
     const float bz = __builtin_fmaf(H.h[6], x, H.h[8]);
     float r_src = 0, r_ss = 0, r_rs = 0;
 #pragma unroll
@@ -651,7 +708,7 @@ DEV void patch36_taps(const Patch36& P, const PassConst& pc, const DevBufs& B, i
       const float qx = __builtin_fmaf(H.h[1], y, bx);
       const float qy = __builtin_fmaf(H.h[4], y, by);
       const float iz = rcp_sel<FAST>(__builtin_fmaf(H.h[7], y, bz));
-      const float sp = sample_src<U8>(B, v, W, Hh, qx * iz, qy * iz);
+      const float sp = sample_src<U8>(B, v, W, Hh, qx, qy, iz);
       const float w = P.w[a * 6 + b], wr = P.wr[a * 6 + b];
       r_src = __builtin_fmaf(w, sp, r_src);
       const float ws = w * sp;

@@ -66,8 +66,10 @@ DEV void patch_lds_pre(const float* pw, float& p_inv, float& p_mref, float& p_va
 // Packed form: (r_src, r_rs) accumulate as one pair; weights are (w, w*grey) pairs in LDS; the two
 // taps of a row pair share each packed op (tap2_at).
 template <int U8, bool IN = false>
-DEV void taps36_at(const float* pw, int px, int py, f2v lim, const uint8_t* base, uint32_t vofs, uint32_t stride,
-                   const Homog& H, float* acc) {
+DEV void taps36_at(const float* pw, int px, int py, f2v tmax, const uint8_t* base, uint32_t vofs, uint32_t stride,
+                   const Homog& H0, float* acc) {
+    const Homog H = scale_cols(H0);
+    const uint32_t vadj = tex_vadj<U8>(vofs, stride);
     // packed form: (r_src, r_rs) accumulate as one pair; weights are (w, w*grey) pairs in LDS
     const f2v* wp = (const f2v*)pw;
     f2v s_sr = f2s(0.0f);
@@ -83,13 +85,13 @@ DEV void taps36_at(const float* pw, int px, int py, f2v lim, const uint8_t* base
 #endif
     for (int a = 0; a < 6; ++a) {
       const float x = (float)(px - 5 + 2 * a);
-      const f2v bxy = fma2((f2v){H.h[0], H.h[3]}, f2s(x), (f2v){H.h[2], H.h[5]});
+      const f2v bxy = fma2((f2v){H.h[0], H.h[3]}, f2s(x), (f2v){H.h[2], H.h[5]}) * f2s(256.0f);
       const float bz = __builtin_fmaf(H.h[6], x, H.h[8]);
       f2v r_sr = f2s(0.0f);
       float r_ss = 0;
 #pragma unroll
       for (int b = 0; b < 6; b += 2) {
-        const f2v sp = tap2_at<U8, IN>(base, vofs, stride, lim, H.h, bxy, bz,
+        const f2v sp = tap2_at<U8, IN>(base, vadj, stride, tmax, H.h, bxy, bz,
                                    (f2v){(float)(py - 5 + 2 * b), (float)(py - 3 + 2 * b)});
         const f2v w0 = wp[a * 6 + b], w1 = wp[a * 6 + b + 1];
         const f2v ws = (f2v){w0.x, w1.x} * sp;
@@ -104,19 +106,20 @@ DEV void taps36_at(const float* pw, int px, int py, f2v lim, const uint8_t* base
 }
 // Old NCC with the patch read from LDS (same arithmetic as ncc_old_patch36)
 template <int U8, bool FAST, bool IN = false>
-DEV void lds_taps(const float* pw, int px, int py, const PassConst& pc, const DevBufs& B, int v, const Homog& H,
+DEV void lds_taps(const float* pw, int px, int py, const PassConst& pc, const DevBufs& B, int v, const Homog& H0,
                   float* acc) {
   const int W = pc.W, Hh = pc.H;
   if constexpr (U8 != TEX_F32 && FAST && DPE_PACKED_TAP) {
-    taps36_at<U8, IN>(pw, px, py, (f2v){(float)W, (float)Hh}, tex_base<U8>(B), (uint32_t)v * tex_view<U8>(B),
-                      tex_stride<U8>(W), H, acc);
+    taps36_at<U8, IN>(pw, px, py, tex_tmax2(W, Hh), tex_base<U8>(B), (uint32_t)v * tex_view<U8>(B),
+                      tex_stride<U8>(W), H0, acc);
   } else {
+    const Homog H = scale_cols(H0);
     float s_src = 0, s_ss = 0, s_rs = 0;
 #pragma unroll
     for (int a = 0; a < 6; ++a) {
       const float x = (float)(px - 5 + 2 * a);
-      const float bx = __builtin_fmaf(H.h[0], x, H.h[2]);
-      const float by = __builtin_fmaf(H.h[3], x, H.h[5]);
+      const float bx = __builtin_fmaf(H.h[0], x, H.h[2]) * 256.0f;
+      const float by = __builtin_fmaf(H.h[3], x, H.h[5]) * 256.0f;
       const float bz = __builtin_fmaf(H.h[6], x, H.h[8]);
       float r_src = 0, r_ss = 0, r_rs = 0;
 #pragma unroll
@@ -125,7 +128,7 @@ DEV void lds_taps(const float* pw, int px, int py, const PassConst& pc, const De
         const float qx = __builtin_fmaf(H.h[1], y, bx);
         const float qy = __builtin_fmaf(H.h[4], y, by);
         const float iz = rcp_sel<FAST>(__builtin_fmaf(H.h[7], y, bz));
-        const float sp = sample_src<U8>(B, v, W, Hh, qx * iz, qy * iz);
+        const float sp = sample_src<U8>(B, v, W, Hh, qx, qy, iz);
         const float w = pw[2 * (a * 6 + b)], wr = pw[2 * (a * 6 + b) + 1];
         r_src = __builtin_fmaf(w, sp, r_src);
         const float ws = w * sp;
@@ -142,22 +145,23 @@ DEV void lds_taps(const float* pw, int px, int py, const PassConst& pc, const De
 // its result bit for bit; the strong sweep's pool uses this to split the jobs of a nearly empty
 // last round over several lanes.
 template <int U8, bool FAST>
-DEV void lds_row(const float* pw, int px, int py, const PassConst& pc, const DevBufs& B, int v, const Homog& H, int a,
+DEV void lds_row(const float* pw, int px, int py, const PassConst& pc, const DevBufs& B, int v, const Homog& H0, int a,
                  float* r3) {
   const int W = pc.W, Hh = pc.H;
+  const Homog H = scale_cols(H0);
   const float x = (float)(px - 5 + 2 * a);
   if constexpr (U8 != TEX_F32 && FAST && DPE_PACKED_TAP) {
-    const uint32_t vofs = (uint32_t)v * tex_view<U8>(B), stride = tex_stride<U8>(W);
-    const f2v lim = (f2v){(float)W, (float)Hh};
+    const uint32_t stride = tex_stride<U8>(W), vadj = tex_vadj<U8>((uint32_t)v * tex_view<U8>(B), stride);
+    const f2v tmax = tex_tmax2(W, Hh);
     const f2v* wp = (const f2v*)pw;
-    const f2v bxy = fma2((f2v){H.h[0], H.h[3]}, f2s(x), (f2v){H.h[2], H.h[5]});
+    const f2v bxy = fma2((f2v){H.h[0], H.h[3]}, f2s(x), (f2v){H.h[2], H.h[5]}) * f2s(256.0f);
     const float bz = __builtin_fmaf(H.h[6], x, H.h[8]);
     f2v r_sr = f2s(0.0f);
     float r_ss = 0;
 #if DPE_TAP_PAIR
 #pragma unroll
     for (int b = 0; b < 6; b += 2) {
-      const f2v sp = tap2_fast<U8>(B, vofs, stride, lim, H.h, bxy, bz, (f2v){(float)(py - 5 + 2 * b), (float)(py - 3 + 2 * b)});
+      const f2v sp = tap2_fast<U8>(B, vadj, stride, tmax, H.h, bxy, bz, (f2v){(float)(py - 5 + 2 * b), (float)(py - 3 + 2 * b)});
       const f2v w0 = wp[a * 6 + b], w1 = wp[a * 6 + b + 1];
       const f2v ws = (f2v){w0.x, w1.x} * sp;
       r_sr = fma2(w0, f2s(sp.x), r_sr);
@@ -168,7 +172,7 @@ DEV void lds_row(const float* pw, int px, int py, const PassConst& pc, const Dev
 #else
 #pragma unroll
     for (int b = 0; b < 6; ++b) {
-      const float sp = tap_u8_fast<U8>(B, vofs, stride, lim, H.h, bxy, bz, (float)(py - 5 + 2 * b));
+      const float sp = tap_u8_fast<U8>(B, vadj, stride, tmax, H.h, bxy, bz, (float)(py - 5 + 2 * b));
       const f2v w = wp[a * 6 + b];
       r_sr = fma2(w, f2s(sp), r_sr);
       const float ws = w.x * sp;
@@ -177,8 +181,8 @@ DEV void lds_row(const float* pw, int px, int py, const PassConst& pc, const Dev
 #endif
     r3[0] = r_sr.x; r3[1] = r_ss; r3[2] = r_sr.y;
   } else {
-    const float bx = __builtin_fmaf(H.h[0], x, H.h[2]);
-    const float by = __builtin_fmaf(H.h[3], x, H.h[5]);
+    const float bx = __builtin_fmaf(H.h[0], x, H.h[2]) * 256.0f;
+    const float by = __builtin_fmaf(H.h[3], x, H.h[5]) * 256.0f;
     const float bz = __builtin_fmaf(H.h[6], x, H.h[8]);
     float r_src = 0, r_ss = 0, r_rs = 0;
 #pragma unroll
@@ -187,7 +191,7 @@ DEV void lds_row(const float* pw, int px, int py, const PassConst& pc, const Dev
       const float qx = __builtin_fmaf(H.h[1], y, bx);
       const float qy = __builtin_fmaf(H.h[4], y, by);
       const float iz = rcp_sel<FAST>(__builtin_fmaf(H.h[7], y, bz));
-      const float sp = sample_src<U8>(B, v, W, Hh, qx * iz, qy * iz);
+      const float sp = sample_src<U8>(B, v, W, Hh, qx, qy, iz);
       const float w = pw[2 * (a * 6 + b)], wr = pw[2 * (a * 6 + b) + 1];
       r_src = __builtin_fmaf(w, sp, r_src);
       const float ws = w * sp;

@@ -693,26 +693,27 @@ struct WeakTab {
 // NN > 0: the patch side n is the compile-time NN, so the tap loop unrolls and the gathers of a
 // patch are in flight together (the weak sweep's patches are 3x3 and 4..6 square).
 template <int U8, bool FAST, int NN = 0, bool IN = false>
-DEV void tab_taps(const PassConst& pc, const DevBufs& B, int v, const Homog& H, int cx, int cy, int rad, int inc,
+DEV void tab_taps(const PassConst& pc, const DevBufs& B, int v, const Homog& H0, int cx, int cy, int rad, int inc,
                   int n_rt, const float* __restrict__ tw, float* acc) {
   const int W = pc.W, Hh = pc.H;
+  const Homog H = scale_cols(H0);
   const int n = NN > 0 ? NN : n_rt;
   const f2v* wp = (const f2v*)tw;            // (w, w*grey) pairs
   if constexpr (U8 != TEX_F32 && FAST && DPE_PACKED_TAP) {
-    const uint32_t vofs = (uint32_t)v * tex_view<U8>(B), stride = tex_stride<U8>(W);
-    const f2v lim = (f2v){(float)W, (float)Hh};
+    const uint32_t stride = tex_stride<U8>(W), vadj = tex_vadj<U8>((uint32_t)v * tex_view<U8>(B), stride);
+    const f2v tmax = tex_tmax2(W, Hh);
     f2v s_sr = f2s(0.0f);
     float s_ss = 0;
 #pragma unroll
     for (int a = 0; a < (NN > 0 ? NN : n); ++a) {
       const float xf = (float)(cx - rad + a * inc);
-      const f2v bxy = fma2((f2v){H.h[0], H.h[3]}, f2s(xf), (f2v){H.h[2], H.h[5]});
+      const f2v bxy = fma2((f2v){H.h[0], H.h[3]}, f2s(xf), (f2v){H.h[2], H.h[5]}) * f2s(256.0f);
       const float bz = __builtin_fmaf(H.h[6], xf, H.h[8]);
       f2v r_sr = f2s(0.0f);
       float r_ss = 0;
 #pragma unroll
       for (int b = 0; b < (NN > 0 ? NN : n); ++b) {
-        const float sp = tap_u8_fast<U8, IN>(B, vofs, stride, lim, H.h, bxy, bz, (float)(cy - rad + b * inc));
+        const float sp = tap_u8_fast<U8, IN>(B, vadj, stride, tmax, H.h, bxy, bz, (float)(cy - rad + b * inc));
         const f2v w = wp[a * n + b];
         r_sr = fma2(w, f2s(sp), r_sr);
         const float ws = w.x * sp;
@@ -725,8 +726,8 @@ DEV void tab_taps(const PassConst& pc, const DevBufs& B, int v, const Homog& H, 
     float s_src = 0, s_ss = 0, s_rs = 0;
     for (int a = 0; a < n; ++a) {
       const float xf = (float)(cx - rad + a * inc);
-      const float bx = __builtin_fmaf(H.h[0], xf, H.h[2]);
-      const float by = __builtin_fmaf(H.h[3], xf, H.h[5]);
+      const float bx = __builtin_fmaf(H.h[0], xf, H.h[2]) * 256.0f;
+      const float by = __builtin_fmaf(H.h[3], xf, H.h[5]) * 256.0f;
       const float bz = __builtin_fmaf(H.h[6], xf, H.h[8]);
       float r_src = 0, r_ss = 0, r_rs = 0;
       for (int b = 0; b < n; ++b) {
@@ -734,7 +735,7 @@ DEV void tab_taps(const PassConst& pc, const DevBufs& B, int v, const Homog& H, 
         const float qx = __builtin_fmaf(H.h[1], yf, bx);
         const float qy = __builtin_fmaf(H.h[4], yf, by);
         const float iz = rcp_sel<FAST>(__builtin_fmaf(H.h[7], yf, bz));
-        const float sp = sample_src<U8>(B, v, W, Hh, qx * iz, qy * iz);
+        const float sp = sample_src<U8>(B, v, W, Hh, qx, qy, iz);
         const f2v w = wp[a * n + b];
         r_src = __builtin_fmaf(w.x, sp, r_src);
         const float ws = w.x * sp;

@@ -41,3 +41,10 @@ void launch_local_refine(bool img8, long L, int nv, hipStream_t s, const PassCon
 }
 
 }  // namespace dpe
+
+#if DPE_LINE_STATS
+extern "C" void dpe_dbg_line_stats_tap(unsigned long long out[16], int reset) {
+  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(dpe::g_lstat), sizeof(dpe::g_lstat));
+  if (reset) { unsigned long long z[16] = {}; (void)hipMemcpyToSymbol(HIP_SYMBOL(dpe::g_lstat), z, sizeof(z)); }
+}
+#endif

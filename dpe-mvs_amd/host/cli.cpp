@@ -8,7 +8,8 @@
 // depth maps are all-gathered after every pass with RCCL over xGMI.  The RCCL unique id goes from
 // rank 0 to the others over a TCP socket at MASTER_ADDR, port DPE_RDZV_PORT (default MASTER_PORT + 1,
 // beside the launcher's own store): nothing is written to the dataset folder and a stale id from an
-// earlier run cannot be read.
+// earlier run cannot be read.  Rank 0 listens on MASTER_ADDR only and answers a rank only after its
+// hello (rank + run token) checks out.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <arpa/inet.h>
@@ -21,10 +22,12 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <cstdint>
 #include <string>
 #include <thread>
 
 #include "../../include/dpe_host.h"
+#include "rdzv.h"
 
 namespace {
 
@@ -58,79 +61,13 @@ int rccl_allgather_dev(void* user, const float* dsend, size_t count, float* drec
   return hipStreamSynchronize(r->stream) == hipSuccess ? 0 : -1;
 }
 
-bool send_all(int fd, const void* p, size_t n) {
-  const char* c = static_cast<const char*>(p);
-  while (n) {
-    const ssize_t k = ::send(fd, c, n, 0);
-    if (k <= 0) return false;
-    c += k; n -= (size_t)k;
-  }
-  return true;
-}
-bool recv_all(int fd, void* p, size_t n) {
-  char* c = static_cast<char*>(p);
-  while (n) {
-    const ssize_t k = ::recv(fd, c, n, 0);
-    if (k <= 0) return false;
-    c += k; n -= (size_t)k;
-  }
-  return true;
-}
-
-// Rank 0 serves the id to world - 1 connections; the others connect (retrying for up to 120 s while
-// rank 0 starts).  Every socket call is bounded, so a missing peer ends in an error, not a hang.
-bool exchange_unique_id(ncclUniqueId& id, int rank, int world) {
-  const char* addr = std::getenv("MASTER_ADDR");
-  const char* rp = std::getenv("DPE_RDZV_PORT");
-  const char* mp = std::getenv("MASTER_PORT");
-  const int port = rp ? std::atoi(rp) : (mp ? std::atoi(mp) + 1 : 29501);
-  timeval tv{120, 0};
-  if (rank == 0) {
-    const int srv = ::socket(AF_INET, SOCK_STREAM, 0);
-    if (srv < 0) return false;
-    const int one = 1;
-    ::setsockopt(srv, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
-    ::setsockopt(srv, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
-    sockaddr_in sa{};
-    sa.sin_family = AF_INET;
-    sa.sin_addr.s_addr = htonl(INADDR_ANY);
-    sa.sin_port = htons((uint16_t)port);
-    bool ok = ::bind(srv, reinterpret_cast<sockaddr*>(&sa), sizeof(sa)) == 0 && ::listen(srv, world) == 0;
-    for (int k = 1; ok && k < world; ++k) {
-      const int c = ::accept(srv, nullptr, nullptr);   // SO_RCVTIMEO bounds the wait
-      if (c < 0) { ok = false; break; }
-      ::setsockopt(c, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof(tv));
-      ok = send_all(c, &id, sizeof(id));
-      ::close(c);
-    }
-    ::close(srv);
-    return ok;
-  }
-  addrinfo hints{}, *res = nullptr;
-  hints.ai_family = AF_INET;
-  hints.ai_socktype = SOCK_STREAM;
-  if (::getaddrinfo(addr ? addr : "127.0.0.1", std::to_string(port).c_str(), &hints, &res) != 0 || !res) return false;
-  const auto t0 = std::chrono::steady_clock::now();
-  bool ok = false;
-  while (!ok && std::chrono::steady_clock::now() - t0 < std::chrono::seconds(120)) {
-    const int c = ::socket(AF_INET, SOCK_STREAM, 0);
-    if (c < 0) break;
-    ::setsockopt(c, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
-    if (::connect(c, res->ai_addr, res->ai_addrlen) == 0) ok = recv_all(c, &id, sizeof(id));
-    ::close(c);
-    if (!ok) std::this_thread::sleep_for(std::chrono::milliseconds(100));
-  }
-  ::freeaddrinfo(res);
-  return ok;
-}
-
 bool rccl_init(Rccl& r, int rank, int world, int device) {
   r.world = world;
   if (hipSetDevice(device) != hipSuccess) return false;
   ncclUniqueId id;
   std::memset(&id, 0, sizeof(id));
   if (rank == 0 && ncclGetUniqueId(&id) != ncclSuccess) return false;
-  if (!exchange_unique_id(id, rank, world)) return false;
+  if (!dpe_rdzv::exchange_blob(&id, sizeof(id), rank, world)) return false;
   if (hipStreamCreate(&r.stream) != hipSuccess) return false;
   return ncclCommInitRank(&r.comm, world, id, rank) == ncclSuccess;
 }

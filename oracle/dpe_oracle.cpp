@@ -34,6 +34,9 @@
 //     Old NCC never reads the radius map).  NCCs whose result is multiplied by a zero view
 //     weight are not evaluated when the product is provably +0 (cost vectors feeding only
 //     `view_weights[j] * c` sums).
+//  7. Bilinear taps: the fixed-point coordinate of the texture unit is RN(256 (q / qz) + 256), rounded
+//     once from the 256-scaled homography numerator and the correctly rounded 1 / qz (OracleSampleQ);
+//     the reference's hardware conversion is unspecified beyond "8 fractional bits".
 #include "oracle_math.h"
 #include "../include/dpe_mvs.h"
 
@@ -248,17 +251,24 @@ static inline float RefTexel(const Pass& S, const std::vector<float>& im, int x,
   return im[(size_t)y * S.W + x];
 }
 // tex2D<float>(img, sx + 0.5f, sy + 0.5f), linear filter, clamp addressing (DPE.cpp:927-933).
-// Texture model: the coordinate is clamped to [-1, W] (beyond that the clamped filter result is
-// constant), converted to fixed point with 8 fractional bits U = (int)fma(x, 256, 256.5)
-// (x + 1 in 1/256 units, rounded), texel index i = (U >> 8) - 1, weight a = (U & 255) / 256.
-static inline float OracleSample(const Pass& S, const std::vector<float>& im, float sx, float sy) {
-  const float xb = fminf(fmaxf(sx, -1.0f), (float)S.W);
-  const float yb = fminf(fmaxf(sy, -1.0f), (float)S.H);
-  const int ux = (int)fmaf(xb, 256.0f, 256.5f);
-  const int uy = (int)fmaf(yb, 256.0f, 256.5f);
-  const float ax = (float)(ux & 255) * 0.00390625f;
-  const float ay = (float)(uy & 255) * 0.00390625f;
-  const int ix = (ux >> 8) - 1, iy = (uy >> 8) - 1;
+// Texture model (restatement choice 7): the tap's homography numerators are scaled by 256
+// (Q = fma(256 h1, y, 256 fma(h0, x, h2)) = 256 q, exact) and the coordinate s + 1 = q / qz + 1 is converted to fixed point with 8
+// fractional bits by ONE round-to-nearest-even, U = RN(Q * iz + 256) with iz = 1 / qz, evaluated
+// as t = fma(Q, iz, 1.5*2^23 + 256) on the unit grid of [2^23, 2^24) so that U = t - 1.5*2^23;
+// U is clamped to [0, 256 lim + 256] (clamp addressing: beyond that the filtered value is the
+// border texel's), NaN -> 0.  Texel index i = (U >> 8) - 1, weight a = (U & 255) / 256.
+static const float kTexMagic = 12582912.0f;   // 1.5 * 2^23
+static inline uint32_t TexU(float Q, float iz, int lim) {
+  const float t = fmaf(Q, iz, kTexMagic + 256.0f);
+  const float tc = fminf(fmaxf(t, kTexMagic), kTexMagic + 256.0f * (float)(lim + 1));
+  uint32_t u; std::memcpy(&u, &tc, 4);
+  return u - 0x4B400000u;
+}
+static inline float OracleSampleQ(const Pass& S, const std::vector<float>& im, float Qx, float Qy, float iz) {
+  const uint32_t ux = TexU(Qx, iz, S.W), uy = TexU(Qy, iz, S.H);
+  const float ax = (float)(ux & 255u) * 0.00390625f;
+  const float ay = (float)(uy & 255u) * 0.00390625f;
+  const int ix = (int)(ux >> 8) - 1, iy = (int)(uy >> 8) - 1;
   int x0 = ix < 0 ? 0 : (ix > S.W - 1 ? S.W - 1 : ix);
   int x1 = ix + 1 < 0 ? 0 : (ix + 1 > S.W - 1 ? S.W - 1 : ix + 1);
   int y0 = iy < 0 ? 0 : (iy > S.H - 1 ? S.H - 1 : iy);
@@ -354,14 +364,18 @@ static inline float BilateralWeight(const Pass& S, int i, int j, float pix, floa
 static inline float PatchNCC(const Pass& S, const std::vector<float>& src, const Homog& H, int cx, int cy,
                              float ref_center_pix, int radius, int increment) {
   const std::vector<float>& ref = S.img[0];
+  const float h1s = H.h[1] * 256.0f, h4s = H.h[4] * 256.0f;   // tap numerators Q = 256 q (choice 7)
   float s_ref = 0, s_rr = 0, s_src = 0, s_ss = 0, s_rs = 0, s_w = 0;
   for (int i = -radius; i <= radius; i += increment) {
     float r_ref = 0, r_src = 0, r_rr = 0, r_ss = 0, r_rs = 0, r_w = 0;
     for (int j = -radius; j <= radius; j += increment) {
       const int x = cx + i, y = cy + j;
       const float rp = RefTexel(S, ref, x, y);
-      float2_ sp_ = Project(H, (float)x, (float)y);
-      const float sp = OracleSample(S, src, sp_.x, sp_.y);
+      const float xf = (float)x, yf = (float)y;
+      const float Qx = fmaf(h1s, yf, fmaf(H.h[0], xf, H.h[2]) * 256.0f);
+      const float Qy = fmaf(h4s, yf, fmaf(H.h[3], xf, H.h[5]) * 256.0f);
+      const float iz = 1.0f / fmaf(H.h[7], yf, fmaf(H.h[6], xf, H.h[8]));
+      const float sp = OracleSampleQ(S, src, Qx, Qy, iz);
       const float w = BilateralWeight(S, i, j, rp, ref_center_pix);
       const float wr = w * rp;
       r_ref = r_ref + wr;
@@ -867,6 +881,24 @@ static void NeigbourUpdate(Pass& S, int x, int y) {
 }
 
 // ComputeMultiViewInitialCostandSelectedViews (DPE.cu:780-826)
+// The selection half of ComputeMultiViewInitialCostandSelectedViews (DPE.cu:800-825): sort the
+// cost vector (cv, zero-initialised past element 0 as `float cost_vector[32] = { 2.0f }`), average the
+// top_k smallest valid costs, select every view whose unsorted cost is <= the k-th smallest.
+static float TopKViews(float* cv, const float* cvc, int cost_count, int num_valid, int top_k_param, int nv,
+                       uint32_t* sel) {
+  const float cost_max = 2.0f;
+  sort_small(cv, cost_count);
+  *sel = 0;
+  int top_k = std::min(num_valid, top_k_param);
+  if (top_k > 0) {
+    float cost = 0.0f;
+    for (int i = 0; i < top_k; ++i) cost += cv[i];
+    float thr = cv[top_k - 1];
+    for (int i = 0; i < nv; ++i) if (cvc[i] <= thr) setBit(sel, i);
+    return cost / top_k;
+  }
+  return cost_max;
+}
 static float InitialCostAndViews(Pass& S, int x, int y) {
   const int center = x + y * S.W;
   float4_ pl = S.planes[center];
@@ -881,35 +913,29 @@ static float InitialCostAndViews(Pass& S, int x, int y) {
     cost_count++;
     if (c < cost_max) num_valid++;
   }
-  sort_small(cv, cost_count);
-  S.sel[center] = 0;
-  int top_k = std::min(num_valid, S.P.top_k);
-  if (top_k > 0) {
-    float cost = 0.0f;
-    for (int i = 0; i < top_k; ++i) cost += cv[i];
-    float thr = cv[top_k - 1];
-    for (int i = 0; i < S.N - 1; ++i) if (cvc[i] <= thr) setBit(&S.sel[center], i);
-    return cost / top_k;
-  }
-  return cost_max;
+  return TopKViews(cv, cvc, cost_count, num_valid, S.P.top_k, S.N - 1, &S.sel[center]);
 }
 
 // ComputeMultiViewInitialCost (DPE.cu:828-857)
-static float InitialCost(Pass& S, int x, int y) {
-  const int center = x + y * S.W;
-  float4_ pl = S.planes[center];
+template <class CostF>
+static float InitialCostOf(int N, uint32_t* sel, CostF ncc) {
   const float cost_max = 2.0f;
   int cost_count = 0;
   float cost = 0.0f;
-  for (int i = 1; i < S.N; ++i) {
-    if (isSet(S.sel[center], i - 1)) {
-      float c = NCCOld(S, x, y, i, pl);
+  for (int i = 1; i < N; ++i) {
+    if (isSet(*sel, i - 1)) {
+      float c = ncc(i);
       if (c < cost_max) { cost_count++; cost += c; }
-      else unSetBit(&S.sel[center], i - 1);
+      else unSetBit(sel, i - 1);
     }
   }
   if (cost_count == 0) return cost_max;
   return cost / cost_count;
+}
+static float InitialCost(Pass& S, int x, int y) {
+  const int center = x + y * S.W;
+  float4_ pl = S.planes[center];
+  return InitialCostOf(S.N, &S.sel[center], [&](int i) { return NCCOld(S, x, y, i, pl); });
 }
 
 // RandomInitialization (DPE.cu:1035-1063)
@@ -935,9 +961,17 @@ static void RandomInitialization(Pass& S, int x, int y) {
 }
 
 // Multi-hypothesis joint view selection shared by both sweeps (DPE.cu:1547-1615 / 1710-1779).
+template <class DrawF>
+static void ViewSelectionDraws(int nv, int iter, const float cost_array[8][32], const float* priors, DrawF draw,
+                               uint8_t* vw, uint32_t* tsv, float* wnorm);
 static void ViewSelection(Pass& S, int center, int iter, const float cost_array[8][32], const float* priors, Philox* rs,
                           uint8_t* vw, uint32_t* tsv, float* wnorm) {
-  const int nv = S.N - 1;
+  ViewSelectionDraws(S.N - 1, iter, cost_array, priors, [&]() { return rng_uniform(rs); }, vw, tsv, wnorm);
+  (void)center;
+}
+template <class DrawF>
+static void ViewSelectionDraws(int nv, int iter, const float cost_array[8][32], const float* priors, DrawF draw,
+                               uint8_t* vw, uint32_t* tsv, float* wnorm) {
   for (int i = 0; i < DPE_MAX_IMAGES; ++i) vw[i] = 0;
   float sp[32];
   for (int i = 0; i < 32; ++i) sp[i] = 0.0f;
@@ -954,7 +988,7 @@ static void ViewSelection(Pass& S, int center, int iter, const float cost_array[
   }
   TransformPDFToCDF(sp, nv);
   for (int s = 0; s < 15; ++s) {
-    const float rp = rng_uniform(rs) - FLT_EPSILON;
+    const float rp = draw() - FLT_EPSILON;
     for (int id = 0; id < nv; ++id) {
       if (sp[id] > rp) { vw[id] += 1; break; }
     }
@@ -962,7 +996,6 @@ static void ViewSelection(Pass& S, int center, int iter, const float cost_array[
   uint32_t t = 0; float wn = 0;
   for (int i = 0; i < nv; ++i) if (vw[i] > 0) { setBit(&t, i); wn += vw[i]; }
   *tsv = t; *wnorm = wn;
-  (void)center;
 }
 
 // PlaneHypothesisRefinementStrong (DPE.cu:1065-1118)
@@ -1872,6 +1905,56 @@ int oracle_local_refine_select(const float tc[11], const int ok[11], const float
                                float* out_depth) {
   return LocalRefineSelect(tc, ok, p_depth, cost_now, od, out_depth) ? 1 : 0;
 }
+// top-k view selection of ComputeMultiViewInitialCostandSelectedViews (DPE.cu:780-826) on the given
+// per-view costs (nv = num_images - 1); returns the cost, *sel the view mask
+float oracle_topk_views(const float* costs, int nv, int top_k, uint32_t* sel) {
+  float cv[32], cvc[32];
+  for (int i = 0; i < 32; ++i) { cv[i] = 0.0f; cvc[i] = 0.0f; }
+  cv[0] = 2.0f; cvc[0] = 2.0f;
+  int num_valid = 0;
+  for (int i = 0; i < nv; ++i) { cv[i] = costs[i]; cvc[i] = costs[i]; if (costs[i] < 2.0f) num_valid++; }
+  return TopKViews(cv, cvc, nv, num_valid, top_k, nv, sel);
+}
+// ComputeMultiViewInitialCost (DPE.cu:828-857) on the given per-view costs; *sel in/out
+float oracle_initial_cost(const float* costs, int nv, uint32_t* sel) {
+  return InitialCostOf(nv + 1, sel, [&](int i) { return costs[i - 1]; });
+}
+// the joint view selection (DPE.cu:1547-1615) with cost_array [8][32], priors [32] and the 15 draws
+// of curand_uniform given; vw [32] out
+void oracle_view_select(const float* cost_array, const float* priors, int nv, int iter, const float* draws, uint8_t* vw,
+                        uint32_t* tsv, float* wnorm) {
+  float ca[8][32];
+  std::memcpy(ca, cost_array, sizeof(ca));
+  int k = 0;
+  ViewSelectionDraws(nv, iter, ca, priors, [&]() { return draws[k++]; }, vw, tsv, wnorm);
+}
+// RANSACToGetFitPlane (DPE.cu:2891-3124) at (x, y) with the given planes [L][4], pixel states and
+// deformable neighbours [L][9] (short2); no edge or label maps (all edges absent, labels 0,
+// complexity 0).  out_plane: the fit plane, *out_radius: the radius map entry (strong_radius before).
+void oracle_ransac_fit(const DpePassInput* in, const float* planes, const uint8_t* weak, const int16_t* neighbours,
+                       int x, int y, int iter, float out_plane[4], int* out_radius) {
+  Pass S;
+  kat_pass(S, in);
+  const size_t L = (size_t)S.W * S.H;
+  S.planes.resize(L);
+  std::memcpy(S.planes.data(), planes, L * sizeof(float4_));
+  S.fit_plane.assign(L, {0, 0, 0, 0});
+  S.weak.assign(weak, weak + L);
+  S.neighbours.resize(L * 9);
+  std::memcpy(S.neighbours.data(), neighbours, L * 9 * sizeof(short2_));
+  S.complex_.assign(L, 0.0f);
+  S.label.assign(L, 0);
+  S.edge_neigh.assign(L * 8, mk_s2(-1, -1));
+  S.label_boundary.assign(L * 8, mk_s2(-1, -1));
+  S.LW = S.W; S.LH = S.H;
+  S.edge.assign(L, 0);
+  S.edge_low.assign(L, 0);
+  S.radius.assign(L, S.P.strong_radius);
+  RANSACFitPlane(S, x, y, iter);
+  const float4_ f = S.fit_plane[(size_t)y * S.W + x];
+  out_plane[0] = f.x; out_plane[1] = f.y; out_plane[2] = f.z; out_plane[3] = f.w;
+  *out_radius = S.radius[(size_t)y * S.W + x];
+}
 float oracle_expf(float x) { return o_expf(x); }
 float oracle_sinf(float x) { return o_sinf(x); }
 float oracle_cosf(float x) { return o_cosf(x); }
@@ -1882,7 +1965,7 @@ void oracle_philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t 
 float oracle_sample(const float* img, int W, int H, float sx, float sy) {
   Pass S; S.W = W; S.H = H;
   std::vector<float> im(img, img + (size_t)W * H);
-  return OracleSample(S, im, sx, sy);
+  return OracleSampleQ(S, im, sx * 256.0f, sy * 256.0f, 1.0f);   // the coordinate itself (iz = 1)
 }
 
 // dpe_pass_runner_fn (include/dpe_host.h) over the restatement, so tests can drive the C++ host

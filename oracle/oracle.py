@@ -68,6 +68,16 @@ def _load():
     lib.oracle_depth_normal.restype = None
     lib.oracle_local_refine_select.argtypes = [P(C.c_float), P(C.c_int), P(C.c_float), C.c_float, C.c_float, P(C.c_float)]
     lib.oracle_local_refine_select.restype = C.c_int
+    lib.oracle_topk_views.argtypes = [P(C.c_float), C.c_int, C.c_int, P(C.c_uint32)]
+    lib.oracle_topk_views.restype = C.c_float
+    lib.oracle_initial_cost.argtypes = [P(C.c_float), C.c_int, P(C.c_uint32)]
+    lib.oracle_initial_cost.restype = C.c_float
+    lib.oracle_view_select.argtypes = [P(C.c_float), P(C.c_float), C.c_int, C.c_int, P(C.c_float), P(C.c_uint8),
+                                       P(C.c_uint32), P(C.c_float)]
+    lib.oracle_view_select.restype = None
+    lib.oracle_ransac_fit.argtypes = [inp, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, P(C.c_float),
+                                      P(C.c_int)]
+    lib.oracle_ransac_fit.restype = None
     return lib
 
 
@@ -180,6 +190,51 @@ def local_refine_select(tc, ok, depths, cost_now: float, od: float) -> tuple:
     okv = (C.c_int * 11)(*[int(bool(v)) for v in ok])
     r = lib().oracle_local_refine_select(_f4(tc), okv, _f4(depths), cost_now, od, C.byref(d))
     return bool(r), d.value
+
+
+def topk_views(costs, top_k: int) -> tuple:
+    """Top-k selection of ComputeMultiViewInitialCostandSelectedViews on the given per-view costs."""
+    c = np.ascontiguousarray(costs, np.float32)
+    sel = C.c_uint32(0)
+    cost = lib().oracle_topk_views(c.ctypes.data_as(C.POINTER(C.c_float)), c.size, top_k, C.byref(sel))
+    return float(cost), sel.value
+
+
+def initial_cost(costs, sel: int) -> tuple:
+    """ComputeMultiViewInitialCost on the given per-view costs and view mask: (cost, new mask)."""
+    c = np.ascontiguousarray(costs, np.float32)
+    s = C.c_uint32(sel)
+    cost = lib().oracle_initial_cost(c.ctypes.data_as(C.POINTER(C.c_float)), c.size, C.byref(s))
+    return float(cost), s.value
+
+
+def view_select(cost_array, priors, iter_: int, draws) -> tuple:
+    """The joint view selection with cost_array [8][nv], priors [nv] and 15 uniform draws:
+    (view weights [nv], selected mask, weight norm)."""
+    nv = np.asarray(priors).size
+    ca = np.zeros((8, 32), np.float32)
+    ca[:, :nv] = cost_array
+    pr = np.zeros(32, np.float32)
+    pr[:nv] = priors
+    dr = np.ascontiguousarray(draws, np.float32)
+    vw = np.zeros(32, np.uint8)
+    tsv, wn = C.c_uint32(0), C.c_float(0)
+    lib().oracle_view_select(ca.ctypes.data_as(C.POINTER(C.c_float)), pr.ctypes.data_as(C.POINTER(C.c_float)), nv, iter_,
+                             dr.ctypes.data_as(C.POINTER(C.c_float)), vw.ctypes.data_as(C.POINTER(C.c_uint8)),
+                             C.byref(tsv), C.byref(wn))
+    return vw[:nv].copy(), tsv.value, wn.value
+
+
+def ransac_fit(pass_input: dict, planes, weak, neighbours, x: int, y: int, iter_: int = 0) -> tuple:
+    """RANSACToGetFitPlane at (x, y): (fit plane [4], radius)."""
+    b = _kat_buffers(pass_input)
+    pl = np.ascontiguousarray(planes, np.float32)
+    wk = np.ascontiguousarray(weak, np.uint8)
+    nb = np.ascontiguousarray(neighbours, np.int16)
+    out = (C.c_float * 4)()
+    rad = C.c_int(0)
+    lib().oracle_ransac_fit(C.byref(b.inp), pl.ctypes.data, wk.ctypes.data, nb.ctypes.data, x, y, iter_, out, C.byref(rad))
+    return np.array(out[:], np.float32), rad.value
 
 
 def philox(ctr, key) -> list:

@@ -453,3 +453,445 @@ def test_local_refine_selection_known_answers():
     acc, dep = oracle.local_refine_select([0.1] * 11, [0] * 11, d, 2.5, 9.0)
     assert (acc, dep) == (True, 9.0)
     assert oracle.local_refine_select([0.1] * 11, [0] * 11, d, 2.05, 9.0)[0] is False
+
+
+# ------------------------------------------------------------------------------ NCC-Old (strong cost)
+def literal_tex2d(img, x, y):
+    """tex2D<float>(img, x, y) with cudaFilterModeLinear, cudaAddressModeClamp and unnormalised
+    coordinates (DPE.cpp:919-935), as the CUDA programming guide's "Linear Filtering" appendix
+    specifies it: x_B = x - 0.5, i = floor(x_B), alpha = frac(x_B) held with 8 fractional bits
+    (taken here as round-to-nearest of 256 x_B), clamp addressing, then
+    (1-a)(1-b) T[i,j] + a(1-b) T[i+1,j] + (1-a) b T[i,j+1] + a b T[i+1,j+1]."""
+    H, W = img.shape
+    xb = f32(f32(x) - f32(0.5))
+    yb = f32(f32(y) - f32(0.5))
+    ux = math.floor(float(xb) * 256.0 + 0.5)
+    uy = math.floor(float(yb) * 256.0 + 0.5)
+    i, j = ux >> 8, uy >> 8
+    a, b = (ux & 255) / 256.0, (uy & 255) / 256.0
+    ci = lambda v, n: min(max(v, 0), n - 1)   # noqa: E731
+    t00, t10 = float(img[ci(j, H), ci(i, W)]), float(img[ci(j, H), ci(i + 1, W)])
+    t01, t11 = float(img[ci(j + 1, H), ci(i, W)]), float(img[ci(j + 1, H), ci(i + 1, W)])
+    return f32((1 - a) * (1 - b) * t00 + a * (1 - b) * t10 + (1 - a) * b * t01 + a * b * t11)
+
+
+def _literal_point_fn(ref, src, plane):
+    Hm = literal_homography(ref, src, plane)
+
+    def point(x, y):
+        x, y = f32(x), f32(y)
+        X = Hm[0] * x + Hm[1] * y + Hm[2]
+        Y = Hm[3] * x + Hm[4] * y + Hm[5]
+        Z = Hm[6] * x + Hm[7] * y + Hm[8]
+        return X / Z, Y / Z
+    return point
+
+
+def _literal_patch(ref_img, src_img, point, cx, cy, center, radius, increment, ss, sc):
+    """One bilateral patch NCC (the body shared by DPE.cu:715-775 and :609-668) in float32."""
+    cost_max = f32(2.0)
+    ss, sc = f32(ss), f32(sc)
+    s_ref = s_rr = s_src = s_ss = s_rs = s_w = f32(0)
+    for i in range(-radius, radius + 1, increment):
+        r_ref = r_rr = r_src = r_ss = r_rs = r_w = f32(0)
+        for j in range(-radius, radius + 1, increment):
+            rx, ry = cx + i, cy + j
+            rp = literal_tex2d(ref_img, f32(rx) + f32(0.5), f32(ry) + f32(0.5))
+            sx, sy = point(rx, ry)
+            sp = literal_tex2d(src_img, sx + f32(0.5), sy + f32(0.5))
+            sd = f32(math.sqrt(float(f32(i) * f32(i) + f32(j) * f32(j))))
+            w = f32(np.exp(-sd / (f32(2.0) * ss * ss) - abs(rp - center) / (f32(2.0) * sc * sc)))
+            r_ref += w * rp
+            r_rr += w * rp * rp
+            r_src += w * sp
+            r_ss += w * sp * sp
+            r_rs += w * rp * sp
+            r_w += w
+        s_ref += r_ref; s_rr += r_rr; s_src += r_src; s_ss += r_ss; s_rs += r_rs; s_w += r_w
+    inv = f32(1.0) / s_w
+    s_ref *= inv; s_rr *= inv; s_src *= inv; s_ss *= inv; s_rs *= inv
+    var_ref = s_rr - s_ref * s_ref
+    var_src = s_ss - s_src * s_src
+    if var_ref < f32(1e-5) or var_src < f32(1e-5):
+        return cost_max
+    cov = s_rs - s_ref * s_src
+    vrs = f32(math.sqrt(float(var_ref * var_src)))
+    return max(f32(0), min(cost_max, f32(1.0) - cov / vrs))
+
+
+def literal_ncc_old(ref_img, src_img, ref, src, plane, px, py, radius=5, increment=2, ss=5.0, sc=3.0):
+    """ComputeBilateralNCCOld + ComputeBilateralWeight (DPE.cu:550-555, 692-778) statement by
+    statement in float32 (each operation rounded once), the homography and projection of
+    DPE.cu:453-522 (literal_homography / literal_point's expressions) and literal_tex2d."""
+    point = _literal_point_fn(ref, src, plane)
+    ptx, pty = point(px, py)
+    if ptx >= src.width or ptx < 0 or pty >= src.height or pty < 0:
+        return 2.0
+    center = literal_tex2d(ref_img, f32(px) + f32(0.5), f32(py) + f32(0.5))
+    return float(_literal_patch(ref_img, src_img, point, px, py, center, radius, increment, ss, sc))
+
+
+def literal_ncc_new(ref_img, src_img, ref, src, plane, px, py, neighbours, sel, radius_map, view,
+                    strong_radius=5, strong_increment=2, weak_radius=5, weak_increment=5, ss=5.0, sc=3.0,
+                    use_radius=True):
+    """ComputeBilateralNCCNew (DPE.cu:557-690) of a WEAK pixel, literal float32 (the centre patch
+    k = 0 and the deformable neighbours k = 1..8; 0.25 centre + 0.75 mean of the neighbours)."""
+    point = _literal_point_fn(ref, src, plane)
+    W, H = ref.width, ref.height
+    ptx, pty = point(px, py)
+    if ptx >= src.width or ptx < 0 or pty >= src.height or pty < 0:
+        return 2.0
+    center = literal_tex2d(ref_img, f32(px) + f32(0.5), f32(py) + f32(0.5))
+    center_cost, strong_cost, strong_count = f32(0), f32(0), 0
+    for k in range(9):
+        nx, ny = int(neighbours[k][0]), int(neighbours[k][1])
+        if nx == -1 or ny == -1:
+            continue
+        nsx, nsy = point(nx, ny)
+        if nsx < 0 or nsy < 0 or nsx >= W or nsy >= H:
+            if k != 0:
+                if (int(sel[ny, nx]) >> (view - 1)) & 1:
+                    strong_cost += f32(2.0)
+                    strong_count += 1
+                continue
+            return 2.0
+        radius = strong_radius if k == 0 else weak_radius
+        increment = strong_increment if k == 0 else weak_increment
+        if use_radius and k == 0:
+            radius = int(radius_map[py, px])
+            increment = max(2, int(2.0 * radius / 5.0))
+        tc = _literal_patch(ref_img, src_img, point, nx, ny, center, radius, increment, ss, sc)
+        if k == 0:
+            center_cost = tc
+        else:
+            strong_cost += tc
+            strong_count += 1
+    if strong_count == 0:
+        return float(center_cost)
+    strong_cost = strong_cost / f32(strong_count)
+    strong_cost = min(strong_cost, f32(2.0))
+    return float(f32(0.25 * float(center_cost) + 0.75 * float(strong_cost)))
+
+
+def _textured_pair(rng, cams, plane, W, H):
+    """A reference image of smooth random texture (8-bit grey levels) and a source image that is its
+    warp under the true plane (float64 bilinear, rounded to 8 bits)."""
+    yy, xx = np.mgrid[0:H, 0:W].astype(np.float64)
+    tex = np.zeros((H, W))
+    for _ in range(6):
+        fx, fy, ph = rng.uniform(0.03, 0.35), rng.uniform(0.03, 0.35), rng.uniform(0, 6.3)
+        tex += rng.uniform(10, 40) * np.sin(fx * xx + fy * yy + ph)
+    ref_img = np.clip(np.rint(128 + tex + rng.normal(0, 3, (H, W))), 0, 255).astype(np.float32)
+    rK, rR, rt = cam_arrays(cams[0])
+    sK, sR, st = cam_arrays(cams[1])
+    n, w = np.array(plane[:3]), plane[3]
+    # source pixel -> reference pixel through the plane (world = reference-camera frame rotated)
+    src_img = np.zeros((H, W), np.float32)
+    Cs = -sR.T @ st
+    for v in range(H):
+        rays = sR.T @ np.linalg.solve(sK, np.stack([np.arange(W), np.full(W, v), np.ones(W)]))
+        # points Cs + s * ray in world; in the reference frame X_r = rR X_w + rt, on n.X_r + w = 0
+        a = n @ (rR @ rays)
+        b = n @ (rR @ Cs + rt) + w
+        s = -b / a
+        Xr = rR @ (Cs[:, None] + rays * s) + rt[:, None]
+        q = rK @ Xr
+        u_, v_ = q[0] / q[2], q[1] / q[2]
+        u0 = np.clip(np.floor(u_).astype(int), 0, W - 1)
+        v0 = np.clip(np.floor(v_).astype(int), 0, H - 1)
+        u1, v1 = np.clip(u0 + 1, 0, W - 1), np.clip(v0 + 1, 0, H - 1)
+        au, av = np.clip(u_ - u0, 0, 1), np.clip(v_ - v0, 0, 1)
+        val = ((1 - au) * (1 - av) * ref_img[v0, u0] + au * (1 - av) * ref_img[v0, u1] +
+               (1 - au) * av * ref_img[v1, u0] + au * av * ref_img[v1, u1])
+        src_img[v] = np.clip(np.rint(val), 0, 255)
+    return ref_img, src_img
+
+
+def test_ncc_old_matches_the_literal_float_sequence():
+    """The restated strong-sweep cost (oracle NCCOld: the re-associated homography, fma projection,
+    the single-rounding fixed-point tap coordinate of restatement choice 7, row-major tap order) is
+    within a stated bound of a literal float32 transcription of ComputeBilateralNCCOld with CUDA's
+    linear-filter texture semantics, over random rigs, textures and planes at costs between the
+    degenerate 0 and 2.  The two differ only where a tap coordinate sits within float32 rounding of a
+    1/256-px weight step (one weight step moves that tap by (b - a) / 256 grey levels)."""
+    rng = np.random.default_rng(21)
+    W, H = 160, 120
+    diffs, costs = [], []
+    for trial in range(6):
+        cams = rig(rng, W=W, H=H, n=2)
+        n0 = rng.standard_normal(3) * 0.2 + np.array([0.0, 0.0, -1.0])
+        n0 /= np.linalg.norm(n0)
+        depth = rng.uniform(4.0, 6.0)
+        true_plane = [float(f32(v)) for v in n0] + [float(f32(-depth * n0[2]))]
+        ref_img, src_img = _textured_pair(rng, cams, true_plane, W, H)
+        inp = pass_input(cams, images=[ref_img, src_img])
+        for k in range(40):
+            if k % 4 == 0:
+                plane = true_plane
+            else:                                          # perturbed normal / depth: intermediate costs
+                n = np.array(true_plane[:3]) + rng.standard_normal(3) * 0.1 * (k % 4)
+                n /= np.linalg.norm(n)
+                plane = [float(f32(v)) for v in n] + [float(f32(true_plane[3] * rng.uniform(0.94, 1.06)))]
+            x, y = int(rng.integers(8, W - 8)), int(rng.integers(8, H - 8))
+            got = oracle.ncc_old(inp, x, y, 1, plane)
+            want = literal_ncc_old(ref_img, src_img, cams[0], cams[1], plane, x, y)
+            if 0.0 < want < 2.0:
+                diffs.append(abs(got - want))
+                costs.append(want)
+    diffs, costs = np.array(diffs), np.array(costs)
+    # measured (seed 21): 207 NCCs, costs median 0.09 / max 1.86; |diff| median 2.6e-6, 90th
+    # percentile 1.5e-5, max 5.5e-5
+    assert len(diffs) > 150 and np.median(costs) > 0.05 and costs.max() > 1.0, (len(diffs), np.median(costs))
+    assert np.median(diffs) <= 1e-5, np.median(diffs)
+    assert np.percentile(diffs, 90) <= 5e-5, np.percentile(diffs, 90)
+    assert diffs.max() <= 2e-4, diffs.max()
+
+
+def test_ncc_new_matches_the_literal_float_sequence():
+    """NCC-New at non-degenerate costs: the restatement (tabulated in the weak sweep, PatchNCC in the
+    oracle) against the literal float32 transcription of DPE.cu:557-690, for WEAK pixels with eight
+    deformable support points (some projecting outside, with and without the view in their mask) over
+    random rigs, textures and planes."""
+    rng = np.random.default_rng(33)
+    W, H = 160, 120
+    diffs, costs = [], []
+    for trial in range(4):
+        cams = rig(rng, W=W, H=H, n=2)
+        n0 = rng.standard_normal(3) * 0.2 + np.array([0.0, 0.0, -1.0])
+        n0 /= np.linalg.norm(n0)
+        depth = rng.uniform(4.0, 6.0)
+        true_plane = [float(f32(v)) for v in n0] + [float(f32(-depth * n0[2]))]
+        ref_img, src_img = _textured_pair(rng, cams, true_plane, W, H)
+        inp = pass_input(cams, images=[ref_img, src_img], weak_radius=5, weak_increment=5)
+        weak = np.full((H, W), _abi.WEAK, np.uint8)
+        sel = (rng.integers(0, 2, (H, W)) * 1).astype(np.uint32)
+        rad = rng.choice([3, 5, 6, 8], (H, W)).astype(np.int32)
+        for k in range(12):
+            x, y = int(rng.integers(12, W - 12)), int(rng.integers(12, H - 12))
+            nb = np.full((H, W, 9, 2), -1, np.int16)
+            nb[y, x, 0] = (x, y)
+            for j in range(1, 9):
+                if rng.random() < 0.85:
+                    nb[y, x, j] = (int(np.clip(x + rng.integers(-30, 31), 0, W - 1)),
+                                   int(np.clip(y + rng.integers(-30, 31), 0, H - 1)))
+            if k % 3 == 0:
+                plane = true_plane
+            else:
+                n = np.array(true_plane[:3]) + rng.standard_normal(3) * 0.1 * (k % 3)
+                n /= np.linalg.norm(n)
+                plane = [float(f32(v)) for v in n] + [float(f32(true_plane[3] * rng.uniform(0.94, 1.06)))]
+            got = oracle.ncc_new(inp, weak, sel, nb, rad, x, y, 1, plane)
+            want = literal_ncc_new(ref_img, src_img, cams[0], cams[1], plane, x, y, nb[y, x], sel, rad, 1)
+            if 0.0 < want < 2.0:
+                diffs.append(abs(got - want))
+                costs.append(want)
+    diffs, costs = np.array(diffs), np.array(costs)
+    assert len(diffs) > 30 and np.median(costs) > 0.05 and costs.max() > 0.5, (len(diffs), np.median(costs), costs.max())
+    assert np.median(diffs) <= 2e-5, np.median(diffs)
+    assert diffs.max() <= 5e-4, diffs.max()
+
+
+# ------------------------------------------------------------------------------ view selection
+def literal_topk(costs, top_k):
+    """ComputeMultiViewInitialCostandSelectedViews' selection (DPE.cu:780-826): cost vectors
+    initialised { 2.0f } (element 0 only), insertion sort (sort_small, DPE.cu:5-14) of the nv costs,
+    mean of the top-k valid ones, views whose cost is <= the k-th smallest."""
+    nv = len(costs)
+    cv = [f32(2.0)] + [f32(0.0)] * 31
+    for i, c in enumerate(costs):
+        cv[i] = f32(c)
+    copy = list(cv)
+    num_valid = sum(1 for c in costs if f32(c) < f32(2.0))
+    for i in range(1, nv):                                      # sort_small
+        tmp, j = cv[i], i
+        while j >= 1 and tmp < cv[j - 1]:
+            cv[j] = cv[j - 1]
+            j -= 1
+        cv[j] = tmp
+    k = min(num_valid, top_k)
+    if k <= 0:
+        return 2.0, 0
+    cost = f32(0)
+    for i in range(k):
+        cost += cv[i]
+    thr = cv[k - 1]
+    sel = 0
+    for i in range(nv):
+        if copy[i] <= thr:
+            sel |= 1 << i
+    return float(cost / f32(k)), sel
+
+
+def literal_initial_cost(costs, sel):
+    """ComputeMultiViewInitialCost (DPE.cu:828-857) with unSetBit's quirk (DPE.cu:77-80: the mask
+    0xFFFFFFFE << n clears bits 0..n, not bit n alone)."""
+    cost, count = f32(0), 0
+    for i in range(1, len(costs) + 1):
+        if (sel >> (i - 1)) & 1:
+            c = f32(costs[i - 1])
+            if c < f32(2.0):
+                count += 1
+                cost += c
+            else:
+                sel &= (0xFFFFFFFE << (i - 1)) & 0xFFFFFFFF
+    return (2.0 if count == 0 else float(cost / f32(count))), sel
+
+
+def test_topk_view_selection_known_answers():
+    rng = np.random.default_rng(41)
+    for trial in range(300):
+        nv = int(rng.integers(1, 32))
+        c = rng.choice([0.1, 0.25, 0.5, 2.0], nv).astype(np.float32) if trial % 3 == 0 else \
+            np.where(rng.random(nv) < 0.2, 2.0, rng.uniform(0, 2, nv)).astype(np.float32)
+        top_k = int(rng.integers(1, 9))
+        got = oracle.topk_views(c, top_k)
+        want = literal_topk(c, top_k)
+        assert got[1] == want[1] and got[0] == pytest.approx(want[0], abs=0), (trial, c, top_k, got, want)
+    # ties at the threshold select every tied view; invalid (2.0) views never count
+    assert oracle.topk_views(np.array([0.3, 0.1, 0.3, 2.0, 0.3], np.float32), 2) == (pytest.approx(0.2), 0b10111)
+    assert oracle.topk_views(np.array([2.0, 2.0], np.float32), 4) == (2.0, 0)
+
+
+def test_initial_cost_unsetbit_quirk():
+    rng = np.random.default_rng(43)
+    for trial in range(300):
+        nv = int(rng.integers(1, 32))
+        c = np.where(rng.random(nv) < 0.3, 2.0, rng.uniform(0, 2, nv)).astype(np.float32)
+        sel = int(rng.integers(0, 1 << nv))
+        assert oracle.initial_cost(c, sel) == pytest.approx(literal_initial_cost(c, sel), abs=0), (trial, c, sel)
+    # views {0, 2, 3} with view 2 invalid: bits 0..2 cleared, only view 3 stays
+    got_cost, got_sel = oracle.initial_cost(np.array([0.2, 0.9, 2.0, 0.4], np.float32), 0b1101)
+    assert got_sel == 0b1000 and got_cost == pytest.approx(float((f32(0.2) + f32(0.4)) / f32(2)))
+
+
+def literal_view_select(cost_array, priors, it, draws):
+    """The joint view selection (DPE.cu:1566-1615): per-view sampling probability from the 8
+    candidates' costs, times the neighbour prior, to a CDF (TransformPDFToCDF :293-307), then 15
+    draws u - FLT_EPSILON, each counted on the first view whose CDF exceeds it."""
+    nv = len(priors)
+    thr = f32(0.8 * float(np.exp(f32(it * it) / f32(-90.0))))
+    sp = [f32(0)] * nv
+    for i in range(nv):
+        count, count_false, tmpw = f32(0), 0, f32(0)
+        for j in range(8):
+            c = f32(cost_array[j][i])
+            if c < thr:
+                tmpw += f32(np.exp(c * c / f32(-0.18)))
+                count += f32(1)
+            if c > f32(1.2):
+                count_false += 1
+        if count > 2 and count_false < 3:
+            sp[i] = tmpw / count
+        elif count_false < 3:
+            sp[i] = f32(np.exp(thr * thr / f32(-0.32)))
+        sp[i] = sp[i] * f32(priors[i])
+    tot = f32(0)
+    for i in range(nv):
+        tot += sp[i]
+    inv = f32(1.0) / tot
+    cum = f32(0)
+    cdf = []
+    for i in range(nv):
+        cum += sp[i] * inv
+        cdf.append(cum)
+    vw = [0] * nv
+    margin = []
+    for d in draws:
+        rp = f32(d) - f32(np.finfo(np.float32).eps)
+        margin.append(min(abs(float(c) - float(rp)) for c in cdf))
+        for i in range(nv):
+            if cdf[i] > rp:
+                vw[i] += 1
+                break
+    return np.array(vw, np.uint8), min(margin)
+
+
+def test_view_selection_known_answers():
+    """Weights and the CDF sampling from a fixed uniform sequence.  Cases whose draws fall within
+    1e-6 of a CDF step are skipped (the restated expf may differ from numpy's by an ulp there)."""
+    rng = np.random.default_rng(47)
+    checked = 0
+    for trial in range(400):
+        nv = int(rng.integers(2, 12))
+        it = int(rng.integers(0, 4))
+        ca = np.where(rng.random((8, nv)) < 0.15, rng.uniform(1.2, 2.0, (8, nv)),
+                      rng.uniform(0, 1.0, (8, nv))).astype(np.float32)
+        priors = rng.choice([0.0, 0.1, 0.2, 0.4, 0.9, 1.0, 1.8, 3.6], nv).astype(np.float32)
+        if priors.sum() == 0:
+            priors[0] = 0.9
+        draws = rng.uniform(1e-6, 1.0, 15).astype(np.float32)
+        want, margin = literal_view_select(ca, priors, it, draws)
+        if margin < 1e-6:
+            continue
+        vw, tsv, wn = oracle.view_select(ca, priors, it, draws)
+        assert np.array_equal(vw, want), (trial, vw, want)
+        assert tsv == sum(1 << i for i in range(nv) if want[i] > 0) and wn == float(want.sum())
+        checked += 1
+    assert checked > 350
+
+
+# ------------------------------------------------------------------------------ RANSAC plane fit
+def _ransac_case(W=64, H=48, support=((20, 12), (44, 14), (32, 38)), plane=(0.1, -0.05, -1.0, 5.0)):
+    K = np.array([[80.0, 0, 32.0], [0, 80.0, 24.0], [0, 0, 1.0]])
+    cam = camera(K, np.eye(3), np.zeros(3), W, H, dmin=1.0, dmax=20.0)
+    n = np.array(plane[:3], np.float64)
+    n /= np.linalg.norm(n)
+    w = plane[3]
+    pl = [float(f32(v)) for v in n] + [float(f32(w))]
+    planes = np.zeros((H, W, 4), np.float32)
+    planes[:, :] = pl
+    weak = np.full((H, W), _abi.STRONG, np.uint8)
+    nb = np.full((H, W, 9, 2), -1, np.int16)
+    x, y = 32, 24
+    weak[y, x] = _abi.WEAK
+    nb[y, x, 0] = (x, y)
+    for k, (sx, sy) in enumerate(support, start=1):
+        nb[y, x, k] = (sx, sy)
+    return cam, planes, weak, nb, x, y, pl
+
+
+def _expected_radius(A, B, C, x, y, strong_radius=5, edge_limit=False):
+    """DPE.cu:3057-3110 in float64 for the winning triangle (A, B, C): the triangle's radius, capped by
+    the nearest corner, rounded down to a multiple of 2.5 (the (r << 1) % 5 loop), then the
+    strong-radius rule without (0 / strong) or with (max) edge_limit."""
+    a, b, c = (math.dist(A, B), math.dist(B, C), math.dist(C, A))
+    p = (a + b + c) / 2
+    S = math.sqrt(p * (p - a) * (p - b) * (p - c))
+    r = int(math.floor(math.sqrt(S) / 2.0))
+    md = min(math.dist(A, (x, y)), math.dist(B, (x, y)), math.dist(C, (x, y)))
+    if 2.5 * md < r:
+        r = int(md)
+    while (r << 1) % 5 != 0:
+        r -= 1
+    if not edge_limit:
+        return 0 if r > strong_radius else strong_radius
+    return r if r > strong_radius else strong_radius
+
+
+def test_ransac_fit_known_answers():
+    # three support points around the pixel, their depths on one plane: the fit is that plane (its
+    # normal turned against the viewing ray), and the radius follows the triangle
+    for sup, pln in [(((20, 12), (44, 14), (32, 38)), (0.1, -0.05, -1.0, 5.0)),
+                     (((28, 20), (37, 21), (31, 29)), (-0.2, 0.1, -1.0, 4.0)),
+                     (((2, 2), (62, 3), (30, 46)), (0.0, 0.0, 1.0, -6.0))]:
+        for lim in (False, True):
+            cam, planes, weak, nb, x, y, pl = _ransac_case(support=sup, plane=pln)
+            inp = pass_input([cam, cam], use_limit=lim, use_edge=False, use_label=False, use_radius=True,
+                             geom_consistency=False, strong_radius=5)
+            fit, rad = oracle.ransac_fit(inp, planes, weak, nb, x, y)
+            n = np.array(pl[:3], np.float64)
+            ray = np.array([(x - 32.0) / 80.0, (y - 24.0) / 80.0, 1.0])
+            sgn = -1.0 if n @ ray > 0 else 1.0            # DPE.cu:3049-3055: facing the camera
+            assert np.allclose(fit[:3], sgn * n, atol=2e-5), (fit, sgn * n)
+            assert abs(fit[3] - sgn * pl[3]) <= 2e-5 * abs(pl[3]) + 1e-5, (fit, pl)
+            assert rad == _expected_radius(*sup, x, y, edge_limit=lim), (sup, lim, rad)
+    # the pixel outside every support triangle: no plane (zeros), radius = strong_radius
+    cam, planes, weak, nb, x, y, pl = _ransac_case(support=((40, 5), (60, 6), (50, 40)))
+    inp = pass_input([cam, cam], use_limit=False, use_edge=False, use_label=False, use_radius=True, strong_radius=5)
+    fit, rad = oracle.ransac_fit(inp, planes, weak, nb, x, y)
+    assert np.all(fit == 0) and rad == 5
+    # fewer than three support points: the pixel's own plane, radius untouched
+    cam, planes, weak, nb, x, y, pl = _ransac_case(support=((20, 12), (44, 14)))
+    planes[y, x] = (0.3, 0.2, -0.9, 7.0)
+    fit, rad = oracle.ransac_fit(inp, planes, weak, nb, x, y)
+    assert np.array_equal(fit, planes[y, x]) and rad == 5
