@@ -472,16 +472,19 @@ static int stage_impl(DpeContext* c, const DpePassInput* in, const StageSrc& src
   const dim3 pg((W + 3 + 15) / 16, (H + 2 + 15) / 16);
   if (in->image_ids) {   // device-resident images: upload and build layouts once per (id, size)
     CachedImage* ent[DPE_MAX_IMAGES];
+    const uint64_t call_clock = c->icache_clock;   // entries used by this call have last_use > call_clock
     for (int i = 0; i < N; ++i) {
       CachedImage* e = nullptr;
       for (CachedImage* q : c->icache)
         if (q->id == in->image_ids[i] && q->W == W && q->H == H) { e = q; break; }
       if (!e) {
-        size_t total = 0;   // keep the cache under 64 GiB: evict least recently used entries
-        for (CachedImage* q : c->icache) total += q->bytes();
-        while (total > (64ull << 30) && !c->icache.empty()) {
-          auto lru = std::min_element(c->icache.begin(), c->icache.end(),
-                                      [](const CachedImage* a, const CachedImage* b) { return a->last_use < b->last_use; });
+        size_t total = 0;   // keep the cache under 64 GiB: evict least recently used entries, never one
+        for (CachedImage* q : c->icache) total += q->bytes();   // this call already placed in ent[]
+        while (total > (64ull << 30)) {
+          auto lru = c->icache.end();
+          for (auto it = c->icache.begin(); it != c->icache.end(); ++it)
+            if ((*it)->last_use <= call_clock && (lru == c->icache.end() || (*it)->last_use < (*lru)->last_use)) lru = it;
+          if (lru == c->icache.end()) break;   // only this pass's own views are cached: keep them
           HIPC(hipStreamSynchronize(c->stream));
           total -= (*lru)->bytes();
           (*lru)->release(); delete *lru; c->icache.erase(lru);
@@ -665,6 +668,7 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
     for (size_t k = have; k < c->ev.size(); ++k) HIPC(hipEventCreate(&c->ev[k]));
   }
   int nev = 0;
+  bool slot_overflow = false;   // more timed sections than slots: fail the timed execute loudly
   std::vector<int> ev_class(timing ? max_slots : 0);
   for (int k = 0; k <= DPE_NUM_CLASSES; ++k) c->launches[k] = 0;
   static const char* const kClassName[DPE_NUM_CLASSES] = {"setup", "init", "strong", "ransac", "weak", "filter",
@@ -675,6 +679,7 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
     if (c->counting) Bc.cnt = c->cnt.p + 4 * cls;
     c->launches[cls]++;
     if (timing && nev < max_slots) { ev_class[nev] = cls; (void)hipEventRecord(c->ev[2 * nev], s); }
+    else if (timing) slot_overflow = true;
     return Bc;
   };
   auto end = [&]() {
@@ -837,6 +842,11 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   launch_local_refine(c->img8, (long)L, nv, s, dpc, Bc);
   end();
   HIPC(hipGetLastError());
+  if (slot_overflow) {   // per-class times would silently miss launches
+    HIPC(hipStreamSynchronize(s));
+    g_err = "dpe_pm_execute: more timed launch sections than timing slots (" + std::to_string(max_slots) + ")";
+    return DPE_ERR_STATE;
+  }
   if (timing && nev > 0) {
     HIPC(hipEventSynchronize(c->ev[2 * nev - 1]));
     for (int k = 0; k <= DPE_NUM_CLASSES; ++k) c->timings[k] = 0.0f;

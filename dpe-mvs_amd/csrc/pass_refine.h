@@ -202,7 +202,7 @@ DEV void lds_row(const float* pw, int px, int py, const PassConst& pc, const Dev
   }
 }
 #ifndef DPE_CLAMP_ELIDE
-#define DPE_CLAMP_ELIDE 1
+#define DPE_CLAMP_ELIDE 0
 #endif
 #ifndef DPE_ELIDE_UNIFORM
 #define DPE_ELIDE_UNIFORM 1
@@ -373,7 +373,6 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_depth_to_weak(const Pass
   if (lane != 0) return;
   B.weak[center] = d2w_class(pc, pcs, is_peak);
 }
-
 
 // ------------------------------------------------------------------------------ LocalRefine
 // LocalRefine with a flat job pool: a wave owns 4 pixels; every (pixel, hypothesis, selected view)

@@ -577,41 +577,57 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
       }
       if (world == 1 && failed) { err = first_err; return 1; }
       if (world > 1 && resident) {   // all-gather of the depth maps from / into the HBM-resident states
+        // Every rank joins the collective with the same count (nmax maps + a status float) whatever
+        // happened locally: a local error sets the status float and the rank sends from a host
+        // buffer through the host hook (the hooks are the same all-gather, so it matches the others'
+        // device-hook call), and every rank then fails together at this exchange.
         size_t nmax = 0;
         for (auto& b : blocks) nmax = std::max(nmax, b.size());
         const size_t per = (size_t)pw * ph, cnt = nmax * per + 1;   // + the status float
         float* dsend = dpe_device_buffer(runner.ctx, 0, cnt);
         float* drecv = dsend ? dpe_device_buffer(runner.ctx, 1, cnt * world) : nullptr;
-        if (!drecv) { err = dpe_last_error(); return 1; }
-        for (size_t k = 0; !failed && k < blocks[rank].size(); ++k)
+        bool dev_ok = drecv != nullptr;
+        if (!dev_ok) fail(dpe_last_error());
+        for (size_t k = 0; dev_ok && !failed && k < blocks[rank].size(); ++k)
           if (dpe_state_export_depth(runner.ctx, problems[blocks[rank][k]].ref_image_id, dsend + k * per, nullptr) != 0)
             fail(dpe_last_error());
-        const float flag = failed ? 1.0f : 0.0f;
-        if (dpe_device_copy(runner.ctx, dsend + nmax * per, &flag, sizeof(float), 0) != 0) { err = dpe_last_error(); return 1; }
-        std::vector<float> status(world);
-        if (opt.allgather_device) {
+        float flag = failed ? 1.0f : 0.0f;
+        if (dev_ok && dpe_device_copy(runner.ctx, dsend + nmax * per, &flag, sizeof(float), 0) != 0) {
+          fail(dpe_last_error());
+          dev_ok = false;
+        }
+        std::vector<float> status(world, 0.0f), hr;
+        if (dev_ok && opt.allgather_device) {
           if (opt.allgather_device(opt.allgather_device_user, dsend, cnt, drecv) != 0) { err = "all-gather failed"; return 1; }
-        } else {   // host hook: one device -> host -> device hop of the packed maps
-          std::vector<float> hs(cnt), hr(cnt * world);
-          if (dpe_device_copy(runner.ctx, hs.data(), dsend, cnt * sizeof(float), 1) != 0) { err = dpe_last_error(); return 1; }
+          for (int r = 0; r < world; ++r)
+            if (dpe_device_copy(runner.ctx, &status[r], drecv + (size_t)r * cnt + nmax * per, sizeof(float), 1) != 0) {
+              fail(dpe_last_error());   // the collective itself completed: every rank is past it
+              status[r] = 1.0f;
+            }
+        } else {   // host hook: one device -> host -> device hop of the packed maps (or a failure flag)
+          std::vector<float> hs(cnt, 0.0f);
+          if (dev_ok && dpe_device_copy(runner.ctx, hs.data(), dsend, cnt * sizeof(float), 1) != 0) {
+            fail(dpe_last_error());
+            dev_ok = false;
+          }
+          if (failed) hs[nmax * per] = 1.0f;
+          hr.assign(cnt * world, 0.0f);
           if (opt.allgather(opt.allgather_user, hs.data(), cnt, hr.data()) != 0) { err = "all-gather failed"; return 1; }
-          if (dpe_device_copy(runner.ctx, drecv, hr.data(), hr.size() * sizeof(float), 0) != 0) { err = dpe_last_error(); return 1; }
+          for (int r = 0; r < world; ++r) status[r] = hr[(size_t)r * cnt + nmax * per];
+          if (dev_ok && !failed && dpe_device_copy(runner.ctx, drecv, hr.data(), hr.size() * sizeof(float), 0) != 0) {
+            fail(dpe_last_error());
+          }
         }
         int bad = -1;
-        for (int r = 0; r < world; ++r) {
-          if (dpe_device_copy(runner.ctx, &status[r], drecv + (size_t)r * cnt + nmax * per, sizeof(float), 1) != 0) {
-            err = dpe_last_error(); return 1;
-          }
-          if (bad < 0 && status[r] != 0.0f) bad = r;
-        }
+        for (int r = 0; r < world; ++r) if (bad < 0 && status[r] != 0.0f) bad = r;
+        if (bad < 0 && failed) bad = rank;   // a local error after the collective
         if (bad >= 0) { err = bad == rank ? first_err : "rank " + std::to_string(bad) + " failed"; return 1; }
         for (int r = 0; r < world; ++r) {
           if (r == rank) continue;
           for (size_t k = 0; k < blocks[r].size(); ++k)
-            if (dpe_state_import_depth(runner.ctx, problems[blocks[r][k]].ref_image_id, pw, ph,
-                                       drecv + (size_t)r * cnt + k * per, nullptr) != 0) {
-              err = dpe_last_error(); return 1;
-            }
+            if (!failed && dpe_state_import_depth(runner.ctx, problems[blocks[r][k]].ref_image_id, pw, ph,
+                                                  drecv + (size_t)r * cnt + k * per, nullptr) != 0)
+              fail(dpe_last_error());   // reported at the next exchange (or the end): the others are past this one
         }
       } else if (world > 1) {   // all-gather of the depth maps (the pass's only cross-image data)
         size_t nmax = 0;

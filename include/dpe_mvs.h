@@ -157,10 +157,17 @@ int dpe_pm_stage(DpeContext* ctx, const DpePassInput* in, const DpePassState* st
  * Runs the whole pass (DPE.cu:3150-3226) on device-resident data on `stream` (a hipStream_t,
  * NULL = the context's stream).  Every call starts from the staged initial state, so repeated
  * calls are idempotent.  Asynchronous w.r.t. the host; ordered after the previous execute (the stream
- * waits on its completion event), and dpe_pm_stage / dpe_pm_fetch / dpe_destroy wait for it.  Part of the pass (GenNeighbours) runs on
- * the context's second stream, forked from and joined back into `stream` with events, so all
- * work is complete when `stream` reaches the end of the call's enqueued work (environment
- * DPE_OVERLAP=0, timing or counting keep everything on `stream`).
+ * waits on its completion event), and dpe_pm_stage / dpe_pm_fetch / dpe_destroy wait for it.
+ * Part of the pass runs on the context's second (aux) stream, forked from and joined back into
+ * `stream` with events, so all work is complete when `stream` reaches the end of the call's
+ * enqueued work (environment DPE_OVERLAP=0, timing or counting keep everything on `stream`).
+ * The aux stream runs the setup chain: GenEdgeInform, FindNearestStrongPoint's tables and search,
+ * the WEAK-pixel list, GenNeighbours and NeigbourUpdate.  Beside it `stream` runs
+ * RandomInitialization (reads planes/sel/images, writes planes/costs/sel) and the iteration-0
+ * colour-0 strong half-sweep, which waits for GenEdgeInform's event only (it reads the edge rays;
+ * it must not read nearest, nb, weak_rel or radius, which the aux stream is still writing); every
+ * later launch waits for the join.  tests/test_gpu_parity.py checks the forked and one-stream
+ * schedules bit for bit, including weak, sel and costs.
  */
 int dpe_pm_execute(DpeContext* ctx, void* stream);
 

@@ -122,13 +122,16 @@ def test_execute_idempotent_and_deterministic(ctx):
         assert bits_equal(a[k], b[k]), k
 
 
-def test_overlapped_and_sequential_schedules_agree(ctx):
-    # untimed executes run GenNeighbours on a second stream beside the first strong half-sweep;
-    # timed executes keep one stream.  Both must give the oracle's bits.
+@pytest.mark.parametrize("kind", ["refine_iter", "refine_init", "first"])
+def test_overlapped_and_sequential_schedules_agree(ctx, kind):
+    # untimed executes fork the setup chain (GenEdgeInform .. NeigbourUpdate) to the aux stream beside
+    # RandomInitialization and the first strong half-sweep; timed executes keep one stream.  Both
+    # must give the oracle's bits in every output (planes, weak, sel, costs), so a launch that reads a
+    # setup output before the join is caught (include/dpe_mvs.h, dpe_pm_execute).
     sc = synthetic.make_scene(128, 96, 6)
-    p = _params("refine_iter")
+    p = _params(kind)
     st = synthetic.gt_state(sc, seed=11)
-    inp = synthetic.pass_input(sc, p, depths=synthetic.src_depths(sc), seed=5)
+    inp = synthetic.pass_input(sc, p, depths=synthetic.src_depths(sc) if p.geom_consistency else None, seed=5)
     ctx.stage(inp, st)
     ctx.set_timing(True)
     ctx.execute(); seq = ctx.fetch()
