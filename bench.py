@@ -162,6 +162,43 @@ def end_to_end(local_rank: int, n_images: int, W: int, H: int, scene=None) -> di
             "note": "dpe_mvs() wall clock incl. JPEG decode, EdgeSegment, host I/O; value is per-pass HBM-resident"}
 
 
+def pipeline_config4(dist, rank: int, world: int, local_rank: int, n: int = 16, W: int = 2688, H: int = 1792) -> dict:
+    """BASELINE configs[3] at the pipeline level: 16 reference images at 2688x1792 (ETH3D high-res
+    size, 9 source views each) through DPE_MVS.run_dpe_pipeline -- decode, EdgeSegment, the full
+    coarse-to-fine schedule of RunDPEPipeline (main.cpp:508-566: 3 resolution rounds x 4 passes,
+    geometric consistency from the second pass on) and the outputs -- with the images sharded in
+    contiguous blocks over the ranks and the depth maps all-gathered between passes (RCCL device
+    hook under "nccl").  Wall time = max over ranks; rate = n * W * H / wall."""
+    import shutil
+    from DPE_MVS import pipeline, synthetic
+    tag = os.environ.get("TORCHELASTIC_RUN_ID") or os.environ.get("MASTER_PORT") or str(os.getpid())
+    folder = os.path.join("/tmp", f"dpe_cfg4_{tag}")
+    if rank == 0:
+        shutil.rmtree(folder, ignore_errors=True)
+        sc = synthetic.make_scene(W, H, n)
+        synthetic.write_dense_folder(folder, W, H, n, max_src=min(9, n - 1), with_edges=False, scene=sc)
+    if dist:
+        dist.barrier()
+    import torch
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    pipeline.run_dpe_pipeline(folder, gpu_index=local_rank, verbose=False, dist=dist if world > 1 else None)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        dist.barrier()
+    if rank == 0:
+        shutil.rmtree(folder, ignore_errors=True)
+    return {"config": "BASELINE configs[3]: ETH3D-size 2688x1792, 16 reference images, 9 source views each, "
+                      "full 3-round schedule, images sharded over the ranks (synthetic scene)",
+            "images": n, "width": W, "height": H, "ranks": world, "wall_s": round(dt, 3),
+            "mpix_s": round(n * W * H / dt / 1e6, 4),
+            "note": "pipeline wall incl. JPEG decode, EdgeSegment, 12 passes per image, depth all-gathers, .npy outputs"}
+
+
 def parity_on_sample(native, local_rank: int, sample) -> dict:
     """The metric's "L1 vs ref": the HIP pass on the cpu_baseline sample against the oracle's output
     of the same run (depth = plane .w; weak/selected-view maps compared exactly)."""
@@ -193,6 +230,7 @@ def main():
     ap.add_argument("--no-pass-types", action="store_true", help="skip the FIRST_INIT / REFINE_INIT passes (kernel traces)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end dpe_mvs() run")
     ap.add_argument("--e2e-images", type=int, default=10)
+    ap.add_argument("--no-pipeline", action="store_true", help="skip the BASELINE configs[3] pipeline line")
     ap.add_argument("--width", type=int, default=W_)
     ap.add_argument("--height", type=int, default=H_)
     args = ap.parse_args()
@@ -368,8 +406,13 @@ def main():
         "kernel_ms": {k: round(v, 3) for k, v in tim.items()},
         "work": {k: v for k, v in cnt.items() if v["launches"]},
     }
-    if rank == 0 and world == 1 and not args.no_e2e:
+    if not args.no_pipeline:   # every rank joins (the pipeline all-gathers depth maps between passes)
         ctx.close()
+        ctx = None
+        result["pipeline_config4"] = pipeline_config4(dist, rank, world, local_rank)
+    if rank == 0 and world == 1 and not args.no_e2e:
+        if ctx is not None:
+            ctx.close()
         ctx = None
         result["end_to_end"] = end_to_end(local_rank, args.e2e_images, Wd, Hd, scene=sc)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -277,13 +277,15 @@ def run_dpe_pipeline(dense_folder: str, gpu_index: int = 0, verbose: bool = True
                      viz: bool = False, depth: bool = True, normal: bool = False, weak: bool = False,
                      edge: bool = False, schedule: str = "reference", dist=None, runner=None,
                      base_seed: int = 0x5EED, keep_intermediate: bool = False, fusion_runner=None,
-                     max_iterations: int = 0, photometric_only: bool = False) -> int:
+                     max_iterations: int = 0, photometric_only: bool = False, allgather_device=None) -> int:
     """RunDPEPipeline (main.cpp:474) through libdpe_host.  `dist`: an initialised torch.distributed
     (one process per GPU; problems split in contiguous blocks, depth maps all-gathered per pass).
     `runner`: (C function pointer, user pointer) of a dpe_pass_runner_fn; default the HIP library.
     `fusion_runner`: (C function pointer, user pointer) of a dpe_fusion_fn; default the HIP kernel.
     `max_iterations` (0 = the reference's 3) and `photometric_only` (no geometric passes) are the
-    schedule knobs of BASELINE configs 1 and 2."""
+    schedule knobs of BASELINE configs 1 and 2.  `allgather_device`: a Python callable
+    (send_ptr, count, recv_ptr) -> int used as the device all-gather hook instead of the torch "nccl"
+    one (tests drive the device exchange path through it on one GPU)."""
     o = DpePipelineOptions()
     lib().dpe_pipeline_default_options(C.byref(o))
     o.gpu_index = gpu_index
@@ -299,7 +301,11 @@ def run_dpe_pipeline(dense_folder: str, gpu_index: int = 0, verbose: bool = True
         cb = _torch_allgather(dist)
         keep.append(cb)
         o.allgather = cb
-        if dist.get_backend() == "nccl" and runner is None:
+        if allgather_device is not None:
+            dcb = ALLGATHER_DEV_FN(lambda _user, send, count, recv: int(allgather_device(send, count, recv)))
+            keep.append(dcb)
+            o.allgather_device = C.cast(dcb, C.c_void_p)
+        elif dist.get_backend() == "nccl" and runner is None:
             dcb = _torch_allgather_device(dist)
             keep.append(dcb)
             o.allgather_device = C.cast(dcb, C.c_void_p)

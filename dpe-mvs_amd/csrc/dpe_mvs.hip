@@ -790,8 +790,8 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   auto strong_sweep = [&](const DevBufs& Bs, int it, const int* lst, const int* cnt) {
     const bool edge = pc.P.use_edge;
     const int P = edge ? 4 : 8, C = edge ? 16 : 8;
-    const size_t lds = (size_t)4 * strong_lds_per_wave(P, C, nv) * sizeof(float);
-    const unsigned grid = (unsigned)((L / 2 + 1 + 4 * P - 1) / (4 * P));
+    const size_t lds = (size_t)DPE_BW_STRONG * strong_lds_per_wave(P, C, nv) * sizeof(float);
+    const unsigned grid = (unsigned)((L / 2 + 1 + DPE_BW_STRONG * P - 1) / (DPE_BW_STRONG * P));
     launch_strong(edge, c->img8, grid, lds, s, dpc, Bs, it, lst, cnt);
   };
   for (int it = 0; it < pc.P.max_iterations; ++it) {

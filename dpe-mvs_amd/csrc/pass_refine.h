@@ -299,14 +299,20 @@ DEV uint8_t d2w_class(const PassConst& pc, const float* pcs, uint64_t is_peak) {
 }
 
 // grid: one wave per pixel, 4 waves per 256-thread workgroup.
+#ifndef DPE_BW_D2W
+#define DPE_BW_D2W 4
+#endif
+#ifndef DPE_BW_LR
+#define DPE_BW_LR 4
+#endif
 template <int U8>
-__global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_depth_to_weak(const PassConst* __restrict__ pcp, DevBufs B) {   // DPE.cu:2593-2747
-  __shared__ float s_patch[4][108];
-  __shared__ float s_pc[4][64];
+__global__ void __launch_bounds__(64 * DPE_BW_D2W, DPE_TAP_WAVES) k_depth_to_weak(const PassConst* __restrict__ pcp, DevBufs B) {   // DPE.cu:2593-2747
+  __shared__ float s_patch[DPE_BW_D2W][108];
+  __shared__ float s_pc[DPE_BW_D2W][64];
   const PassConst& pc = *pcp;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int W = pc.W, H = pc.H;
-  const long pix = (long)xcd_remap(blockIdx.x, gridDim.x, B.xcd_rows * 16 * ((pc.W + 3) / 4)) * 4 + wave;
+  const long pix = (long)xcd_remap(blockIdx.x, gridDim.x, B.xcd_rows * 16 * ((pc.W + DPE_BW_D2W - 1) / DPE_BW_D2W)) * DPE_BW_D2W + wave;
   if (pix >= (long)W * H) return;                 // wave-uniform
   const int x = (int)(pix % W), y = (int)(pix / W);
   const int center = (int)pix;
@@ -384,20 +390,21 @@ constexpr int kLrPix = 4;
 #define DPE_LR_VIEW_MAJOR 1
 #endif
 template <int U8>
-__global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_local_refine_jobs(const PassConst* __restrict__ pcp, DevBufs B) {   // DPE.cu:2749-2835
-  __shared__ float s_patch[4][kLrPix][108];
-  __shared__ float s_sum[4][kLrPix][3];
-  __shared__ float4 s_hyp[4][kLrPix][12];
-  extern __shared__ float s_dyn[];                // [4 waves][kLrPix][12][nv][2] job results
-  __shared__ float s_tc[4][kLrPix][12];
-  __shared__ float3 s_fw[4][kLrPix][12];          // geometric-consistency world point of each hypothesis
-  __shared__ uint8_t s_sel[4][kLrPix][DPE_MAX_IMAGES];
-  __shared__ int s_cnt[4][kLrPix][2];           // [0] selected views, [1] hypothesis mask (bit 11 = current)
+__global__ void __launch_bounds__(64 * DPE_BW_LR, DPE_TAP_WAVES) k_local_refine_jobs(const PassConst* __restrict__ pcp, DevBufs B) {   // DPE.cu:2749-2835
+  constexpr int BW = DPE_BW_LR;
+  __shared__ float s_patch[BW][kLrPix][108];
+  __shared__ float s_sum[BW][kLrPix][3];
+  __shared__ float4 s_hyp[BW][kLrPix][12];
+  extern __shared__ float s_dyn[];                // [BW waves][kLrPix][12][nv][2] job results
+  __shared__ float s_tc[BW][kLrPix][12];
+  __shared__ float3 s_fw[BW][kLrPix][12];         // geometric-consistency world point of each hypothesis
+  __shared__ uint8_t s_sel[BW][kLrPix][DPE_MAX_IMAGES];
+  __shared__ int s_cnt[BW][kLrPix][2];          // [0] selected views, [1] hypothesis mask (bit 11 = current)
   const PassConst& pc = *pcp;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int W = pc.W;
   const long L = (long)W * pc.H;
-  const long base = ((long)xcd_remap(blockIdx.x, gridDim.x, B.xcd_rows * 16 * ((pc.W + 15) / 16)) * 4 + wave) * kLrPix;
+  const long base = ((long)xcd_remap(blockIdx.x, gridDim.x, B.xcd_rows * 16 * ((pc.W + 4 * kLrPix - 1) / (4 * kLrPix))) * BW + wave) * kLrPix;
   if (base >= L) return;                          // wave-uniform
   const DpeCamera& c0 = pc.cams[0];
   const bool fast = DPE_FAST_PATCH(pc);

@@ -308,8 +308,11 @@ DEV bool job_decode(const int* cnt, int j, int& p, int& r) {
   return false;
 }
 
+#ifndef DPE_BW_STRONG
+#define DPE_BW_STRONG 4
+#endif
 template <int U8, bool EDGE>
-__global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_strong_coop(const PassConst* __restrict__ pcp, DevBufs B, int iter,
+__global__ void __launch_bounds__(64 * DPE_BW_STRONG, DPE_TAP_WAVES) k_strong_coop(const PassConst* __restrict__ pcp, DevBufs B, int iter,
                                                      const int* __restrict__ list, const int* __restrict__ nlist_p) {
   extern __shared__ float4 lds4[];
   float* lds = (float*)lds4;
@@ -321,7 +324,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_strong_coop(const PassCo
   const int ps = lane / C, c = lane % C;
   const int W = pc.W, nv = pc.N - 1;
   const DpeCamera& c0 = pc.cams[0];
-  const int wbase = (xcd_remap(blockIdx.x, gridDim.x, B.xcd_rows * 16) * 4 + wave) * P;
+  const int wbase = (xcd_remap(blockIdx.x, gridDim.x, B.xcd_rows * 16) * DPE_BW_STRONG + wave) * P;
   if (wbase >= nlist) return;                          // wave-uniform tail
   const int gi = wbase + ps;
   const bool active = gi < nlist;

@@ -25,6 +25,19 @@
 #define DPE_TEX_INIT TEX_F16
 #endif
 
+// Waves per workgroup of the tap kernels.  A workgroup's waves share one CU (and its L1), and its
+// waves take consecutive pixels, so a larger workgroup keeps neighbouring pixels' gathers (whose
+// patches overlap) in one L1.
+#ifndef DPE_BW_STRONG
+#define DPE_BW_STRONG 4
+#endif
+#ifndef DPE_BW_D2W
+#define DPE_BW_D2W 4
+#endif
+#ifndef DPE_BW_LR
+#define DPE_BW_LR 4
+#endif
+
 namespace dpe {
 constexpr int kTexInit = DPE_TEX_INIT, kTexStrong = DPE_TEX_STRONG, kTexWeak = DPE_TEX_WEAK;
 constexpr int kTexD2W = DPE_TEX_D2W, kTexLR = DPE_TEX_LR;

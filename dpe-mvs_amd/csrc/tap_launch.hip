@@ -18,26 +18,45 @@ namespace dpe {
 
 void launch_strong(bool edge, bool img8, unsigned grid, size_t lds, hipStream_t s, const PassConst* dpc,
                    const DevBufs& B, int it, const int* list, const int* count) {
+  constexpr int T = 64 * DPE_BW_STRONG;
+  if (lds > 65536) {   // dynamic LDS beyond the default limit (gfx950 has 160 KB per CU)
+    static bool once = false;
+    if (!once) {
+      once = true;
+      (void)hipFuncSetAttribute((const void*)k_strong_coop<kTexStrong, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)k_strong_coop<TEX_F32, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)k_strong_coop<kTexStrong, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)k_strong_coop<TEX_F32, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    }
+  }
   if (edge) {
-    if (img8) k_strong_coop<kTexStrong, true><<<grid, 256, lds, s>>>(dpc, B, it, list, count);
-    else k_strong_coop<TEX_F32, true><<<grid, 256, lds, s>>>(dpc, B, it, list, count);
+    if (img8) k_strong_coop<kTexStrong, true><<<grid, T, lds, s>>>(dpc, B, it, list, count);
+    else k_strong_coop<TEX_F32, true><<<grid, T, lds, s>>>(dpc, B, it, list, count);
   } else {
-    if (img8) k_strong_coop<kTexStrong, false><<<grid, 256, lds, s>>>(dpc, B, it, list, count);
-    else k_strong_coop<TEX_F32, false><<<grid, 256, lds, s>>>(dpc, B, it, list, count);
+    if (img8) k_strong_coop<kTexStrong, false><<<grid, T, lds, s>>>(dpc, B, it, list, count);
+    else k_strong_coop<TEX_F32, false><<<grid, T, lds, s>>>(dpc, B, it, list, count);
   }
 }
 
 void launch_depth_to_weak(bool img8, long L, hipStream_t s, const PassConst* dpc, const DevBufs& B) {
-  const unsigned g = (unsigned)((L + 3) / 4);
-  if (img8) k_depth_to_weak<kTexD2W><<<g, 256, 0, s>>>(dpc, B);
-  else k_depth_to_weak<TEX_F32><<<g, 256, 0, s>>>(dpc, B);
+  const unsigned g = (unsigned)((L + DPE_BW_D2W - 1) / DPE_BW_D2W);
+  if (img8) k_depth_to_weak<kTexD2W><<<g, 64 * DPE_BW_D2W, 0, s>>>(dpc, B);
+  else k_depth_to_weak<TEX_F32><<<g, 64 * DPE_BW_D2W, 0, s>>>(dpc, B);
 }
 
 void launch_local_refine(bool img8, long L, int nv, hipStream_t s, const PassConst* dpc, const DevBufs& B) {
-  const unsigned g = (unsigned)((L + 4 * kLrPix - 1) / (4 * kLrPix));
-  const size_t lds = (size_t)4 * kLrPix * 12 * nv * 2 * sizeof(float);
-  if (img8) k_local_refine_jobs<kTexLR><<<g, 256, lds, s>>>(dpc, B);
-  else k_local_refine_jobs<TEX_F32><<<g, 256, lds, s>>>(dpc, B);
+  const unsigned g = (unsigned)((L + DPE_BW_LR * kLrPix - 1) / (DPE_BW_LR * kLrPix));
+  const size_t lds = (size_t)DPE_BW_LR * kLrPix * 12 * nv * 2 * sizeof(float);
+  if (lds > 65536) {
+    static bool once = false;
+    if (!once) {
+      once = true;
+      (void)hipFuncSetAttribute((const void*)k_local_refine_jobs<kTexLR>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)k_local_refine_jobs<TEX_F32>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    }
+  }
+  if (img8) k_local_refine_jobs<kTexLR><<<g, 64 * DPE_BW_LR, lds, s>>>(dpc, B);
+  else k_local_refine_jobs<TEX_F32><<<g, 64 * DPE_BW_LR, lds, s>>>(dpc, B);
 }
 
 }  // namespace dpe

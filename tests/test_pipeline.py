@@ -202,14 +202,18 @@ def _rank_main(rank, world, port, folder):
         dist.destroy_process_group()
 
 
-def test_two_rank_jacobi_matches_one_rank(tmp_path, dense4):
+@pytest.mark.parametrize("world", [2, 3])
+def test_multi_rank_jacobi_matches_one_rank(tmp_path, dense4, world):
+    """2 ranks split the 4 problems evenly; 3 ranks unevenly (blocks {0}, {1}, {2, 3}, so ranks 0 and
+    1 pad their all-gather message to nmax = 2 maps, host/pipeline.cpp): both byte-identical to a
+    1-rank Jacobi run."""
     import torch.multiprocessing as mp
     one = _copy(dense4, tmp_path, "one")
-    two = _copy(dense4, tmp_path, "two")
+    many = _copy(dense4, tmp_path, "many")
     assert pipeline.run_dpe_pipeline(one, runner=oracle_runner(), schedule="jacobi", normal=True, weak=True,
                                      edge=True, verbose=False) == 0
-    mp.start_processes(_rank_main, args=(2, _free_port(), two), nprocs=2, join=True, start_method="spawn")
-    a, b = _outputs(one, 4), _outputs(two, 4)
+    mp.start_processes(_rank_main, args=(world, _free_port(), many), nprocs=world, join=True, start_method="spawn")
+    a, b = _outputs(one, 4), _outputs(many, 4)
     for k in a:
         assert a[k].dtype == b[k].dtype and a[k].tobytes() == b[k].tobytes(), k
 

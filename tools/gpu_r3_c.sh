@@ -4,5 +4,5 @@
 cd "$GRAFT_REPO_ROOT" || exit 1
 export PYTHONUNBUFFERED=1
 mkdir -p gpurun_out
-bash tools/gpu_tests_subset.sh r3c_parity tests/test_gpu_parity.py -k "not golden" || exit $?
-AB_NOCHECK=1 AB_ROUNDS=4 timeout -k 10 500 python -u tools/ab_libs.py "$@" > gpurun_out/r3c_ab.log 2>&1
+bash tools/gpu_tests_subset.sh ${TAG:-r3c}_parity tests/test_gpu_parity.py -k "not golden" || exit $?
+AB_NOCHECK=1 AB_ROUNDS=4 timeout -k 10 500 python -u tools/ab_libs.py "$@" > gpurun_out/${TAG:-r3c}_ab.log 2>&1
