@@ -26,8 +26,9 @@ lib.dpe_set_timing(ctx, 1)
 buf = (C.c_ulonglong * 16)()
 for fn in ("dpe_dbg_line_stats_main", "dpe_dbg_line_stats_tap"):
     getattr(lib, fn)(buf, 1)
-assert lib.dpe_pm_execute(ctx, None) == 0
-assert lib.dpe_pm_fetch(ctx, C.byref(bufs.st)) == 0
+rc = lib.dpe_pm_execute(ctx, None)
+assert rc == 0, (rc, lib.dpe_last_error())
+assert lib.dpe_pm_fetch(ctx, C.byref(bufs.st)) == 0, lib.dpe_last_error()
 tot = [0] * 16
 for fn in ("dpe_dbg_line_stats_main", "dpe_dbg_line_stats_tap"):
     getattr(lib, fn)(buf, 1)
