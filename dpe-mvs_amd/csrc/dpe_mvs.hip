@@ -365,6 +365,12 @@ extern "C" void dpe_dbg_line_stats_main(unsigned long long out[16], int reset) {
   if (reset) { unsigned long long z[16] = {}; (void)hipMemcpyToSymbol(HIP_SYMBOL(dpe::g_lstat), z, sizeof(z)); }
 }
 #endif
+#if DPE_WEAK_STATS
+extern "C" void dpe_dbg_weak_stats(unsigned long long out[24], int reset) {
+  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(dpe::g_wstat), sizeof(dpe::g_wstat));
+  if (reset) { unsigned long long z[24] = {}; (void)hipMemcpyToSymbol(HIP_SYMBOL(dpe::g_wstat), z, sizeof(z)); }
+}
+#endif
 
 extern "C" int dpe_pm_stage(DpeContext* c, const DpePassInput* in, const DpePassState* st) {
   g_err.clear();

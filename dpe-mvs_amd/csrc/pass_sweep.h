@@ -750,11 +750,58 @@ DEV void tab_taps(const PassConst& pc, const DevBufs& B, int v, const Homog& H0,
     acc[0] = s_src; acc[1] = s_ss; acc[2] = s_rs;
   }
 }
+// The fast tap loop of a runtime side n <= NMAX on one code path: rows and columns beyond n are
+// masked off, so lanes whose patches differ in size run together (same per-lane tap sequence and
+// sums as tab_taps<U8, true, n>).
+#ifndef DPE_WEAK_MASKED
+#define DPE_WEAK_MASKED 0
+#endif
+template <int U8, int NMAX>
+DEV void tab_taps_masked(const PassConst& pc, const DevBufs& B, int v, const Homog& H0, int cx, int cy, int rad, int inc,
+                         int n, const float* __restrict__ tw, float* acc) {
+  const int W = pc.W, Hh = pc.H;
+  const Homog H = scale_cols(H0);
+  const f2v* wp = (const f2v*)tw;
+  const uint32_t stride = tex_stride<U8>(W), vadj = tex_vadj<U8>((uint32_t)v * tex_view<U8>(B), stride);
+  const f2v tmax = tex_tmax2(W, Hh);
+  f2v s_sr = f2s(0.0f);
+  float s_ss = 0;
+#pragma unroll
+  for (int a = 0; a < NMAX; ++a) {
+    if (a < n) {
+      const float xf = (float)(cx - rad + a * inc);
+      const f2v bxy = fma2((f2v){H.h[0], H.h[3]}, f2s(xf), (f2v){H.h[2], H.h[5]}) * f2s(256.0f);
+      const float bz = __builtin_fmaf(H.h[6], xf, H.h[8]);
+      f2v r_sr = f2s(0.0f);
+      float r_ss = 0;
+#pragma unroll
+      for (int b = 0; b < NMAX; ++b) {
+        if (b < n) {
+          const float sp = tap_u8_fast<U8, false>(B, vadj, stride, tmax, H.h, bxy, bz, (float)(cy - rad + b * inc));
+          const f2v w = wp[a * n + b];
+          r_sr = fma2(w, f2s(sp), r_sr);
+          const float ws = w.x * sp;
+          r_ss = __builtin_fmaf(ws, sp, r_ss);
+        }
+      }
+      s_sr += r_sr; s_ss += r_ss;
+    }
+  }
+  acc[0] = s_sr.x; acc[1] = s_ss; acc[2] = s_sr.y;
+}
+
 template <int U8>
 DEV float patch_ncc_tab(const PassConst& pc, const DevBufs& B, int v, const Homog& H, int cx, int cy, int rad, int inc,
                         int n, const float* __restrict__ tw, const float* sm) {
   float a[3];
   if (rcp_range_ok(H, (float)(cx - rad), (float)(cx + rad), (float)(cy - rad), (float)(cy + rad))) {
+    if constexpr (DPE_WEAK_MASKED && U8 != TEX_F32 && DPE_PACKED_TAP) {
+      if (n >= 3 && n <= 6) {
+        tab_taps_masked<U8, 6>(pc, B, v, H, cx, cy, rad, inc, n, tw, a);
+        count_work(B, 0, (unsigned long long)(n * n));
+        return ncc_finalize_pre(sm[0], sm[1], sm[2], a[0], a[1], a[2]);
+      }
+    }
     switch (n) {
       case 3: tab_taps<U8, true, 3>(pc, B, v, H, cx, cy, rad, inc, n, tw, a); break;
       case 4: tab_taps<U8, true, 4>(pc, B, v, H, cx, cy, rad, inc, n, tw, a); break;
@@ -769,13 +816,44 @@ DEV float patch_ncc_tab(const PassConst& pc, const DevBufs& B, int v, const Homo
   return ncc_finalize_pre(sm[0], sm[1], sm[2], a[0], a[1], a[2]);
 }
 
+// Weak-sweep path statistics (build with -DDPE_WEAK_STATS=1; tools/weak_stats.py): per NCC-New,
+// the centre patch side and path, the neighbour-patch paths, and per wave the number of distinct
+// centre-patch variants its lanes execute one after another.  Off in the product.
+#ifndef DPE_WEAK_STATS
+#define DPE_WEAK_STATS 0
+#endif
+#if DPE_WEAK_STATS
+// 0 jobs, 1 centre outside, 2..11 n_c histogram (n 0..9, 9 = larger), 12 centre generic (untabulated),
+// 13 centre tabulated but slow reciprocal, 14 neighbour box fast, 15 neighbour patches, 16 neighbour
+// generic, 17 sum of distinct centre variants per wave call, 18 wave calls, 19 active lanes per wave call
+static __device__ unsigned long long g_wstat[24];
+DEV void wstat(int k, unsigned long long n = 1) { atomicAdd(&g_wstat[k], n); }
+DEV void wstat_variants(int variant) {
+  uint64_t rem = __ballot(1);
+  const int first = __builtin_ctzll(rem);
+  const unsigned long long act = __popcll(rem);
+  unsigned long long nv = 0;
+  while (rem) {
+    const int l = __builtin_ctzll(rem);
+    const int V = __shfl(variant, l);
+    rem &= ~__ballot(variant == V);
+    ++nv;
+  }
+  if ((int)(threadIdx.x & 63) == first) { wstat(17, nv); wstat(18); wstat(19, act); }
+}
+#define WSTAT(...) wstat(__VA_ARGS__)
+#else
+#define WSTAT(...) do {} while (0)
+#endif
+
 // ComputeBilateralNCCNew (DPE.cu:557-690) of the tabulated weak pixel (px, py)
 template <int U8>
 DEV float ncc_new_tab(const PassConst& pc, const DevBufs& B, const WeakTab& T, int px, int py, int v, const float4& pl) {
   const int W = pc.W, Hh = pc.H;
   const Homog H = make_homography(pc, v, pl);
   count_work(B, 1, 0);
-  if (center_outside(pc, v, H, px, py)) return 2.0f;
+  WSTAT(0);
+  if (center_outside(pc, v, H, px, py)) { WSTAT(1); return 2.0f; }
   float center_cost = 0.0f, strong_cost = 0.0f;
   int strong_count = 0;
   {   // k = 0: the pixel's own patch
@@ -783,6 +861,12 @@ DEV float ncc_new_tab(const PassConst& pc, const DevBufs& B, const WeakTab& T, i
     if (!(np.x == -1 || np.y == -1)) {
       const float2 nsp = project_h(H, (float)np.x, (float)np.y);
       if (nsp.x < 0 || nsp.y < 0 || nsp.x >= (float)W || nsp.y >= (float)Hh) return 2.0f;
+#if DPE_WEAK_STATS
+      WSTAT(2 + min(T.n_c, 9));
+      if (!T.tab_c) WSTAT(12);
+      else if (!rcp_range_ok(H, (float)(np.x - T.rad_c), (float)(np.x + T.rad_c), (float)(np.y - T.rad_c), (float)(np.y + T.rad_c))) WSTAT(13);
+      wstat_variants(T.tab_c ? T.n_c : 100 + T.n_c);
+#endif
       center_cost = T.tab_c ? patch_ncc_tab<U8>(pc, B, v, H, np.x, np.y, T.rad_c, T.inc_c, T.n_c, T.tc, T.sums)
                             : patch_ncc_generic<U8>(pc, B, v, H, np.x, np.y, T.rc, T.rad_c, T.inc_c);
     }
@@ -790,6 +874,7 @@ DEV float ncc_new_tab(const PassConst& pc, const DevBufs& B, const WeakTab& T, i
   // k = 1..8; one range check over the union of the 3x3 neighbour patches selects the fast
   // reciprocal for all of them (it is exact on every tap inside that box)
   const bool nfast = T.nb3 && rcp_range_ok(H, T.nbox[0], T.nbox[1], T.nbox[2], T.nbox[3]);
+  if (nfast) WSTAT(14);
 #pragma unroll 1
   for (int k = 1; k < DPE_NEIGHBOUR_NUM; ++k) {
     const short2 np = T.nbl[k];
@@ -800,6 +885,8 @@ DEV float ncc_new_tab(const PassConst& pc, const DevBufs& B, const WeakTab& T, i
       continue;
     }
     float tc;
+    WSTAT(15);
+    if (!nfast && !T.tab_n) WSTAT(16);
     if (nfast) {
       float a[3];
       tab_taps<U8, true, 3>(pc, B, v, H, np.x, np.y, T.rad_n, T.inc_n, 3, T.tn + (k - 1) * 18, a);
@@ -822,8 +909,11 @@ DEV float ncc_new_tab(const PassConst& pc, const DevBufs& B, const WeakTab& T, i
 #ifndef DPE_WEAK_VIEW_MAJOR
 #define DPE_WEAK_VIEW_MAJOR 1
 #endif
-// LDS floats per weak pixel (fixed part 480, see the carve in k_weak_coop); multiple of 4
-__host__ __device__ inline int weak_lds_per_pixel(int nv) { return (480 + 17 * nv + 3) & ~3; }
+#ifndef DPE_WEAK_POOL
+#define DPE_WEAK_POOL 1
+#endif
+// LDS floats per weak pixel (fixed part 496, see the carve in k_weak_coop); multiple of 4
+__host__ __device__ inline int weak_lds_per_pixel(int nv) { return (496 + 17 * nv + 3) & ~3; }
 
 // CheckerboardPropagationWeak (DPE.cu:1668-1862) + PlaneHypothesisRefinementWeak (:1120-1212).
 // C lanes per pixel, 64/C pixels per wave, blockDim.x/64 waves per workgroup.
@@ -862,7 +952,10 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassCons
   uint32_t* nsv = (uint32_t*)(pb + 452);                 // [9]
   int* alias = (int*)(pb + 464);                         // [8] earlier row with a bitwise-identical plane
   uint8_t* vwl = (uint8_t*)(pb + 472);                   // [32] view weights
-  float* cost = pb + 480;                                // [8][nv]
+  // [480..495] the pixel's header, read by the lanes of other pixels in the pooled phases: 0 rad_c,
+  // 1 inc_c, 2 n_c, 3 nb3, 4..7 nbox, 8..11 current plane, 12..15 fit plane ([351]: grey level)
+  int* hdr = (int*)(pb + 480);
+  float* cost = pb + 496;                                // [8][nv]
   float* sp = cost + 8 * nv;                             // [nv]
   int* sel_list = (int*)(sp + nv);                       // [nv]
   float* hv = (float*)(sel_list + nv);                   // [7][nv] hypothesis x selected-view values
@@ -881,6 +974,25 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassCons
   T.rc = active ? ref_texel(B.ref, W, Hh, x, y) : 0.0f;
   T.tc = tcp; T.tn = tnp; T.sums = sums; T.nbl = nbl; T.nsv = nsv;
   const short2* nbg = B.nb + (size_t)center * 9;
+#if DPE_WEAK_POOL
+  // pooled phases: the NCCs of all the wave's pixels are dealt round-robin over its 64 lanes (as
+  // in the strong sweep), so a job carries its pixel q; pix(q) = that pixel's LDS block
+  auto pix = [&](int q) -> float* { return (float*)lds4 + (size_t)(wave * P + q) * S; };
+  auto tab_of = [&](int q) -> WeakTab {
+    const float* qb = pix(q);
+    const int* h = (const int*)(qb + 480);
+    WeakTab t;
+    t.rad_c = h[0]; t.inc_c = h[1]; t.n_c = h[2]; t.nb3 = h[3] != 0;
+    t.rad_n = T.rad_n; t.inc_n = T.inc_n; t.n_n = T.n_n; t.tab_n = T.tab_n;
+    t.tab_c = t.n_c >= 1 && t.n_c <= 6;
+    t.rc = qb[351];
+    t.nbox[0] = qb[484]; t.nbox[1] = qb[485]; t.nbox[2] = qb[486]; t.nbox[3] = qb[487];
+    t.tc = qb + 108; t.tn = qb + 180; t.sums = qb + 324;
+    t.nbl = (const short2*)(qb + 440); t.nsv = (const uint32_t*)(qb + 452);
+    return t;
+  };
+  int pcnt[P];
+#endif
 
   PHASE_BEGIN();
   // ---- phase 1: neighbours, weight tables, Old-NCC patch, candidate rows
@@ -932,6 +1044,11 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassCons
   }
   // ---- phase 1b: reference sums of every tabulated patch (tap order of patch_ncc_generic)
   if (active) {
+    if (c == C - 2) {
+      hdr[0] = T.rad_c; hdr[1] = T.inc_c; hdr[2] = T.n_c; hdr[3] = T.nb3 ? 1 : 0;
+      pb[484] = T.nbox[0]; pb[485] = T.nbox[1]; pb[486] = T.nbox[2]; pb[487] = T.nbox[3];
+      pb[351] = T.rc;
+    }
     for (int k = c; k < 9; k += C) {
       const short2 np = nbl[k];
       if (np.x == -1 || np.y == -1 || !(k == 0 ? T.tab_c : T.tab_n)) continue;
@@ -969,6 +1086,34 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassCons
   wave_sync();
   PHASE(1);
   // ---- phase 2: candidate cost vectors, jobs (unique flagged neighbour plane, view)
+#if DPE_WEAK_POOL
+  if (active && c == 0) {
+    uint32_t um = 0;
+    for (int i = 0; i < 8; ++i) if (misc[8 + i] && alias[i] == i) um |= 1u << i;
+    misc[5] = (int)um;
+  }
+  wave_sync();
+  {
+    int Sj = 0;
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+      pcnt[q] = wbase + q < nlist ? __builtin_popcount((uint32_t)((const int*)(pix(q) + 424))[5]) : 0;
+      Sj += pcnt[q];
+    }
+    int q, r;
+    // view-major: the lanes of one round gather from the same source images
+    for (int j = lane; j < Sj * nv; j += 64) {
+      job_decode<P>(pcnt, j % Sj, q, r);
+      const int v = j / Sj + 1;
+      float* qb = pix(q);
+      uint32_t m = (uint32_t)((const int*)(qb + 424))[5];
+      for (; r > 0; --r) m &= m - 1;
+      const int i = __builtin_ctz(m);
+      const int cq = list[wbase + q];
+      (qb + 496)[i * nv + v - 1] = ncc_new_tab<U8>(pc, B, tab_of(q), cq % W, cq / W, v, ((const float4*)(qb + 356))[i]);
+    }
+  }
+#else
   if (active) {
     uint32_t um = 0;
     for (int i = 0; i < 8; ++i) if (misc[8 + i] && alias[i] == i) um |= 1u << i;
@@ -985,6 +1130,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassCons
       cost[i * nv + v - 1] = ncc_new_tab<U8>(pc, B, T, x, y, v, cpl[i]);
     }
   }
+#endif
   wave_sync();
   PHASE(2);
   if (active)
@@ -1019,6 +1165,10 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassCons
     for (int i = 0; i < nv; ++i) if (vwl[i] > 0) { setBit(tsv, i); wnorm += vwl[i]; sel_list[ns++] = i; }
     misc[0] = ns;
     misc[4] = __float_as_int(wnorm);
+#if DPE_WEAK_POOL
+    ((float4*)(pb + 488))[0] = B.planes[center];
+    ((float4*)(pb + 492))[0] = B.fit_plane[center];
+#endif
   }
   wave_sync();
   PHASE(5);
@@ -1032,12 +1182,40 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassCons
     return geom ? cn + gf * geom_cost(pc, B, x, y, v, pl) : cn;
   };
   // ---- phase 4: current plane and fit plane over the selected views; final candidate costs
+#if DPE_WEAK_POOL
+  // pixel q's hyp_cost term (view v, plane pl) into its hv row
+  auto hyp_val_q = [&](int q, int v, const float4& pl) __attribute__((always_inline)) -> float {
+    const int cq = list[wbase + q];
+    const int qx = cq % W, qy = cq / W;
+    const float cn = ncc_new_tab<U8>(pc, B, tab_of(q), qx, qy, v, pl);
+    return geom ? cn + gf * geom_cost(pc, B, qx, qy, v, pl) : cn;
+  };
+  auto nsel_of = [&](int q) -> int { return wbase + q < nlist ? ((const int*)(pix(q) + 424))[0] : 0; };
+  auto fit_of = [&](int q) -> bool {
+    const float4 f = ((const float4*)(pix(q) + 492))[0];
+    return !(f.x == 0 && f.y == 0 && f.z == 0);
+  };
+  {
+#pragma unroll
+    for (int q = 0; q < P; ++q) pcnt[q] = (fit_of(q) ? 2 : 1) * nsel_of(q);
+    int q, r;
+    for (int j = lane; job_decode<P>(pcnt, j, q, r); j += 64) {
+      float* qb = pix(q);
+      const int ns = ((const int*)(qb + 424))[0];
+      const int h = r / ns, k = r % ns;
+      const int v = ((const int*)(qb + 496 + 9 * nv))[k] + 1;
+      (qb + 496 + 10 * nv)[h * nv + k] = hyp_val_q(q, v, ((const float4*)(qb + (h ? 492 : 488)))[0]);
+    }
+  }
+  if (active) {
+#else
   if (active) {
     const int nj = (has_fit ? 2 : 1) * nsel;
     for (int j = c; j < nj; j += C) {
       const int h = j / nsel, k = j % nsel;
       hv[h * nv + k] = hyp_val(sel_list[k] + 1, h ? fp : cur);
     }
+#endif
     for (int i = c; i < 8; i += C) {
       const bool fl = misc[8 + i] != 0;
       const float3 fwi = (geom && fl) ? geom_point(pc, x, y, cpl[i]) : make_float3(0.0f, 0.0f, 0.0f);
@@ -1099,7 +1277,23 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassCons
   wave_sync();
   PHASE(7);
   // ---- phase 5: refinement NCCs, jobs (hypothesis, selected view)
+#if DPE_WEAK_POOL
+  {
+#pragma unroll
+    for (int q = 0; q < P; ++q) pcnt[q] = fit_of(q) ? 5 * nsel_of(q) : 0;
+    int q, r;
+    for (int j = lane; job_decode<P>(pcnt, j, q, r); j += 64) {
+      float* qb = pix(q);
+      const int ns = ((const int*)(qb + 424))[0];
+      const int h = r / ns, k = r % ns;
+      const int v = ((const int*)(qb + 496 + 9 * nv))[k] + 1;
+      (qb + 496 + 10 * nv)[(2 + h) * nv + k] = hyp_val_q(q, v, ((const float4*)(qb + 388))[h]);
+    }
+  }
+  if (false) {
+#else
   if (active && has_fit) {
+#endif
     for (int j = c; j < 5 * nsel; j += C) {
       const int h = j / nsel, k = j % nsel;
       hv[(2 + h) * nv + k] = hyp_val(sel_list[k] + 1, hyp[h]);
@@ -1131,7 +1325,23 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassCons
   wave_sync();
   PHASE(9);
   // ---- phase 6: the stored cost is the Old NCC of the final plane (DPE.cu:1845-1861)
+#if DPE_WEAK_POOL
+  {
+#pragma unroll
+    for (int q = 0; q < P; ++q) pcnt[q] = nsel_of(q);
+    int q, r;
+    for (int j = lane; job_decode<P>(pcnt, j, q, r); j += 64) {
+      float* qb = pix(q);
+      const int cq = list[wbase + q];
+      const int v = ((const int*)(qb + 496 + 9 * nv))[r] + 1;
+      (qb + 496 + 10 * nv)[r] = ncc_old_any<U8, true>(fast_old, qb, qb[352], qb[353], qb[354], cq % W, cq / W, pc, B, v,
+                                                      ((const float4*)(qb + 388))[5]);
+    }
+  }
+  if (false) {
+#else
   if (active) {
+#endif
     const float4 fin = hyp[5];
     for (int k = c; k < nsel; k += C)
       hv[k] = ncc_old_any<U8, true>(fast_old, pw, osum[0], osum[1], osum[2], x, y, pc, B, sel_list[k] + 1, fin);
