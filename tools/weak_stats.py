@@ -26,6 +26,7 @@ buf = (C.c_ulonglong * 24)()
 lib.dpe_dbg_weak_stats(buf, 1)
 rc = lib.dpe_pm_execute(ctx, None)
 assert rc == 0, (rc, lib.dpe_last_error())
+assert lib.dpe_pm_fetch(ctx, C.byref(bufs.st)) == 0, lib.dpe_last_error()   # joins the pass's streams
 lib.dpe_dbg_weak_stats(buf, 1)
 s = list(buf)
 jobs = max(1, s[0])
