@@ -912,8 +912,10 @@ DEV float ncc_new_tab(const PassConst& pc, const DevBufs& B, const WeakTab& T, i
 #ifndef DPE_WEAK_POOL
 #define DPE_WEAK_POOL 1
 #endif
-// LDS floats per weak pixel (fixed part 496, see the carve in k_weak_coop); multiple of 4
-__host__ __device__ inline int weak_lds_per_pixel(int nv) { return (496 + 17 * nv + 3) & ~3; }
+// LDS floats per weak pixel (fixed part kWeakFixed, see the carve in k_weak_coop); multiple of 4.
+// At 9 source views a pixel takes 636 floats, so four 4-wave workgroups (4 x 40.7 KB) fit a CU's LDS.
+constexpr int kWeakFixed = 480;
+__host__ __device__ inline int weak_lds_per_pixel(int nv) { return (kWeakFixed + 17 * nv + 3) & ~3; }
 
 // CheckerboardPropagationWeak (DPE.cu:1668-1862) + PlaneHypothesisRefinementWeak (:1120-1212).
 // C lanes per pixel, 64/C pixels per wave, blockDim.x/64 waves per workgroup.
@@ -947,15 +949,15 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassCons
   float4* cpl = (float4*)(pb + 356);                     // [8] candidate planes
   float4* hyp = (float4*)(pb + 388);                     // [7] refinement hypotheses / final plane
   float* fc = pb + 416;                                  // [8] final candidate costs
-  int* misc = (int*)(pb + 424);                          // 0 nsel, 1 ncand, 2 skip, 3 tsv, 4 wnorm, 8..15 flags
+  int* misc = (int*)(pb + 424);                          // 0 nsel, 1..3 + 6 header, 4 wnorm, 5 candidate mask, 8..15 flags
   short2* nbl = (short2*)(pb + 440);                     // [9]
   uint32_t* nsv = (uint32_t*)(pb + 452);                 // [9]
   int* alias = (int*)(pb + 464);                         // [8] earlier row with a bitwise-identical plane
   uint8_t* vwl = (uint8_t*)(pb + 472);                   // [32] view weights
-  // [480..495] the pixel's header, read by the lanes of other pixels in the pooled phases: 0 rad_c,
-  // 1 inc_c, 2 n_c, 3 nb3, 4..7 nbox, 8..11 current plane, 12..15 fit plane ([351]: grey level)
-  int* hdr = (int*)(pb + 480);
-  float* cost = pb + 496;                                // [8][nv]
+  // the pixel's header, read by the lanes of other pixels in the pooled phases, sits in free slots
+  // of the carve: misc[1] rad_c, misc[2] inc_c, misc[3] n_c, misc[6] nb3; nbox at [449..451], [461];
+  // grey level at [351]; fit plane in hyp[6]
+  float* cost = pb + kWeakFixed;                         // [8][nv]
   float* sp = cost + 8 * nv;                             // [nv]
   int* sel_list = (int*)(sp + nv);                       // [nv]
   float* hv = (float*)(sel_list + nv);                   // [7][nv] hypothesis x selected-view values
@@ -980,13 +982,13 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassCons
   auto pix = [&](int q) -> float* { return (float*)lds4 + (size_t)(wave * P + q) * S; };
   auto tab_of = [&](int q) -> WeakTab {
     const float* qb = pix(q);
-    const int* h = (const int*)(qb + 480);
+    const int* h = (const int*)(qb + 424);
     WeakTab t;
-    t.rad_c = h[0]; t.inc_c = h[1]; t.n_c = h[2]; t.nb3 = h[3] != 0;
+    t.rad_c = h[1]; t.inc_c = h[2]; t.n_c = h[3]; t.nb3 = h[6] != 0;
     t.rad_n = T.rad_n; t.inc_n = T.inc_n; t.n_n = T.n_n; t.tab_n = T.tab_n;
     t.tab_c = t.n_c >= 1 && t.n_c <= 6;
     t.rc = qb[351];
-    t.nbox[0] = qb[484]; t.nbox[1] = qb[485]; t.nbox[2] = qb[486]; t.nbox[3] = qb[487];
+    t.nbox[0] = qb[449]; t.nbox[1] = qb[450]; t.nbox[2] = qb[451]; t.nbox[3] = qb[461];
     t.tc = qb + 108; t.tn = qb + 180; t.sums = qb + 324;
     t.nbl = (const short2*)(qb + 440); t.nsv = (const uint32_t*)(qb + 452);
     return t;
@@ -1045,8 +1047,8 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassCons
   // ---- phase 1b: reference sums of every tabulated patch (tap order of patch_ncc_generic)
   if (active) {
     if (c == C - 2) {
-      hdr[0] = T.rad_c; hdr[1] = T.inc_c; hdr[2] = T.n_c; hdr[3] = T.nb3 ? 1 : 0;
-      pb[484] = T.nbox[0]; pb[485] = T.nbox[1]; pb[486] = T.nbox[2]; pb[487] = T.nbox[3];
+      misc[1] = T.rad_c; misc[2] = T.inc_c; misc[3] = T.n_c; misc[6] = T.nb3 ? 1 : 0;
+      pb[449] = T.nbox[0]; pb[450] = T.nbox[1]; pb[451] = T.nbox[2]; pb[461] = T.nbox[3];
       pb[351] = T.rc;
     }
     for (int k = c; k < 9; k += C) {
@@ -1110,7 +1112,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassCons
       for (; r > 0; --r) m &= m - 1;
       const int i = __builtin_ctz(m);
       const int cq = list[wbase + q];
-      (qb + 496)[i * nv + v - 1] = ncc_new_tab<U8>(pc, B, tab_of(q), cq % W, cq / W, v, ((const float4*)(qb + 356))[i]);
+      (qb + kWeakFixed)[i * nv + v - 1] = ncc_new_tab<U8>(pc, B, tab_of(q), cq % W, cq / W, v, ((const float4*)(qb + 356))[i]);
     }
   }
 #else
@@ -1166,8 +1168,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassCons
     misc[0] = ns;
     misc[4] = __float_as_int(wnorm);
 #if DPE_WEAK_POOL
-    ((float4*)(pb + 488))[0] = B.planes[center];
-    ((float4*)(pb + 492))[0] = B.fit_plane[center];
+    hyp[6] = B.fit_plane[center];
 #endif
   }
   wave_sync();
@@ -1192,7 +1193,7 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassCons
   };
   auto nsel_of = [&](int q) -> int { return wbase + q < nlist ? ((const int*)(pix(q) + 424))[0] : 0; };
   auto fit_of = [&](int q) -> bool {
-    const float4 f = ((const float4*)(pix(q) + 492))[0];
+    const float4 f = ((const float4*)(pix(q) + 388))[6];
     return !(f.x == 0 && f.y == 0 && f.z == 0);
   };
   {
@@ -1203,8 +1204,8 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassCons
       float* qb = pix(q);
       const int ns = ((const int*)(qb + 424))[0];
       const int h = r / ns, k = r % ns;
-      const int v = ((const int*)(qb + 496 + 9 * nv))[k] + 1;
-      (qb + 496 + 10 * nv)[h * nv + k] = hyp_val_q(q, v, ((const float4*)(qb + (h ? 492 : 488)))[0]);
+      const int v = ((const int*)(qb + kWeakFixed + 9 * nv))[k] + 1;
+      (qb + kWeakFixed + 10 * nv)[h * nv + k] = hyp_val_q(q, v, h ? ((const float4*)(qb + 388))[6] : B.planes[list[wbase + q]]);
     }
   }
   if (active) {
@@ -1286,8 +1287,8 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassCons
       float* qb = pix(q);
       const int ns = ((const int*)(qb + 424))[0];
       const int h = r / ns, k = r % ns;
-      const int v = ((const int*)(qb + 496 + 9 * nv))[k] + 1;
-      (qb + 496 + 10 * nv)[(2 + h) * nv + k] = hyp_val_q(q, v, ((const float4*)(qb + 388))[h]);
+      const int v = ((const int*)(qb + kWeakFixed + 9 * nv))[k] + 1;
+      (qb + kWeakFixed + 10 * nv)[(2 + h) * nv + k] = hyp_val_q(q, v, ((const float4*)(qb + 388))[h]);
     }
   }
   if (false) {
@@ -1333,8 +1334,8 @@ __global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassCons
     for (int j = lane; job_decode<P>(pcnt, j, q, r); j += 64) {
       float* qb = pix(q);
       const int cq = list[wbase + q];
-      const int v = ((const int*)(qb + 496 + 9 * nv))[r] + 1;
-      (qb + 496 + 10 * nv)[r] = ncc_old_any<U8, true>(fast_old, qb, qb[352], qb[353], qb[354], cq % W, cq / W, pc, B, v,
+      const int v = ((const int*)(qb + kWeakFixed + 9 * nv))[r] + 1;
+      (qb + kWeakFixed + 10 * nv)[r] = ncc_old_any<U8, true>(fast_old, qb, qb[352], qb[353], qb[354], cq % W, cq / W, pc, B, v,
                                                       ((const float4*)(qb + 388))[5]);
     }
   }
