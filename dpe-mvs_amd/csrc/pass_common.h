@@ -353,10 +353,20 @@ template <int T> DEV uint32_t tex_view(const DevBufs& B) {
 template <int T> constexpr uint32_t tex_bytes() { return T == TEX_F16 ? 8u : 4u; }
 template <int T> DEV uint32_t tex_stride(int W) { return (uint32_t)(W + (T == TEX_P16 ? 3 : 2)); }
 // the two row interpolations (r0 at y0, r1 at y1) of the texel at `p` for the raw x fraction fx
+// DPE_FAKE_GATHER=1: timing-only diagnostic (wrong results): the P16 / F16 texel comes from its
+// address bits instead of memory, so the tap loops keep their VALU work without the gathers
+#ifndef DPE_FAKE_GATHER
+#define DPE_FAKE_GATHER 0
+#endif
 template <int T>
 DEV void texel_rows(const uint8_t* p, float fx, float& r0, float& r1) {
   if constexpr (T == TEX_P16) {
+#if DPE_FAKE_GATHER
+    const uint32_t lo = (uint32_t)(uintptr_t)p;
+    const uint2 t = make_uint2((lo & 0x00FF00FFu) | 0x58005800u, (lo & 0x00FF00FFu) | 0x58005900u);
+#else
     const uint2 t = *(const uint2_a4*)p;                 // (a, c), (b, d)
+#endif
     const h2v df = __builtin_bit_cast(h2v, t.y) - __builtin_bit_cast(h2v, t.x);
     const uint32_t d = __builtin_bit_cast(uint32_t, df);
     const float ax = fx * 0.00390625f;
@@ -365,7 +375,12 @@ DEV void texel_rows(const uint8_t* p, float fx, float& r0, float& r1) {
   } else if constexpr (T == TEX_F16) {
     // v_fma_mix_f32 is fma(fx, (float)half, (float)half) with one rounding; the compiler only forms
     // it under f32 denormal flushing, which cannot matter here (|fx*d| >= 2^-8 or 0, a integer)
+#if DPE_FAKE_GATHER
+    const uint32_t lo = (uint32_t)(uintptr_t)p;
+    const uint2 t = make_uint2((lo & 0x00FF00FFu) | 0x58005800u, (lo & 0x00FF00FFu) | 0x20002000u);
+#else
     const uint2 t = *(const uint2*)p;
+#endif
     asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(r0) : "v"(fx), "v"(t.y), "v"(t.x));
     asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[0,1,1] op_sel_hi:[0,1,1]" : "=v"(r1) : "v"(fx), "v"(t.y), "v"(t.x));
   } else {
