@@ -153,6 +153,8 @@ struct DpeContext {
   DevArr<short2> nb, nearest, edge_neigh, lab_bound;
   DevArr<int> radius;
   DevArr<int> tab_right, tab_down;   // FindNearestStrongPoint tables
+  DevArr<int> gn_ovf;                // GenNeighbours pixels left to the scratch kernel (k_gen_neighbours_lds)
+  DevArr<float> gn_tab;              // normalised image coordinates per column / row (k_gn_tables)
   DevArr<int> lists, row_counts, list_totals;   // per-colour pixel lists for the sweeps
   DevBufs bufs;
   // fusion (dpe_fusion_stage / dpe_fusion_candidates)
@@ -198,6 +200,9 @@ void dpe_params_default(DpePatchMatchParams* p) {   // main.h:78-106
 
 const char* dpe_last_error(void) { return g_err.c_str(); }
 
+#ifndef DPE_GN_LDS
+#define DPE_GN_LDS 0   // scratch-free GenNeighbours (pass_kernels.h k_gen_neighbours_lds)
+#endif
 #ifndef DPE_EARLY_FORK
 #define DPE_EARLY_FORK 1
 #endif
@@ -287,7 +292,7 @@ void dpe_destroy(DpeContext* c) {
   c->e_rows.release(); c->e_mag.release(); c->e_itab.release(); c->e_dx.release(); c->e_dy.release();
   c->e_ftab.release(); c->e_stab.release();
   c->cnt.release();
-  c->tab_right.release(); c->tab_down.release();
+  c->tab_right.release(); c->tab_down.release(); c->gn_ovf.release(); c->gn_tab.release();
   c->lists.release(); c->row_counts.release(); c->list_totals.release();
   (void)hipStreamSynchronize(c->aux);
   (void)hipEventDestroy(c->ev_fork); (void)hipEventDestroy(c->ev_join); (void)hipEventDestroy(c->ev_ei);
@@ -623,6 +628,7 @@ static int stage_impl(DpeContext* c, const DpePassInput* in, const StageSrc& src
   HIPC(c->nb.ensure(L * 9)); HIPC(c->nearest.ensure(L)); HIPC(c->edge_neigh.ensure(L * 8)); HIPC(c->lab_bound.ensure(L * 8));
   HIPC(c->radius.ensure(L));
   HIPC(c->tab_right.ensure(L)); HIPC(c->tab_down.ensure(L));
+  HIPC(c->gn_ovf.ensure(L + 64)); HIPC(c->gn_tab.ensure((size_t)W + H));
   HIPC(c->lists.ensure(5 * (L / 2 + 64) + L + 64)); HIPC(c->row_counts.ensure(4 * (size_t)H + 4)); HIPC(c->list_totals.ensure(8));
   B.planes = c->planes.p; B.planes_snap = c->planes_snap.p; B.fit_plane = c->fit_plane.p;
   B.planes0 = c->planes0.p;
@@ -768,7 +774,19 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
       HIPC(hipEventRecord(c->ev_fork, s));
       HIPC(hipStreamWaitEvent(a, c->ev_fork, 0));
     }
+#if DPE_GN_LDS
+    if (pc.P.rotate_time <= 4) {   // probe slots in the reference's compaction order (dir_index < 32)
+      HIPC(hipMemsetAsync(c->list_totals.p + 6, 0, sizeof(int), a));
+      k_gn_tables<<<(unsigned)((W + H + 255) / 256), 256, 0, a>>>(dpc, c->gn_tab.p);
+      k_gen_neighbours_lds<<<(unsigned)((L + DPE_GN_BT - 1) / DPE_GN_BT), DPE_GN_BT, 0, a>>>(
+          dpc, Bgn, weak_list, c->list_totals.p + 4, c->gn_tab.p, c->gn_ovf.p, c->list_totals.p + 6);
+      k_gen_neighbours<<<(unsigned)((L + 255) / 256), 256, 0, a>>>(dpc, Bgn, c->gn_ovf.p, c->list_totals.p + 6);
+    } else
+#endif
     k_gen_neighbours<<<(unsigned)((L + 255) / 256), 256, 0, a>>>(dpc, Bgn, weak_list, c->list_totals.p + 4);
+#ifdef DPE_GN_TWICE   // timing-only sensitivity probe (not the reference's results)
+    k_gen_neighbours<<<(unsigned)((L + 255) / 256), 256, 0, a>>>(dpc, Bgn, weak_list, c->list_totals.p + 4);
+#endif
     k_neighbour_update<<<fg, fb, 0, a>>>(dpc, Bgn);
     if (overlap) {
       k_list_count<2><<<(pc.half_rows + 3) / 4, 256, 0, a>>>(dpc, Bgn, c->row_counts.p);

@@ -297,31 +297,58 @@ DEV float ref_texel(const float* ref, int W, int H, int x, int y) {
 // trunc(fma(q·iz, 256, 256.5)): a multiply, an FMA, a clamp and a half-rate conversion).  The clamp
 // is taken on t (monotone; NaN -> the low end), and the bound |256 s + 256| < 2^22 for unclamped taps
 // holds for images narrower than 16383 px (dpe_pm_stage checks).
+// DPE_TEX_FRACT=1 (round 4): the same U on the 1/256-unit grid of [2^15, 2^16) instead of the unit grid
+// of [2^23, 2^24): t' = fma(q, iz, 1.5·2^15 + 1) = t / 256 exactly (scaling by a power of two commutes
+// with the FMA's one rounding, and the row terms are no longer scaled), its encoding still differs
+// from that of 1.5·2^15 by U, and the tap's weight (U & 255) / 256 is v_fract_f32(t') straight from
+// the float (one full-rate op in place of v_cvt_f32_ubyte0 + a multiply per axis).
+#ifndef DPE_TEX_FRACT
+#define DPE_TEX_FRACT 0
+#endif
+#if DPE_TEX_FRACT
+constexpr float kTexMagic = 49152.0f;             // 1.5 * 2^15
+constexpr uint32_t kTexMagicBits = 0x47400000u;   // its encoding
+constexpr uint32_t kTexMagicHi = 0x474000u;       // encoding >> 8: texel index bias of t >> 8
+constexpr float kTexUnit = 1.0f;                  // one texel in t units
+#else
 constexpr float kTexMagic = 12582912.0f;          // 1.5 * 2^23
 constexpr uint32_t kTexMagicBits = 0x4B400000u;   // its encoding
 constexpr uint32_t kTexMagicHi = 0x4B4000u;       // encoding >> 8: texel index bias of t >> 8
-DEV float tex_tmax(int lim) { return kTexMagic + 256.0f * (float)(lim + 1); }   // t of U = 256 lim + 256
+constexpr float kTexUnit = 256.0f;
+#endif
+DEV float tex_tmax(int lim) { return kTexMagic + kTexUnit * (float)(lim + 1); }   // t of U = 256 lim + 256
 // clamped t of a tap with scaled row value Q (generic path: NaN -> kTexMagic)
 DEV float tex_t(float Q, float iz, float tmax) {
-  const float t = __builtin_fmaf(Q, iz, kTexMagic + 256.0f);
+  const float t = __builtin_fmaf(Q, iz, kTexMagic + kTexUnit);
   return __builtin_fminf(__builtin_fmaxf(t, kTexMagic), tmax);
+}
+// bilinear weight (U & 255) / 256 of a clamped t whose encoding is `bits`
+DEV float tex_frac(float t, uint32_t bits) {
+#if DPE_TEX_FRACT
+  (void)bits;
+  return __builtin_amdgcn_fractf(t);
+#else
+  (void)t;
+  return (float)(bits & 255u) * 0.00390625f;
+#endif
 }
 // The taps' numerators Q = 256 q: the column coefficients h1, h4 scaled by 256 here, the row terms
 // (h0 x + h2, h3 x + h5) scaled after their FMA (the oracle's OracleSampleQ caller does the same).
 DEV Homog scale_cols(const Homog& H) {
   Homog S = H;
-  S.h[1] = H.h[1] * 256.0f;
-  S.h[4] = H.h[4] * 256.0f;
+  S.h[1] = H.h[1] * kTexUnit;
+  S.h[4] = H.h[4] * kTexUnit;
   return S;
 }
 
 // Bilinear sample with 8-bit weights on the padded quad image (see oracle OracleSampleQ), at the
 // tap with scaled numerators (Qx, Qy) and reciprocal denominator iz.
 DEV float sample_quad(const float4* __restrict__ q, int W, int H, float Qx, float Qy, float iz) {
-  const uint32_t ux = __float_as_uint(tex_t(Qx, iz, tex_tmax(W))) - kTexMagicBits;
-  const uint32_t uy = __float_as_uint(tex_t(Qy, iz, tex_tmax(H))) - kTexMagicBits;
-  const float ax = (float)(ux & 255u) * 0.00390625f;
-  const float ay = (float)(uy & 255u) * 0.00390625f;
+  const float tx = tex_t(Qx, iz, tex_tmax(W)), ty = tex_t(Qy, iz, tex_tmax(H));
+  const uint32_t ux = __float_as_uint(tx) - kTexMagicBits;
+  const uint32_t uy = __float_as_uint(ty) - kTexMagicBits;
+  const float ax = tex_frac(tx, ux);
+  const float ay = tex_frac(ty, uy);
   const float4 t = q[(uy >> 8) * (W + 2) + (ux >> 8)];
   const float r0 = __builtin_fmaf(ax, t.y - t.x, t.x);
   const float r1 = __builtin_fmaf(ax, t.w - t.z, t.z);
@@ -331,11 +358,10 @@ DEV float sample_quad(const float4* __restrict__ q, int W, int H, float Qx, floa
 // grey levels); the other two hold 8-bit grey levels.  A quad texel holds the 2x2 neighbourhood
 // a=(x0,y0), b=(x1,y0), c=(x0,y1), d=(x1,y1) of its bilinear footprint:
 //   TEX_U8:  4 B, bytes (a, b, c, d)
-//   TEX_F16: 8 B, f16 (a, c, (b-a)/256, (d-c)/256): all exact (integers <= 255 and their
-//     differences scaled by a power of two), so fma(fx, (b-a)/256, a) with the raw 8-bit fraction
-//     fx equals the reference's fma(fx/256, b-a, a) bit for bit (the products are the same real
-//     number), and each row interpolation is one v_fma_mix_f32 on the loaded halves: 7 fewer
-//     VALU ops per tap than TEX_U8 for twice the bytes.
+//   TEX_F16: 8 B, f16 (a, c, b-a, d-c): all exact (integers of magnitude <= 255), so each row
+//     interpolation is one v_fma_mix_f32 on the loaded halves with the weight fx/256 (exact),
+//     bit for bit the reference's fma(fx/256, b-a, a): 7 fewer VALU ops per tap than TEX_U8 for
+//     twice the bytes.
 //   TEX_P16: 4 B column pairs, f16 (g(X-1, Y-1), g(X-1, Y)) at (X, Y), row stride W + 3: the quad
 //     texel (X, Y) is the 8 B at pair X (a, c) and pair X+1 (b, d), read with one unaligned 8-B
 //     load; the row differences are one packed f16 subtraction (exact: integers <= 255), so each row
@@ -352,14 +378,14 @@ template <int T> DEV uint32_t tex_view(const DevBufs& B) {
 }
 template <int T> constexpr uint32_t tex_bytes() { return T == TEX_F16 ? 8u : 4u; }
 template <int T> DEV uint32_t tex_stride(int W) { return (uint32_t)(W + (T == TEX_P16 ? 3 : 2)); }
-// the two row interpolations (r0 at y0, r1 at y1) of the texel at `p` for the raw x fraction fx
+// the two row interpolations (r0 at y0, r1 at y1) of the texel at `p` for the x weight ax = fx / 256
 // DPE_FAKE_GATHER=1: timing-only diagnostic (wrong results): the P16 / F16 texel comes from its
 // address bits instead of memory, so the tap loops keep their VALU work without the gathers
 #ifndef DPE_FAKE_GATHER
 #define DPE_FAKE_GATHER 0
 #endif
 template <int T>
-DEV void texel_rows(const uint8_t* p, float fx, float& r0, float& r1) {
+DEV void texel_rows(const uint8_t* p, float ax, float& r0, float& r1) {
   if constexpr (T == TEX_P16) {
 #if DPE_FAKE_GATHER
     const uint32_t lo = (uint32_t)(uintptr_t)p;
@@ -369,23 +395,21 @@ DEV void texel_rows(const uint8_t* p, float fx, float& r0, float& r1) {
 #endif
     const h2v df = __builtin_bit_cast(h2v, t.y) - __builtin_bit_cast(h2v, t.x);
     const uint32_t d = __builtin_bit_cast(uint32_t, df);
-    const float ax = fx * 0.00390625f;
     asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(r0) : "v"(ax), "v"(d), "v"(t.x));
     asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[0,1,1] op_sel_hi:[0,1,1]" : "=v"(r1) : "v"(ax), "v"(d), "v"(t.x));
   } else if constexpr (T == TEX_F16) {
-    // v_fma_mix_f32 is fma(fx, (float)half, (float)half) with one rounding; the compiler only forms
-    // it under f32 denormal flushing, which cannot matter here (|fx*d| >= 2^-8 or 0, a integer)
+    // v_fma_mix_f32 is fma(ax, (float)half, (float)half) with one rounding; the compiler only forms
+    // it under f32 denormal flushing, which cannot matter here (|ax*d| >= 2^-8 or 0, a integer)
 #if DPE_FAKE_GATHER
     const uint32_t lo = (uint32_t)(uintptr_t)p;
-    const uint2 t = make_uint2((lo & 0x00FF00FFu) | 0x58005800u, (lo & 0x00FF00FFu) | 0x20002000u);
+    const uint2 t = make_uint2((lo & 0x00FF00FFu) | 0x58005800u, (lo & 0x00FF00FFu) | 0x58005900u);
 #else
     const uint2 t = *(const uint2*)p;
 #endif
-    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(r0) : "v"(fx), "v"(t.y), "v"(t.x));
-    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[0,1,1] op_sel_hi:[0,1,1]" : "=v"(r1) : "v"(fx), "v"(t.y), "v"(t.x));
+    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(r0) : "v"(ax), "v"(t.y), "v"(t.x));
+    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[0,1,1] op_sel_hi:[0,1,1]" : "=v"(r1) : "v"(ax), "v"(t.y), "v"(t.x));
   } else {
     const uint32_t t = *(const uint32_t*)p;
-    const float ax = fx * 0.00390625f;
     const float t00 = (float)(t & 255u), t10 = (float)((t >> 8) & 255u);
     const float t01 = (float)((t >> 16) & 255u), t11 = (float)(t >> 24);
     r0 = __builtin_fmaf(ax, t10 - t00, t00);
@@ -395,11 +419,12 @@ DEV void texel_rows(const uint8_t* p, float fx, float& r0, float& r1) {
 // Same sampler on the 8-bit quad texels of one view: identical values to the f32 layout's.
 template <int T>
 DEV float sample_quad8(const uint8_t* __restrict__ q, int W, int H, float Qx, float Qy, float iz) {
-  const uint32_t ux = __float_as_uint(tex_t(Qx, iz, tex_tmax(W))) - kTexMagicBits;
-  const uint32_t uy = __float_as_uint(tex_t(Qy, iz, tex_tmax(H))) - kTexMagicBits;
-  const float ay = (float)(uy & 255u) * 0.00390625f;
+  const float tx = tex_t(Qx, iz, tex_tmax(W)), ty = tex_t(Qy, iz, tex_tmax(H));
+  const uint32_t ux = __float_as_uint(tx) - kTexMagicBits;
+  const uint32_t uy = __float_as_uint(ty) - kTexMagicBits;
+  const float ay = tex_frac(ty, uy);
   float r0, r1;
-  texel_rows<T>(q + (size_t)((uy >> 8) * tex_stride<T>(W) + (ux >> 8)) * tex_bytes<T>(), (float)(ux & 255u), r0, r1);
+  texel_rows<T>(q + (size_t)((uy >> 8) * tex_stride<T>(W) + (ux >> 8)) * tex_bytes<T>(), tex_frac(tx, ux), r0, r1);
   return __builtin_fmaf(ay, r1 - r0, r0);
 }
 // The default 36-tap patch (strong radius 5, increment 2) that the tabulated fast paths serve.
@@ -490,18 +515,19 @@ DEV float tap_u8_fast(const DevBufs& B, uint32_t vadj, uint32_t stride, f2v tmax
                       float yf) {
   const f2v q = fma2((f2v){h[1], h[4]}, f2s(yf), bxy);
   const float iz = d_rcp_fast(__builtin_fmaf(h[7], yf, bz));
-  const f2v t = fma2(q, f2s(iz), f2s(kTexMagic + 256.0f));
-  const uint32_t ux = __float_as_uint(tex_t_fast<IN>(t.x, tmax.x)), uy = __float_as_uint(tex_t_fast<IN>(t.y, tmax.y));
+  const f2v t = fma2(q, f2s(iz), f2s(kTexMagic + kTexUnit));
+  const float ctx = tex_t_fast<IN>(t.x, tmax.x), cty = tex_t_fast<IN>(t.y, tmax.y);
+  const uint32_t ux = __float_as_uint(ctx), uy = __float_as_uint(cty);
   const uint8_t* p = tex_base<T>(B) + (vadj + (__umul24(uy >> 8, stride) + (ux >> 8)) * tex_bytes<T>());
   LINE_STAT(T, p);
-  const float ay = (float)(uy & 255u) * 0.00390625f;
+  const float ay = tex_frac(cty, uy);
   if constexpr (T == TEX_F16 || T == TEX_P16) {
     float r0, r1;
-    texel_rows<T>(p, (float)(ux & 255u), r0, r1);
+    texel_rows<T>(p, tex_frac(ctx, ux), r0, r1);
     return __builtin_fmaf(ay, r1 - r0, r0);
   } else {
     const uint32_t tt = *(const uint32_t*)p;
-    const float ax = (float)(ux & 255u) * 0.00390625f;
+    const float ax = tex_frac(ctx, ux);
     const f2v lo = (f2v){(float)(tt & 255u), (float)((tt >> 16) & 255u)};
     const f2v hi = (f2v){(float)((tt >> 8) & 255u), (float)(tt >> 24)};
     const f2v r = fma2(f2s(ax), hi - lo, lo);
@@ -530,17 +556,19 @@ DEV f2v tap2_at(const uint8_t* base, uint32_t vadj, uint32_t stride, f2v tmax, c
 #else
   const f2v iz = fma2(fma2(-qz, r, f2s(1.0f)), r, r);
 #endif
-  const f2v tx = fma2(qx, iz, f2s(kTexMagic + 256.0f)), ty = fma2(qy, iz, f2s(kTexMagic + 256.0f));
-  const uint32_t ux0 = __float_as_uint(tex_t_fast<IN>(tx.x, tmax.x)), ux1 = __float_as_uint(tex_t_fast<IN>(tx.y, tmax.x));
-  const uint32_t uy0 = __float_as_uint(tex_t_fast<IN>(ty.x, tmax.y)), uy1 = __float_as_uint(tex_t_fast<IN>(ty.y, tmax.y));
+  const f2v tx = fma2(qx, iz, f2s(kTexMagic + kTexUnit)), ty = fma2(qy, iz, f2s(kTexMagic + kTexUnit));
+  const float cx0 = tex_t_fast<IN>(tx.x, tmax.x), cx1 = tex_t_fast<IN>(tx.y, tmax.x);
+  const float cy0 = tex_t_fast<IN>(ty.x, tmax.y), cy1 = tex_t_fast<IN>(ty.y, tmax.y);
+  const uint32_t ux0 = __float_as_uint(cx0), ux1 = __float_as_uint(cx1);
+  const uint32_t uy0 = __float_as_uint(cy0), uy1 = __float_as_uint(cy1);
   const uint8_t* p0 = base + (vadj + (__umul24(uy0 >> 8, stride) + (ux0 >> 8)) * tex_bytes<T>());
   const uint8_t* p1 = base + (vadj + (__umul24(uy1 >> 8, stride) + (ux1 >> 8)) * tex_bytes<T>());
   LINE_STAT(T, p0);
   LINE_STAT(T, p1);
-  const f2v ay = (f2v){(float)(uy0 & 255u), (float)(uy1 & 255u)} * f2s(0.00390625f);
+  const f2v ay = (f2v){tex_frac(cy0, uy0), tex_frac(cy1, uy1)};
   float a0, a1, b0, b1;
-  texel_rows<T>(p0, (float)(ux0 & 255u), a0, a1);
-  texel_rows<T>(p1, (float)(ux1 & 255u), b0, b1);
+  texel_rows<T>(p0, tex_frac(cx0, ux0), a0, a1);
+  texel_rows<T>(p1, tex_frac(cx1, ux1), b0, b1);
   const f2v r0 = (f2v){a0, b0}, r1 = (f2v){a1, b1};
   return fma2(ay, r1 - r0, r0);
 }
@@ -607,8 +635,8 @@ DEV void generic_taps(const PassConst& pc, const DevBufs& B, int v, const Homog&
     float r_ref = 0, r_src = 0, r_rr = 0, r_ss = 0, r_rs = 0, r_w = 0;
     const int x = cx + i;
     const float xf = (float)x;
-    const float bx = __builtin_fmaf(H.h[0], xf, H.h[2]) * 256.0f;
-    const float by = __builtin_fmaf(H.h[3], xf, H.h[5]) * 256.0f;
+    const float bx = __builtin_fmaf(H.h[0], xf, H.h[2]) * kTexUnit;
+    const float by = __builtin_fmaf(H.h[3], xf, H.h[5]) * kTexUnit;
     const float bz = __builtin_fmaf(H.h[6], xf, H.h[8]);
     for (int j = -radius; j <= radius; j += increment) {
       const int y = cy + j;
@@ -713,8 +741,8 @@ DEV void patch36_taps(const Patch36& P, const PassConst& pc, const DevBufs& B, i
 #pragma unroll
   for (int a = 0; a < 6; ++a) {
     const float x = (float)(P.px - 5 + 2 * a);
-    const float bx = __builtin_fmaf(H.h[0], x, H.h[2]) * 256.0f;
-    const float by = __builtin_fmaf(H.h[3], x, H.h[5]) * 256.0f;
+    const float bx = __builtin_fmaf(H.h[0], x, H.h[2]) * kTexUnit;
+    const float by = __builtin_fmaf(H.h[3], x, H.h[5]) * kTexUnit;
     const float bz = __builtin_fmaf(H.h[6], x, H.h[8]);
     float r_src = 0, r_ss = 0, r_rs = 0;
 #pragma unroll

@@ -466,6 +466,358 @@ __global__ void __launch_bounds__(256, DPE_GN_WAVES) k_gen_neighbours(const Pass
   PHASE_END_ALL(2);
 }
 
+// ------------------------------------------------------------------------------ GenNeighbours, scratch-free
+// The same GenNeighbours with no per-thread arrays (k_gen_neighbours keeps 2.3 KB/lane of them in
+// scratch, re-read from HBM on every RANSAC try).  The support points are appended in probe order,
+// which is the order of the reference's compaction of strong_points[] (dir_index grows through the
+// probe loops, the label extension follows at 32+), so they go straight into an LDS column per
+// thread: packed pixel and depth, kGnK slots ([slot][thread], conflict-free).  The normalised image
+// coordinates of a point come from per-column / per-row tables (`gtab`: the same expression per
+// coordinate), the edge tests are recomputed instead of cached (BresenhamLine is a pure function of
+// its end points; the reference's edge_test[][] only saves work), and the two sorts become
+// order-statistic selections whose results equal the insertion sorts' whenever no residual or
+// weight is NaN.  A pixel with more than kGnK support points, or a NaN where a sort needs the order,
+// writes nothing and is appended to `ovf` for k_gen_neighbours (its Philox stream is addressed by
+// the pixel, so the rerun draws the same numbers).
+constexpr int kGnK = 32;
+#ifndef DPE_GN_BT
+#define DPE_GN_BT 64
+#endif
+// table of the normalised image coordinates: gtab[x] = (x - K[2]) / K[0], gtab[W + y] = (y - K[5]) / K[4]
+__global__ void k_gn_tables(const PassConst* __restrict__ pcp, float* __restrict__ gtab) {
+  const PassConst& pc = *pcp;
+  const DpeCamera& camera = pc.cams[0];
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < pc.W) gtab[i] = ((float)i - camera.K[2]) / camera.K[0];
+  else if (i < pc.W + pc.H) gtab[i] = ((float)(i - pc.W) - camera.K[5]) / camera.K[4];
+}
+// BresenhamLine for walks of at most 16 steps per direction (high-resolution images: max_step =
+// round(max(LH, LW) / 60)): all positions of both directions generated first and their low-res edge
+// bytes loaded together, one memory round trip; the result is the OR over the visited positions.
+DEV bool bresenham_short(const PassConst& pc, const DevBufs& B, int Ax, int Ay, int Bx, int By, int max_step) {
+  const int W = pc.W;
+  const uint8_t ea = B.edge[Ax + Ay * W], eb = B.edge[Bx + By * W];
+  const float scale_x = 1.0f * pc.LW / (float)pc.W;
+  const float scale_y = 1.0f * pc.LH / (float)pc.H;
+  const int height = pc.LH, width = pc.LW;
+  int idx[2][16];
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    const int fx = pass == 0 ? Bx : Ax, fy = pass == 0 ? By : Ay;
+    const int tx = pass == 0 ? Ax : Bx, ty = pass == 0 ? Ay : By;
+    int x0 = (int)MINo(__builtin_roundf(fx * scale_x), (float)(width - 1));
+    int y0 = (int)MINo(__builtin_roundf(fy * scale_y), (float)(height - 1));
+    const int x1 = (int)MINo(__builtin_roundf(tx * scale_x), (float)(width - 1));
+    const int y1 = (int)MINo(__builtin_roundf(ty * scale_y), (float)(height - 1));
+    const int dx = abs(x1 - x0), sx = x0 < x1 ? 1 : -1;
+    const int dy = abs(y1 - y0), sy = y0 < y1 ? 1 : -1;
+    int erro = (dx > dy ? dx : dy) / 2;
+    bool tagx = true, tagy = true;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      idx[pass][k] = -1;                                  // low_edge_at(-1) == 0
+      if (k < MAXo(max_step, 1) && (tagx || tagy)) {     // the first step is taken before the limit test
+        if (x0 == x1) tagx = false;
+        if (y0 == y1) tagy = false;
+        const int e2 = erro;
+        if (e2 > -dx) { erro -= dy; x0 += sx; }
+        if (e2 < dy) { erro += dx; y0 += sy; }
+        idx[pass][k] = x0 + y0 * width;
+      }
+    }
+  }
+  uint8_t hit = 0;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) hit |= low_edge_at(pc, B, idx[pass][k]);
+  return !(ea || eb) && hit != 0;
+}
+
+__global__ void __launch_bounds__(DPE_GN_BT) k_gen_neighbours_lds(const PassConst* __restrict__ pcp, DevBufs B,
+                                                                  const int* __restrict__ list, const int* __restrict__ nlist_p,
+                                                                  const float* __restrict__ gtab, int* __restrict__ ovf,
+                                                                  int* __restrict__ novf) {   // DPE.cu:2103-2463
+  __shared__ uint32_t s_pt[kGnK][DPE_GN_BT];    // support point (x | y << 16)
+  __shared__ float s_dp[kGnK][DPE_GN_BT];       // its depth, then (after the RANSAC) its weight
+  const PassConst& pc = *pcp;
+  const int t = threadIdx.x;
+  const int gi = xcd_remap(blockIdx.x, gridDim.x, B.xcd_rows * 64) * DPE_GN_BT + t;
+  if (gi >= *nlist_p) return;
+  const int W = pc.W, H = pc.H;
+  const int center = list[gi];
+  const int x = center % W, y = center / W;
+  const int min_margin = 6;
+  const float depth_diff = pc.P.depth_max - pc.P.depth_min;
+  const DpeCamera& camera = pc.cams[0];
+  Rng rs; rng_init(rs, (uint32_t)center, pc.seed32, STREAM_GEN_NEIGHBOURS, pc.salt);
+  int valid_count = 0;
+  bool overflow = false;
+  auto push = [&](short2 np) {
+    if (valid_count < kGnK) s_pt[valid_count][t] = (uint32_t)(uint16_t)np.x | ((uint32_t)(uint16_t)np.y << 16);
+    else overflow = true;
+    valid_count++;
+  };
+  auto pt_at = [&](int i) -> short2 {
+    const uint32_t v = s_pt[i][t];
+    return make_short2((short)(v & 0xFFFFu), (short)(v >> 16));
+  };
+  const int rotate_time = pc.P.rotate_time;
+  const float cos_angle = pc.gn_cos, sin_angle = pc.gn_sin, threshhold = pc.gn_thr;
+  const int shift_range = pc.gn_shift;
+  const float ransac_threshold = pc.P.ransac_threshold * depth_diff;
+  const int max_step = pc.P.high_res_img ? (int)__builtin_round(MAXo(pc.LH, pc.LW) / 60.0) : MAXo(pc.LH, pc.LW);
+  auto crosses = [&](int ax, int ay, int bx, int by) -> bool {
+    return max_step <= 16 ? bresenham_short(pc, B, ax, ay, bx, by, max_step) : bresenham(pc, B, ax, ay, bx, by);
+  };
+  bool edge_limit = false;
+  float complex_new = -1.0f;                       // complex_[center] to write once the pixel is done
+  if (pc.P.use_limit) {
+    edge_limit = true;
+    if (pc.P.use_edge) {
+      const float cv = B.complex_[center];
+      const float rp = rng_uniform(rs) - 1.1920929e-07f;
+      if (rp < cv) edge_limit = false;
+      else complex_new = MAXo(0.99f, cv);
+    }
+  }
+  for (int odx = -1; odx <= 1; ++odx) {
+    for (int ody = -1; ody <= 1; ++ody) {
+      if (odx == 0 && ody == 0) continue;
+      float2 od = make_float2((float)odx, (float)ody);
+      normalize2(od);
+      for (int rotate_iter = 0; rotate_iter < rotate_time; ++rotate_iter) {
+        bool dir_found = false;
+        for (int radius = 2; radius <= 4096 && !dir_found; radius = MINo(radius * 2, radius + 25)) {
+          const float tpx = (float)x + od.x * radius, tpy = (float)y + od.y * radius;
+          if (tpx < 0 || tpy < 0 || tpx >= W || tpy >= H) break;
+          // 4 attempts at a time: draws, targets and weak[] / nearest[] loads issued first, then tested
+          // in order; the stream is put back to just after the attempt that succeeded
+          short2 cand[4], nnv[4];
+          uint8_t wkv[4];
+          bool inm[4];
+          uint32_t rb[4][4], rc[4];
+          int ri[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const uint32_t r1 = rng_u32(rs); const uint32_t r2 = rng_u32(rs);
+            const int rxs = (int)(((r1 % 2 == 0) ? 1u : 0xFFFFFFFFu) * r2 % (uint32_t)shift_range);
+            const uint32_t r3 = rng_u32(rs); const uint32_t r4 = rng_u32(rs);
+            const int rys = (int)(((r3 % 2 == 0) ? 1u : 0xFFFFFFFFu) * r4 % (uint32_t)shift_range);
+            rb[q][0] = rs.b0; rb[q][1] = rs.b1; rb[q][2] = rs.b2; rb[q][3] = rs.b3; rc[q] = rs.ctr; ri[q] = rs.idx;
+            float2 dir = make_float2(od.x * 20 + (float)rxs, od.y * 20 + (float)rys);
+            normalize2(dir);
+            const short2 np = make_short2((short)f2i((float)x + dir.x * radius), (short)f2i((float)y + dir.y * radius));
+            inm[q] = !(np.x < min_margin || np.y < min_margin || np.x >= W - min_margin || np.y >= H - min_margin);
+            const int npc = inm[q] ? np.x + np.y * W : center;
+            wkv[q] = B.weak[npc];
+            nnv[q] = B.nearest[npc];
+            cand[q] = np;
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            if (dir_found || !inm[q]) continue;
+            short2 np = cand[q];
+            if (wkv[q] != DPE_STRONG) {
+              np = nnv[q];
+              if (np.x == -1 || np.y == -1) continue;
+            }
+            float2 td = make_float2((float)(np.x - x), (float)(np.y - y));
+            normalize2(td);
+            const float ca = td.x * od.x + td.y * od.y;
+            if (ca > threshhold && (!edge_limit || !crosses(x, y, np.x, np.y))) {
+              push(np);
+              dir_found = true;
+              rs.b0 = rb[q][0]; rs.b1 = rb[q][1]; rs.b2 = rb[q][2]; rs.b3 = rb[q][3]; rs.ctr = rc[q]; rs.idx = ri[q];
+            }
+          }
+        }
+        float2 rd = make_float2(od.x * cos_angle - od.y * sin_angle, od.x * sin_angle + od.y * cos_angle);
+        normalize2(rd);
+        od = rd;
+      }
+    }
+  }
+  if (pc.P.use_label && B.label[center] > 0) {
+    const short2* lb = B.lab_bound + (size_t)center * 8;
+    for (int i = 0; i < 8; ++i) {
+      const short2 bp = lb[i];
+      float dist = 0.0f;
+      if (bp.x != -1 && bp.y != -1) {
+        const double dxx = (double)(x - bp.x), dyy = (double)(y - bp.y);
+        dist = (float)__builtin_sqrt(dxx * dxx + dyy * dyy);
+        if (i >= 4) dist = (float)((double)dist / 1.4142135623730951);
+      }
+      const int nstep = (i % 2 == 0) ? 2 * rotate_time - 1 : 1;   // dir_step (DPE.cu:2236-2247)
+      const int step_len = MAXo(1, d2i(__builtin_floor(1.0 * dist / (nstep + 1))));
+      for (int step = 1; step <= nstep; ++step) {
+        short2 np = make_short2((short)(x + step * step_len * kDir[i][0]), (short)(y + step * step_len * kDir[i][1]));
+        if (np.x < min_margin || np.y < min_margin || np.x >= W - min_margin || np.y >= H - min_margin) continue;
+        int npc = np.x + np.y * W;
+        if (B.weak[npc] != DPE_STRONG) {
+          np = B.nearest[npc];
+          if (np.x == -1 || np.y == -1) continue;
+          npc = np.x + np.y * W;
+        }
+        if (B.label[npc] != 0 && B.label[npc] != B.label[center]) continue;
+        push(np);
+      }
+    }
+  }
+  auto defer = [&]() { ovf[atomicAdd(novf, 1)] = center; };
+  auto finish_fail = [&]() {
+    if (complex_new >= 0.0f) B.complex_[center] = complex_new;
+    short2* nb = B.nb + (size_t)center * 9;
+    nb[0] = make_short2((short)x, (short)y);
+    for (int i = 1; i < 9; ++i) nb[i] = make_short2(-1, -1);
+    B.weak_rel[center] = 0;
+  };
+  if (overflow) { defer(); return; }
+  if (valid_count <= 3) { finish_fail(); return; }
+  // depths of the support points (the reference's spv3[].z); the 3-D points and normals of the
+  // drawn triples are recomputed from (pixel, depth) / planes0[] with the reference's expressions
+  for (int i = 0; i < valid_count; ++i) { const short2 sp = pt_at(i); s_dp[i][t] = B.planes0[sp.x + sp.y * W].w; }
+  float X[3];
+  get3d(camera, x, y, B.planes0[center].w, X);
+  const float cpz = X[2];
+  auto resid_of = [&](const float4& pl, int si) -> float {
+    const uint32_t v = s_pt[si][t];
+    const float fx = gtab[v & 0xFFFFu], fy = gtab[W + (v >> 16)];
+    const float fd = -pl.w / (pl.x * fx + pl.y * fy + pl.z);
+    return __builtin_fabsf(fd - s_dp[si][t]);
+  };
+  float4 best_plane = make_float4(0, 0, 0, 0);
+  bool has_valid_plane = false, nan_sort = false;
+  {
+    int iteration = 50, max_iter = pc.P.high_res_img ? 200 : 125, max_count = 3;
+    float min_cost = 3.40282347e+38f;
+    float temp_thr = ransac_threshold;
+    bool has_consist_normal_plane = false;
+    bool must_in_triangle = (pc.P.use_label && B.label[center] > 0 && edge_limit) ? false : true;
+    while (iteration > 0 && max_iter > 0) {
+      max_iter--;
+      const int a = (int)(rng_u32(rs) % (uint32_t)valid_count);
+      const int b = (int)(rng_u32(rs) % (uint32_t)valid_count);
+      const int c = (int)(rng_u32(rs) % (uint32_t)valid_count);
+      if (a == b || b == c || a == c) continue;
+      const short2 pa = pt_at(a), pb = pt_at(b), pcc = pt_at(c);
+      if (must_in_triangle && !point_in_triangle(pa, pb, pcc, x, y)) continue;
+      if (edge_limit) {
+        const bool eab = crosses(pa.x, pa.y, pb.x, pb.y);
+        const bool ebc = crosses(pb.x, pb.y, pcc.x, pcc.y);
+        const bool eca = crosses(pcc.x, pcc.y, pa.x, pa.y);
+        if (eab || ebc || eca) continue;
+      }
+      bool normal_consistency = false;
+      if (pc.P.geom_consistency && edge_limit) {
+        const float4 a4 = transform_normal_ref(camera, B.planes0[pa.x + pa.y * W]);
+        const float4 b4 = transform_normal_ref(camera, B.planes0[pb.x + pb.y * W]);
+        const float4 c4 = transform_normal_ref(camera, B.planes0[pcc.x + pcc.y * W]);
+        normal_consistency = true;
+        if ((double)(a4.x * b4.x + a4.y * b4.y + a4.z * b4.z) < 0.8660254 ||
+            (double)(a4.x * c4.x + a4.y * c4.y + a4.z * c4.z) < 0.8660254 ||
+            (double)(b4.x * c4.x + b4.y * c4.y + b4.z * c4.z) < 0.8660254)
+          normal_consistency = false;
+        if (has_consist_normal_plane && !normal_consistency) continue;
+      }
+      iteration--;
+      float A[3], Bq[3], C[3];
+      get3d(camera, pa.x, pa.y, s_dp[a][t], A);
+      get3d(camera, pb.x, pb.y, s_dp[b][t], Bq);
+      get3d(camera, pcc.x, pcc.y, s_dp[c][t], C);
+      const float ACx = A[0] - C[0], ACy = A[1] - C[1], ACz = A[2] - C[2];
+      const float BCx = Bq[0] - C[0], BCy = Bq[1] - C[1], BCz = Bq[2] - C[2];
+      float4 cv;
+      cv.x = ACy * BCz - BCy * ACz;
+      cv.y = -(ACx * BCz - BCx * ACz);
+      cv.z = ACx * BCy - BCx * ACy;
+      if ((cv.x == 0 && cv.y == 0 && cv.z == 0) || cv.x != cv.x || cv.y != cv.y || cv.z != cv.z) continue;
+      normalize3(cv);
+      cv.w = -(cv.x * A[0] + cv.y * A[1] + cv.z * A[2]);
+      int temp_count = 0;
+      for (int si = 0; si < valid_count; ++si)
+        if (resid_of(cv, si) < temp_thr) temp_count++;
+      if (temp_count < 6) continue;
+      if (temp_count > max_count) {
+        if (!must_in_triangle && point_in_triangle(pa, pb, pcc, x, y)) must_in_triangle = true;
+        if (!has_consist_normal_plane && normal_consistency) has_consist_normal_plane = true;
+        const float fx = ((float)x - camera.K[2]) / camera.K[0];
+        const float fy = ((float)y - camera.K[5]) / camera.K[4];
+        const float fd = -cv.w / (cv.x * fx + cv.y * fy + cv.z);
+        const float cd = __builtin_fabsf(fd - cpz);
+        best_plane = cv; max_count = temp_count; min_cost = cd; has_valid_plane = true;
+        if ((double)temp_thr > (pc.P.high_res_img ? 0.05 : 0.005)) {
+          // sort_small(residuals, valid_count) then residuals[DPE_NEIGHBOUR_NUM] (DPE.cu:5-14,
+          // 2367-2376): the 10th smallest residual (0 when there are at most 9: the untouched entry);
+          // the count that follows is the number of residuals below the new threshold, all of them
+          // among those 10 smallest
+          float top[DPE_NEIGHBOUR_NUM + 1];
+#pragma unroll
+          for (int k = 0; k <= DPE_NEIGHBOUR_NUM; ++k) top[k] = __builtin_inff();
+          bool has_nan = false;
+          for (int si = 0; si < valid_count; ++si) {
+            float r = resid_of(cv, si);
+            has_nan |= r != r;
+#pragma unroll
+            for (int k = 0; k <= DPE_NEIGHBOUR_NUM; ++k) {   // sorted insertion, static indices
+              const float lo = __builtin_fminf(top[k], r), hi = __builtin_fmaxf(top[k], r);
+              top[k] = lo; r = hi;
+            }
+          }
+          if (has_nan) { nan_sort = true; break; }
+          const float kth = valid_count > DPE_NEIGHBOUR_NUM ? top[DPE_NEIGHBOUR_NUM] : 0.0f;
+          if (temp_thr < kth) continue;
+          temp_thr = (float)((double)kth - 1e-6);
+          temp_count = 0;
+#pragma unroll
+          for (int k = 0; k <= DPE_NEIGHBOUR_NUM; ++k)
+            if (k < valid_count && top[k] < temp_thr) temp_count++;
+          max_count = temp_count;
+        }
+      } else if (temp_count == max_count) {
+        if (!must_in_triangle && point_in_triangle(pa, pb, pcc, x, y)) must_in_triangle = true;
+        const float fx = ((float)x - camera.K[2]) / camera.K[0];
+        const float fy = ((float)y - camera.K[5]) / camera.K[4];
+        const float fd = -cv.w / (cv.x * fx + cv.y * fy + cv.z);
+        const float cd = __builtin_fabsf(fd - cpz);
+        if (cd < min_cost) { best_plane = cv; max_count = temp_count; min_cost = cd; }
+      }
+    }
+  }
+  if (nan_sort) { defer(); return; }
+  if (!has_valid_plane) { finish_fail(); return; }
+  // weights (DPE.cu:2437-2449) in place of the depths, then sort_small_weighted (:16-29) and the
+  // first 8 points: the insertion sort is stable, so with no NaN weight the k-th output is the k-th
+  // smallest (weight, index) -- outliers carry FLT_MAX and the point (-1, -1)
+  bool wnan = false;
+  for (int i = 0; i < valid_count; ++i) {
+    const float dist = resid_of(best_plane, i);
+    wnan |= dist != dist;
+    s_dp[i][t] = dist >= ransac_threshold ? 3.40282347e+38f : dist;
+    if (dist >= ransac_threshold) s_pt[i][t] = 0xFFFFFFFFu;
+  }
+  if (wnan) { defer(); return; }
+  short2 out[DPE_NEIGHBOUR_NUM - 1];
+  uint32_t taken = 0;
+#pragma unroll
+  for (int k = 0; k < DPE_NEIGHBOUR_NUM - 1; ++k) {
+    int bi = -1; float bw = 0.0f;
+    for (int i = 0; i < valid_count; ++i) {
+      if ((taken >> i) & 1u) continue;
+      const float w = s_dp[i][t];
+      if (bi < 0 || w < bw) { bi = i; bw = w; }
+    }
+    if (bi >= 0) { taken |= 1u << bi; out[k] = pt_at(bi); }
+    else out[k] = make_short2(-1, -1);
+  }
+  if (complex_new >= 0.0f) B.complex_[center] = complex_new;
+  short2* nb = B.nb + (size_t)center * 9;
+  nb[0] = make_short2((short)x, (short)y);
+#pragma unroll
+  for (int k = 0; k < DPE_NEIGHBOUR_NUM - 1; ++k) nb[k + 1] = out[k];
+  B.weak_rel[center] = 1;
+}
+
 // ------------------------------------------------------------------------------ NeigbourUpdate
 __global__ void k_neighbour_update(const PassConst* __restrict__ pcp, DevBufs B) {   // DPE.cu:2465-2481
   const PassConst& pc = *pcp;
@@ -755,7 +1107,7 @@ __global__ void k_build_quad8(const float* __restrict__ img, uint32_t* __restric
   const size_t o = (size_t)Y * (W + 2) + X;
   q8[o] = (uint32_t)a | ((uint32_t)b << 8) | ((uint32_t)c << 16) | ((uint32_t)d << 24);
   const h2v lo = (h2v){(_Float16)a, (_Float16)c};
-  const h2v df = (h2v){(_Float16)((b - a) * 0.00390625f), (_Float16)((d - c) * 0.00390625f)};
+  const h2v df = (h2v){(_Float16)(b - a), (_Float16)(d - c)};
   q16[o] = make_uint2(__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, df));
 }
 // TEX_P16 column pairs (pass_common.h): (g(X-1, Y-1), g(X-1, Y)) as f16, X in [0, W+2], Y in [0, H+1]

@@ -85,7 +85,7 @@ DEV void taps36_at(const float* pw, int px, int py, f2v tmax, const uint8_t* bas
 #endif
     for (int a = 0; a < 6; ++a) {
       const float x = (float)(px - 5 + 2 * a);
-      const f2v bxy = fma2((f2v){H.h[0], H.h[3]}, f2s(x), (f2v){H.h[2], H.h[5]}) * f2s(256.0f);
+      const f2v bxy = fma2((f2v){H.h[0], H.h[3]}, f2s(x), (f2v){H.h[2], H.h[5]}) * f2s(kTexUnit);
       const float bz = __builtin_fmaf(H.h[6], x, H.h[8]);
       f2v r_sr = f2s(0.0f);
       float r_ss = 0;
@@ -118,8 +118,8 @@ DEV void lds_taps(const float* pw, int px, int py, const PassConst& pc, const De
 #pragma unroll
     for (int a = 0; a < 6; ++a) {
       const float x = (float)(px - 5 + 2 * a);
-      const float bx = __builtin_fmaf(H.h[0], x, H.h[2]) * 256.0f;
-      const float by = __builtin_fmaf(H.h[3], x, H.h[5]) * 256.0f;
+      const float bx = __builtin_fmaf(H.h[0], x, H.h[2]) * kTexUnit;
+      const float by = __builtin_fmaf(H.h[3], x, H.h[5]) * kTexUnit;
       const float bz = __builtin_fmaf(H.h[6], x, H.h[8]);
       float r_src = 0, r_ss = 0, r_rs = 0;
 #pragma unroll
@@ -154,7 +154,7 @@ DEV void lds_row(const float* pw, int px, int py, const PassConst& pc, const Dev
     const uint32_t stride = tex_stride<U8>(W), vadj = tex_vadj<U8>((uint32_t)v * tex_view<U8>(B), stride);
     const f2v tmax = tex_tmax2(W, Hh);
     const f2v* wp = (const f2v*)pw;
-    const f2v bxy = fma2((f2v){H.h[0], H.h[3]}, f2s(x), (f2v){H.h[2], H.h[5]}) * f2s(256.0f);
+    const f2v bxy = fma2((f2v){H.h[0], H.h[3]}, f2s(x), (f2v){H.h[2], H.h[5]}) * f2s(kTexUnit);
     const float bz = __builtin_fmaf(H.h[6], x, H.h[8]);
     f2v r_sr = f2s(0.0f);
     float r_ss = 0;
@@ -181,8 +181,8 @@ DEV void lds_row(const float* pw, int px, int py, const PassConst& pc, const Dev
 #endif
     r3[0] = r_sr.x; r3[1] = r_ss; r3[2] = r_sr.y;
   } else {
-    const float bx = __builtin_fmaf(H.h[0], x, H.h[2]) * 256.0f;
-    const float by = __builtin_fmaf(H.h[3], x, H.h[5]) * 256.0f;
+    const float bx = __builtin_fmaf(H.h[0], x, H.h[2]) * kTexUnit;
+    const float by = __builtin_fmaf(H.h[3], x, H.h[5]) * kTexUnit;
     const float bz = __builtin_fmaf(H.h[6], x, H.h[8]);
     float r_src = 0, r_ss = 0, r_rs = 0;
 #pragma unroll

@@ -710,7 +710,7 @@ DEV void tab_taps(const PassConst& pc, const DevBufs& B, int v, const Homog& H0,
 #pragma unroll
     for (int a = 0; a < (NN > 0 ? NN : n); ++a) {
       const float xf = (float)(cx - rad + a * inc);
-      const f2v bxy = fma2((f2v){H.h[0], H.h[3]}, f2s(xf), (f2v){H.h[2], H.h[5]}) * f2s(256.0f);
+      const f2v bxy = fma2((f2v){H.h[0], H.h[3]}, f2s(xf), (f2v){H.h[2], H.h[5]}) * f2s(kTexUnit);
       const float bz = __builtin_fmaf(H.h[6], xf, H.h[8]);
       f2v r_sr = f2s(0.0f);
       float r_ss = 0;
@@ -729,8 +729,8 @@ DEV void tab_taps(const PassConst& pc, const DevBufs& B, int v, const Homog& H0,
     float s_src = 0, s_ss = 0, s_rs = 0;
     for (int a = 0; a < n; ++a) {
       const float xf = (float)(cx - rad + a * inc);
-      const float bx = __builtin_fmaf(H.h[0], xf, H.h[2]) * 256.0f;
-      const float by = __builtin_fmaf(H.h[3], xf, H.h[5]) * 256.0f;
+      const float bx = __builtin_fmaf(H.h[0], xf, H.h[2]) * kTexUnit;
+      const float by = __builtin_fmaf(H.h[3], xf, H.h[5]) * kTexUnit;
       const float bz = __builtin_fmaf(H.h[6], xf, H.h[8]);
       float r_src = 0, r_ss = 0, r_rs = 0;
       for (int b = 0; b < n; ++b) {
@@ -770,7 +770,7 @@ DEV void tab_taps_masked(const PassConst& pc, const DevBufs& B, int v, const Hom
   for (int a = 0; a < NMAX; ++a) {
     if (a < n) {
       const float xf = (float)(cx - rad + a * inc);
-      const f2v bxy = fma2((f2v){H.h[0], H.h[3]}, f2s(xf), (f2v){H.h[2], H.h[5]}) * f2s(256.0f);
+      const f2v bxy = fma2((f2v){H.h[0], H.h[3]}, f2s(xf), (f2v){H.h[2], H.h[5]}) * f2s(kTexUnit);
       const float bz = __builtin_fmaf(H.h[6], xf, H.h[8]);
       f2v r_sr = f2s(0.0f);
       float r_ss = 0;
