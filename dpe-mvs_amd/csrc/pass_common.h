@@ -297,13 +297,13 @@ DEV float ref_texel(const float* ref, int W, int H, int x, int y) {
 // trunc(fma(q·iz, 256, 256.5)): a multiply, an FMA, a clamp and a half-rate conversion).  The clamp
 // is taken on t (monotone; NaN -> the low end), and the bound |256 s + 256| < 2^22 for unclamped taps
 // holds for images narrower than 16383 px (dpe_pm_stage checks).
-// DPE_TEX_FRACT=1 (round 4): the same U on the 1/256-unit grid of [2^15, 2^16) instead of the unit grid
+// DPE_TEX_FRACT=1 (round 3): the same U on the 1/256-unit grid of [2^15, 2^16) instead of the unit grid
 // of [2^23, 2^24): t' = fma(q, iz, 1.5·2^15 + 1) = t / 256 exactly (scaling by a power of two commutes
 // with the FMA's one rounding, and the row terms are no longer scaled), its encoding still differs
 // from that of 1.5·2^15 by U, and the tap's weight (U & 255) / 256 is v_fract_f32(t') straight from
 // the float (one full-rate op in place of v_cvt_f32_ubyte0 + a multiply per axis).
 #ifndef DPE_TEX_FRACT
-#define DPE_TEX_FRACT 0
+#define DPE_TEX_FRACT 1
 #endif
 #if DPE_TEX_FRACT
 constexpr float kTexMagic = 49152.0f;             // 1.5 * 2^15

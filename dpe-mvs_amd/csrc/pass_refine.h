@@ -94,11 +94,11 @@ DEV void taps36_at(const float* pw, int px, int py, f2v tmax, const uint8_t* bas
         const f2v sp = tap2_at<U8, IN>(base, vadj, stride, tmax, H.h, bxy, bz,
                                    (f2v){(float)(py - 5 + 2 * b), (float)(py - 3 + 2 * b)});
         const f2v w0 = wp[a * 6 + b], w1 = wp[a * 6 + b + 1];
-        const f2v ws = (f2v){w0.x, w1.x} * sp;
+        const float ws0 = w0.x * sp.x, ws1 = w1.x * sp.y;   // two plain multiplies: no operand packing
         r_sr = fma2(w0, f2s(sp.x), r_sr);
-        r_ss = __builtin_fmaf(ws.x, sp.x, r_ss);
+        r_ss = __builtin_fmaf(ws0, sp.x, r_ss);
         r_sr = fma2(w1, f2s(sp.y), r_sr);
-        r_ss = __builtin_fmaf(ws.y, sp.y, r_ss);
+        r_ss = __builtin_fmaf(ws1, sp.y, r_ss);
       }
       s_sr += r_sr; s_ss += r_ss;
     }
@@ -163,11 +163,11 @@ DEV void lds_row(const float* pw, int px, int py, const PassConst& pc, const Dev
     for (int b = 0; b < 6; b += 2) {
       const f2v sp = tap2_fast<U8>(B, vadj, stride, tmax, H.h, bxy, bz, (f2v){(float)(py - 5 + 2 * b), (float)(py - 3 + 2 * b)});
       const f2v w0 = wp[a * 6 + b], w1 = wp[a * 6 + b + 1];
-      const f2v ws = (f2v){w0.x, w1.x} * sp;
+      const float ws0 = w0.x * sp.x, ws1 = w1.x * sp.y;
       r_sr = fma2(w0, f2s(sp.x), r_sr);
-      r_ss = __builtin_fmaf(ws.x, sp.x, r_ss);
+      r_ss = __builtin_fmaf(ws0, sp.x, r_ss);
       r_sr = fma2(w1, f2s(sp.y), r_sr);
-      r_ss = __builtin_fmaf(ws.y, sp.y, r_ss);
+      r_ss = __builtin_fmaf(ws1, sp.y, r_ss);
     }
 #else
 #pragma unroll
@@ -210,6 +210,9 @@ DEV void lds_row(const float* pw, int px, int py, const PassConst& pc, const Dev
 // clamp-free tap loop in the strong sweep's pools and LocalRefine (A/B knobs)
 #ifndef DPE_STRONG_ELIDE
 #define DPE_STRONG_ELIDE false
+#endif
+#ifndef DPE_D2W_ELIDE
+#define DPE_D2W_ELIDE true
 #endif
 #ifndef DPE_LR_ELIDE
 #define DPE_LR_ELIDE false
@@ -305,8 +308,11 @@ DEV uint8_t d2w_class(const PassConst& pc, const float* pcs, uint64_t is_peak) {
 #ifndef DPE_BW_LR
 #define DPE_BW_LR 4
 #endif
+#ifndef DPE_D2W_WAVES
+#define DPE_D2W_WAVES DPE_TAP_WAVES
+#endif
 template <int U8>
-__global__ void __launch_bounds__(64 * DPE_BW_D2W, DPE_TAP_WAVES) k_depth_to_weak(const PassConst* __restrict__ pcp, DevBufs B) {   // DPE.cu:2593-2747
+__global__ void __launch_bounds__(64 * DPE_BW_D2W, DPE_D2W_WAVES) k_depth_to_weak(const PassConst* __restrict__ pcp, DevBufs B) {   // DPE.cu:2593-2747
   __shared__ float s_patch[DPE_BW_D2W][108];
   __shared__ float s_pc[DPE_BW_D2W][64];
   const PassConst& pc = *pcp;
@@ -355,7 +361,7 @@ __global__ void __launch_bounds__(64 * DPE_BW_D2W, DPE_TAP_WAVES) k_depth_to_wea
         const int vi = si - 1;
         if (isSet(sel, vi)) {
           float tcst = 0.0f;
-          tcst += ncc_old_any<U8, true>(fast, pw, s_ref, s_rr, s_w, x, y, pc, B, si, tp);
+          tcst += ncc_old_any<U8, DPE_D2W_ELIDE>(fast, pw, s_ref, s_rr, s_w, x, y, pc, B, si, tp);
           PHASE(1);
           if (pc.P.geom_consistency) tcst += pc.P.geom_factor * geom_cost_at(pc, B, x, y, si, fw);
           PHASE(2);
@@ -400,6 +406,7 @@ __global__ void __launch_bounds__(64 * DPE_BW_LR, DPE_TAP_WAVES) k_local_refine_
   __shared__ float3 s_fw[BW][kLrPix][12];         // geometric-consistency world point of each hypothesis
   __shared__ uint8_t s_sel[BW][kLrPix][DPE_MAX_IMAGES];
   __shared__ int s_cnt[BW][kLrPix][2];          // [0] selected views, [1] hypothesis mask (bit 11 = current)
+  __shared__ int s_xy[BW][kLrPix];              // pixel x | y << 16 (read by the job pool)
   const PassConst& pc = *pcp;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int W = pc.W;
@@ -449,6 +456,7 @@ __global__ void __launch_bounds__(64 * DPE_BW_LR, DPE_TAP_WAVES) k_local_refine_
   }
   if (gl == 0) {
     int ns = 0;
+    s_xy[wave][gp] = (int)((uint32_t)x | ((uint32_t)y << 16));
     if (go) for (uint32_t bits = sel & vmask; bits; bits &= bits - 1) s_sel[wave][gp][ns++] = (uint8_t)__builtin_ctz(bits);
     s_cnt[wave][gp][0] = ns;
     if (!go) s_cnt[wave][gp][1] = 0;
@@ -479,8 +487,8 @@ __global__ void __launch_bounds__(64 * DPE_BW_LR, DPE_TAP_WAVES) k_local_refine_
     for (int q = r / ns; q > 0; --q) m &= m - 1;     // the (r / ns)-th valid hypothesis
     const int h = __builtin_ctz(m), k = r % ns;
 #endif
-    const long px = base + p;
-    const int jx = (int)(px % W), jy = (int)(px / W);
+    const uint32_t jxy = (uint32_t)s_xy[wave][p];
+    const int jx = (int)(jxy & 0xFFFFu), jy = (int)(jxy >> 16);
     const int si = s_sel[wave][p][k] + 1;
     const float4 tp = s_hyp[wave][p][h];
     const float* sm = s_sum[wave][p];
