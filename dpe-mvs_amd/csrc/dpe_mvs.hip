@@ -201,7 +201,7 @@ void dpe_params_default(DpePatchMatchParams* p) {   // main.h:78-106
 const char* dpe_last_error(void) { return g_err.c_str(); }
 
 #ifndef DPE_GN_LDS
-#define DPE_GN_LDS 0   // scratch-free GenNeighbours (pass_kernels.h k_gen_neighbours_lds)
+#define DPE_GN_LDS 1   // scratch-free GenNeighbours (pass_kernels.h k_gen_neighbours_lds)
 #endif
 #ifndef DPE_EARLY_FORK
 #define DPE_EARLY_FORK 1

@@ -470,18 +470,26 @@ __global__ void __launch_bounds__(256, DPE_GN_WAVES) k_gen_neighbours(const Pass
 // The same GenNeighbours with no per-thread arrays (k_gen_neighbours keeps 2.3 KB/lane of them in
 // scratch, re-read from HBM on every RANSAC try).  The support points are appended in probe order,
 // which is the order of the reference's compaction of strong_points[] (dir_index grows through the
-// probe loops, the label extension follows at 32+), so they go straight into an LDS column per
-// thread: packed pixel and depth, kGnK slots ([slot][thread], conflict-free).  The normalised image
-// coordinates of a point come from per-column / per-row tables (`gtab`: the same expression per
-// coordinate), the edge tests are recomputed instead of cached (BresenhamLine is a pure function of
-// its end points; the reference's edge_test[][] only saves work), and the two sorts become
-// order-statistic selections whose results equal the insertion sorts' whenever no residual or
-// weight is NaN.  A pixel with more than kGnK support points, or a NaN where a sort needs the order,
-// writes nothing and is appended to `ovf` for k_gen_neighbours (its Philox stream is addressed by
-// the pixel, so the rerun draws the same numbers).
+// probe loops, the label extension follows at 32+; rotate_time <= 4), so they go straight into an
+// LDS column per thread: the packed pixel, kGnK slots ([slot][thread], conflict-free, 8 KB per
+// 64-thread workgroup).  A point's depth is re-read from planes0[] and its normalised image
+// coordinates come from per-column / per-row tables (`gtab`, the same expression per coordinate), so
+// nothing else is stored.  The edge tests are recomputed instead of cached (BresenhamLine is a pure
+// function of its end points; the reference's edge_test[][] only saves work), the probe batches
+// re-position the Philox stream by its word index instead of saving its state, and the two sorts
+// become order-statistic selections whose results equal the insertion sorts' whenever no residual
+// or weight is NaN.  A pixel with more than kGnK support points, or a NaN where a sort needs the
+// order, writes nothing and is appended to `ovf` for k_gen_neighbours (its Philox stream is
+// addressed by the pixel, so the rerun draws the same numbers).  96 VGPRs, 5 waves per SIMD.
 constexpr int kGnK = 32;
 #ifndef DPE_GN_BT
 #define DPE_GN_BT 64
+#endif
+#ifndef DPE_GN_DP
+#define DPE_GN_DP 0      // 1: support-point depths in LDS too (0: re-read from planes0, half the LDS)
+#endif
+#ifndef DPE_GN_SHORT
+#define DPE_GN_SHORT 0   // 1: one-round-trip Bresenham walks for max_step <= 16 (more registers, slower)
 #endif
 // table of the normalised image coordinates: gtab[x] = (x - K[2]) / K[0], gtab[W + y] = (y - K[5]) / K[4]
 __global__ void k_gn_tables(const PassConst* __restrict__ pcp, float* __restrict__ gtab) {
@@ -534,12 +542,17 @@ DEV bool bresenham_short(const PassConst& pc, const DevBufs& B, int Ax, int Ay, 
   return !(ea || eb) && hit != 0;
 }
 
-__global__ void __launch_bounds__(DPE_GN_BT) k_gen_neighbours_lds(const PassConst* __restrict__ pcp, DevBufs B,
+#ifndef DPE_GN_MINW
+#define DPE_GN_MINW 1
+#endif
+__global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(const PassConst* __restrict__ pcp, DevBufs B,
                                                                   const int* __restrict__ list, const int* __restrict__ nlist_p,
                                                                   const float* __restrict__ gtab, int* __restrict__ ovf,
                                                                   int* __restrict__ novf) {   // DPE.cu:2103-2463
   __shared__ uint32_t s_pt[kGnK][DPE_GN_BT];    // support point (x | y << 16)
+#if DPE_GN_DP
   __shared__ float s_dp[kGnK][DPE_GN_BT];       // its depth, then (after the RANSAC) its weight
+#endif
   const PassConst& pc = *pcp;
   const int t = threadIdx.x;
   const int gi = xcd_remap(blockIdx.x, gridDim.x, B.xcd_rows * 64) * DPE_GN_BT + t;
@@ -568,7 +581,7 @@ __global__ void __launch_bounds__(DPE_GN_BT) k_gen_neighbours_lds(const PassCons
   const float ransac_threshold = pc.P.ransac_threshold * depth_diff;
   const int max_step = pc.P.high_res_img ? (int)__builtin_round(MAXo(pc.LH, pc.LW) / 60.0) : MAXo(pc.LH, pc.LW);
   auto crosses = [&](int ax, int ay, int bx, int by) -> bool {
-    return max_step <= 16 ? bresenham_short(pc, B, ax, ay, bx, by, max_step) : bresenham(pc, B, ax, ay, bx, by);
+    return (DPE_GN_SHORT && max_step <= 16) ? bresenham_short(pc, B, ax, ay, bx, by, max_step) : bresenham(pc, B, ax, ay, bx, by);
   };
   bool edge_limit = false;
   float complex_new = -1.0f;                       // complex_[center] to write once the pixel is done
@@ -592,19 +605,18 @@ __global__ void __launch_bounds__(DPE_GN_BT) k_gen_neighbours_lds(const PassCons
           const float tpx = (float)x + od.x * radius, tpy = (float)y + od.y * radius;
           if (tpx < 0 || tpy < 0 || tpx >= W || tpy >= H) break;
           // 4 attempts at a time: draws, targets and weak[] / nearest[] loads issued first, then tested
-          // in order; the stream is put back to just after the attempt that succeeded
+          // in order; the stream is then positioned just after the attempt that succeeded (each
+          // attempt draws 4 words, and the stream is position-addressable)
           short2 cand[4], nnv[4];
           uint8_t wkv[4];
           bool inm[4];
-          uint32_t rb[4][4], rc[4];
-          int ri[4];
+          const uint32_t pos0 = rs.idx == 4 ? rs.ctr * 4u : (rs.ctr - 1u) * 4u + (uint32_t)rs.idx;
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const uint32_t r1 = rng_u32(rs); const uint32_t r2 = rng_u32(rs);
             const int rxs = (int)(((r1 % 2 == 0) ? 1u : 0xFFFFFFFFu) * r2 % (uint32_t)shift_range);
             const uint32_t r3 = rng_u32(rs); const uint32_t r4 = rng_u32(rs);
             const int rys = (int)(((r3 % 2 == 0) ? 1u : 0xFFFFFFFFu) * r4 % (uint32_t)shift_range);
-            rb[q][0] = rs.b0; rb[q][1] = rs.b1; rb[q][2] = rs.b2; rb[q][3] = rs.b3; rc[q] = rs.ctr; ri[q] = rs.idx;
             float2 dir = make_float2(od.x * 20 + (float)rxs, od.y * 20 + (float)rys);
             normalize2(dir);
             const short2 np = make_short2((short)f2i((float)x + dir.x * radius), (short)f2i((float)y + dir.y * radius));
@@ -628,7 +640,7 @@ __global__ void __launch_bounds__(DPE_GN_BT) k_gen_neighbours_lds(const PassCons
             if (ca > threshhold && (!edge_limit || !crosses(x, y, np.x, np.y))) {
               push(np);
               dir_found = true;
-              rs.b0 = rb[q][0]; rs.b1 = rb[q][1]; rs.b2 = rb[q][2]; rs.b3 = rb[q][3]; rs.ctr = rc[q]; rs.idx = ri[q];
+              rng_seek(rs, pos0 + 4u * (uint32_t)(q + 1));
             }
           }
         }
@@ -676,7 +688,12 @@ __global__ void __launch_bounds__(DPE_GN_BT) k_gen_neighbours_lds(const PassCons
   if (valid_count <= 3) { finish_fail(); return; }
   // depths of the support points (the reference's spv3[].z); the 3-D points and normals of the
   // drawn triples are recomputed from (pixel, depth) / planes0[] with the reference's expressions
+#if DPE_GN_DP
   for (int i = 0; i < valid_count; ++i) { const short2 sp = pt_at(i); s_dp[i][t] = B.planes0[sp.x + sp.y * W].w; }
+  auto depth_at = [&](int i) -> float { return s_dp[i][t]; };
+#else
+  auto depth_at = [&](int i) -> float { const uint32_t v = s_pt[i][t]; return B.planes0[(v & 0xFFFFu) + (v >> 16) * W].w; };
+#endif
   float X[3];
   get3d(camera, x, y, B.planes0[center].w, X);
   const float cpz = X[2];
@@ -684,7 +701,7 @@ __global__ void __launch_bounds__(DPE_GN_BT) k_gen_neighbours_lds(const PassCons
     const uint32_t v = s_pt[si][t];
     const float fx = gtab[v & 0xFFFFu], fy = gtab[W + (v >> 16)];
     const float fd = -pl.w / (pl.x * fx + pl.y * fy + pl.z);
-    return __builtin_fabsf(fd - s_dp[si][t]);
+    return __builtin_fabsf(fd - depth_at(si));
   };
   float4 best_plane = make_float4(0, 0, 0, 0);
   bool has_valid_plane = false, nan_sort = false;
@@ -722,9 +739,9 @@ __global__ void __launch_bounds__(DPE_GN_BT) k_gen_neighbours_lds(const PassCons
       }
       iteration--;
       float A[3], Bq[3], C[3];
-      get3d(camera, pa.x, pa.y, s_dp[a][t], A);
-      get3d(camera, pb.x, pb.y, s_dp[b][t], Bq);
-      get3d(camera, pcc.x, pcc.y, s_dp[c][t], C);
+      get3d(camera, pa.x, pa.y, depth_at(a), A);
+      get3d(camera, pb.x, pb.y, depth_at(b), Bq);
+      get3d(camera, pcc.x, pcc.y, depth_at(c), C);
       const float ACx = A[0] - C[0], ACy = A[1] - C[1], ACz = A[2] - C[2];
       const float BCx = Bq[0] - C[0], BCy = Bq[1] - C[1], BCz = Bq[2] - C[2];
       float4 cv;
@@ -790,12 +807,21 @@ __global__ void __launch_bounds__(DPE_GN_BT) k_gen_neighbours_lds(const PassCons
   // first 8 points: the insertion sort is stable, so with no NaN weight the k-th output is the k-th
   // smallest (weight, index) -- outliers carry FLT_MAX and the point (-1, -1)
   bool wnan = false;
+#if DPE_GN_DP
   for (int i = 0; i < valid_count; ++i) {
     const float dist = resid_of(best_plane, i);
     wnan |= dist != dist;
     s_dp[i][t] = dist >= ransac_threshold ? 3.40282347e+38f : dist;
     if (dist >= ransac_threshold) s_pt[i][t] = 0xFFFFFFFFu;
   }
+  auto weight_at = [&](int i) -> float { return s_dp[i][t]; };
+#else
+  for (int i = 0; i < valid_count; ++i) { const float dist = resid_of(best_plane, i); wnan |= dist != dist; }
+  auto weight_at = [&](int i) -> float {
+    const float dist = resid_of(best_plane, i);
+    return dist >= ransac_threshold ? 3.40282347e+38f : dist;
+  };
+#endif
   if (wnan) { defer(); return; }
   short2 out[DPE_NEIGHBOUR_NUM - 1];
   uint32_t taken = 0;
@@ -804,10 +830,14 @@ __global__ void __launch_bounds__(DPE_GN_BT) k_gen_neighbours_lds(const PassCons
     int bi = -1; float bw = 0.0f;
     for (int i = 0; i < valid_count; ++i) {
       if ((taken >> i) & 1u) continue;
-      const float w = s_dp[i][t];
+      const float w = weight_at(i);
       if (bi < 0 || w < bw) { bi = i; bw = w; }
     }
+#if DPE_GN_DP
     if (bi >= 0) { taken |= 1u << bi; out[k] = pt_at(bi); }
+#else
+    if (bi >= 0) { taken |= 1u << bi; out[k] = bw >= ransac_threshold ? make_short2(-1, -1) : pt_at(bi); }
+#endif
     else out[k] = make_short2(-1, -1);
   }
   if (complex_new >= 0.0f) B.complex_[center] = complex_new;

@@ -231,6 +231,15 @@ DEV float ncc_old_lds(const float* pw, float s_ref, float s_rr, float s_w, int p
     bool in = false;
     if constexpr (ELIDE) {
       in = patch_inside(H, (float)(px - 5), (float)(px + 5), (float)(py - 5), (float)(py + 5), pc.W, pc.H);
+#if DPE_LINE_STATS   // row 0 of the statistics: [wave calls all inside, wave calls, lanes inside, lanes]
+      {
+        const uint64_t bi = __ballot(in), ba = __ballot(1);
+        if ((int)(threadIdx.x & 63) == __builtin_ctzll(ba)) {
+          atomicAdd(&g_lstat[0][0], bi == ba ? 1ull : 0ull); atomicAdd(&g_lstat[0][1], 1ull);
+          atomicAdd(&g_lstat[0][2], (unsigned long long)__popcll(bi)); atomicAdd(&g_lstat[0][3], (unsigned long long)__popcll(ba));
+        }
+      }
+#endif
 #if DPE_ELIDE_UNIFORM
       in = __all(in);
 #endif

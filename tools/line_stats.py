@@ -32,6 +32,9 @@ assert lib.dpe_pm_fetch(ctx, C.byref(bufs.st)) == 0, lib.dpe_last_error()
 tot = [0] * 16
 for fn in ("dpe_dbg_line_stats_main", "dpe_dbg_line_stats_tap"):
     getattr(lib, fn)(buf, 1)
+    if buf[1]:   # row 0: the clamp-free choice of ELIDE builds, per translation unit
+        print(f"{fn}: clamp-free choice: wave calls {buf[1]:.3e}, all lanes inside {buf[0] / buf[1]:.3f}, "
+              f"lanes inside {buf[2] / max(buf[3], 1):.3f}", flush=True)
     for k in range(16):
         tot[k] += buf[k]
 for t, name in ((1, "U8 (weak sweep)"), (2, "F16 (DepthToWeak, LocalRefine, init)"), (3, "P16 (strong sweep)")):
