@@ -542,6 +542,9 @@ DEV bool bresenham_short(const PassConst& pc, const DevBufs& B, int Ax, int Ay, 
   return !(ea || eb) && hit != 0;
 }
 
+#ifndef DPE_GNL_SPEC
+#define DPE_GNL_SPEC 4   // probe attempts drawn and loaded together (1, 2 or 4)
+#endif
 #ifndef DPE_GN_MINW
 #define DPE_GN_MINW 1
 #endif
@@ -564,6 +567,7 @@ __global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(c
   const float depth_diff = pc.P.depth_max - pc.P.depth_min;
   const DpeCamera& camera = pc.cams[0];
   Rng rs; rng_init(rs, (uint32_t)center, pc.seed32, STREAM_GEN_NEIGHBOURS, pc.salt);
+  PHASE_BEGIN();
   int valid_count = 0;
   bool overflow = false;
   auto push = [&](short2 np) {
@@ -594,25 +598,37 @@ __global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(c
       else complex_new = MAXo(0.99f, cv);
     }
   }
-  for (int odx = -1; odx <= 1; ++odx) {
-    for (int ody = -1; ody <= 1; ++ody) {
-      if (odx == 0 && ody == 0) continue;
-      float2 od = make_float2((float)odx, (float)ody);
+  // The 8 x rotate_time direction walks as ONE loop per lane: a lane that ends a walk (support point
+  // found, radius past the image or 4096) moves on to its next direction at once, so a wave's time
+  // is its slowest lane's total walk, not the sum over directions of each direction's slowest walk.
+  // Each lane's sequence of probes (and of Philox draws) is the nested loops' sequence.  One radius
+  // of a walk is DPE_GNL_SPEC attempts at a time: their draws, targets and weak[] / nearest[] loads
+  // issued first, then tested in order; the stream is then positioned just after the attempt that
+  // succeeded (each attempt draws 4 words; the stream is position-addressable).
+  {
+    auto origin_od = [](int oi) -> float2 {   // odx -1..1 outer, ody -1..1 inner, (0, 0) skipped
+      const int k = oi < 4 ? oi : oi + 1;
+      float2 od = make_float2((float)(k / 3 - 1), (float)(k % 3 - 1));
       normalize2(od);
-      for (int rotate_iter = 0; rotate_iter < rotate_time; ++rotate_iter) {
+      return od;
+    };
+    int oi = 0, ri = 0, radius = 2;
+    float2 od = origin_od(0);
+    while (oi < 8) {
+      bool next = radius > 4096;
+      if (!next) {
+        const float tpx = (float)x + od.x * radius, tpy = (float)y + od.y * radius;
+        if (tpx < 0 || tpy < 0 || tpx >= W || tpy >= H) next = true;
+      }
+      if (!next) {
         bool dir_found = false;
-        for (int radius = 2; radius <= 4096 && !dir_found; radius = MINo(radius * 2, radius + 25)) {
-          const float tpx = (float)x + od.x * radius, tpy = (float)y + od.y * radius;
-          if (tpx < 0 || tpy < 0 || tpx >= W || tpy >= H) break;
-          // 4 attempts at a time: draws, targets and weak[] / nearest[] loads issued first, then tested
-          // in order; the stream is then positioned just after the attempt that succeeded (each
-          // attempt draws 4 words, and the stream is position-addressable)
-          short2 cand[4], nnv[4];
-          uint8_t wkv[4];
-          bool inm[4];
+        for (int ra = 0; ra < 4 && !dir_found; ra += DPE_GNL_SPEC) {
+          short2 cand[DPE_GNL_SPEC], nnv[DPE_GNL_SPEC];
+          uint8_t wkv[DPE_GNL_SPEC];
+          bool inm[DPE_GNL_SPEC];
           const uint32_t pos0 = rs.idx == 4 ? rs.ctr * 4u : (rs.ctr - 1u) * 4u + (uint32_t)rs.idx;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
+          for (int q = 0; q < DPE_GNL_SPEC; ++q) {
             const uint32_t r1 = rng_u32(rs); const uint32_t r2 = rng_u32(rs);
             const int rxs = (int)(((r1 % 2 == 0) ? 1u : 0xFFFFFFFFu) * r2 % (uint32_t)shift_range);
             const uint32_t r3 = rng_u32(rs); const uint32_t r4 = rng_u32(rs);
@@ -627,7 +643,7 @@ __global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(c
             cand[q] = np;
           }
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
+          for (int q = 0; q < DPE_GNL_SPEC; ++q) {
             if (dir_found || !inm[q]) continue;
             short2 np = cand[q];
             if (wkv[q] != DPE_STRONG) {
@@ -644,12 +660,23 @@ __global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(c
             }
           }
         }
-        float2 rd = make_float2(od.x * cos_angle - od.y * sin_angle, od.x * sin_angle + od.y * cos_angle);
-        normalize2(rd);
-        od = rd;
+        if (dir_found) next = true;
+        else radius = MINo(radius * 2, radius + 25);
+      }
+      if (next) {
+        radius = 2;
+        if (++ri < rotate_time) {
+          float2 rd = make_float2(od.x * cos_angle - od.y * sin_angle, od.x * sin_angle + od.y * cos_angle);
+          normalize2(rd);
+          od = rd;
+        } else {
+          ri = 0;
+          if (++oi < 8) od = origin_od(oi);
+        }
       }
     }
   }
+  PHASE(0);
   if (pc.P.use_label && B.label[center] > 0) {
     const short2* lb = B.lab_bound + (size_t)center * 8;
     for (int i = 0; i < 8; ++i) {
@@ -676,13 +703,15 @@ __global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(c
       }
     }
   }
-  auto defer = [&]() { ovf[atomicAdd(novf, 1)] = center; };
+  PHASE(1);
+  auto defer = [&]() { ovf[atomicAdd(novf, 1)] = center; PHASE_END_ALL(2); };
   auto finish_fail = [&]() {
     if (complex_new >= 0.0f) B.complex_[center] = complex_new;
     short2* nb = B.nb + (size_t)center * 9;
     nb[0] = make_short2((short)x, (short)y);
     for (int i = 1; i < 9; ++i) nb[i] = make_short2(-1, -1);
     B.weak_rel[center] = 0;
+    PHASE_END_ALL(2);
   };
   if (overflow) { defer(); return; }
   if (valid_count <= 3) { finish_fail(); return; }
@@ -703,6 +732,7 @@ __global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(c
     const float fd = -pl.w / (pl.x * fx + pl.y * fy + pl.z);
     return __builtin_fabsf(fd - depth_at(si));
   };
+  PHASE(2);
   float4 best_plane = make_float4(0, 0, 0, 0);
   bool has_valid_plane = false, nan_sort = false;
   {
@@ -801,6 +831,7 @@ __global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(c
       }
     }
   }
+  PHASE(3);
   if (nan_sort) { defer(); return; }
   if (!has_valid_plane) { finish_fail(); return; }
   // weights (DPE.cu:2437-2449) in place of the depths, then sort_small_weighted (:16-29) and the
@@ -846,6 +877,8 @@ __global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(c
 #pragma unroll
   for (int k = 0; k < DPE_NEIGHBOUR_NUM - 1; ++k) nb[k + 1] = out[k];
   B.weak_rel[center] = 1;
+  PHASE(4);
+  PHASE_END_ALL(2);
 }
 
 // ------------------------------------------------------------------------------ NeigbourUpdate
