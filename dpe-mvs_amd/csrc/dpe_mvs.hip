@@ -116,7 +116,7 @@ struct DpeContext {
   uint64_t icache_clock = 0;
   hipStream_t stream = nullptr;
   hipStream_t aux = nullptr;         // GenNeighbours beside the first strong half-sweep
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_ei = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_ei = nullptr, ev_gn0 = nullptr;
   hipEvent_t ev_done = nullptr;      // end of the last dpe_pm_execute's work on its stream
   bool pending = false;              // ev_done recorded and not yet waited for
   bool staged = false;
@@ -203,6 +203,9 @@ const char* dpe_last_error(void) { return g_err.c_str(); }
 #ifndef DPE_GN_LDS
 #define DPE_GN_LDS 1   // scratch-free GenNeighbours (pass_kernels.h k_gen_neighbours_lds)
 #endif
+#ifndef DPE_GN_SPLIT
+#define DPE_GN_SPLIT 0   // 1: GenNeighbours of the colour-0 grid pixels first (early fork only; measured slower)
+#endif
 #ifndef DPE_EARLY_FORK
 #define DPE_EARLY_FORK 1
 #endif
@@ -225,6 +228,7 @@ DpeContext* dpe_create(int device) {
   if (hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_gn0, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_ei, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming) != hipSuccess ||
       hipEventCreate(&c->ev_start) != hipSuccess) {
@@ -232,6 +236,7 @@ DpeContext* dpe_create(int device) {
     if (c->ev_start) (void)hipEventDestroy(c->ev_start);
     if (c->ev_done) (void)hipEventDestroy(c->ev_done);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+    if (c->ev_gn0) (void)hipEventDestroy(c->ev_gn0);
     if (c->ev_ei) (void)hipEventDestroy(c->ev_ei);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->aux) (void)hipStreamDestroy(c->aux);
@@ -296,6 +301,7 @@ void dpe_destroy(DpeContext* c) {
   c->lists.release(); c->row_counts.release(); c->list_totals.release();
   (void)hipStreamSynchronize(c->aux);
   (void)hipEventDestroy(c->ev_fork); (void)hipEventDestroy(c->ev_join); (void)hipEventDestroy(c->ev_ei);
+  (void)hipEventDestroy(c->ev_gn0);
   (void)hipStreamDestroy(c->aux);
   (void)hipStreamDestroy(c->stream);
   delete c;
@@ -629,7 +635,7 @@ static int stage_impl(DpeContext* c, const DpePassInput* in, const StageSrc& src
   HIPC(c->radius.ensure(L));
   HIPC(c->tab_right.ensure(L)); HIPC(c->tab_down.ensure(L));
   HIPC(c->gn_ovf.ensure(L + 64)); HIPC(c->gn_tab.ensure((size_t)W + H));
-  HIPC(c->lists.ensure(5 * (L / 2 + 64) + L + 64)); HIPC(c->row_counts.ensure(4 * (size_t)H + 4)); HIPC(c->list_totals.ensure(8));
+  HIPC(c->lists.ensure(6 * (L / 2 + 64) + 3 * (L + 64))); HIPC(c->row_counts.ensure(4 * (size_t)H + 4)); HIPC(c->list_totals.ensure(16));
   B.planes = c->planes.p; B.planes_snap = c->planes_snap.p; B.fit_plane = c->fit_plane.p;
   B.planes0 = c->planes0.p;
   B.costs = c->costs.p; B.costs_snap = c->costs_snap.p; B.complex_ = c->complex_.p;
@@ -744,12 +750,26 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   k_strong_tables_rows<<<(H + 63) / 64, 64, 0, se>>>(dpc, Bc, c->tab_right.p);
   k_strong_tables_cols<<<(W + 63) / 64, 64, 0, se>>>(dpc, Bc, c->tab_down.p);
   k_find_nearest_strong<<<fg, fb, 0, se>>>(dpc, Bc, c->tab_right.p, c->tab_down.p);
-  // list of all WEAK pixels (list slot 4), then GenNeighbours one thread per WEAK pixel
+  // list of all WEAK pixels (list slot 4), then GenNeighbours one thread per WEAK pixel.  With
+  // DPE_GN_SPLIT (early fork) the WEAK pixels come as two lists instead (MODE 3: colour 0 of the
+  // sweep grid, slot 9; the rest, slot 10), GenNeighbours runs over the first, the colour-0 failed
+  // list is built (slot 5) and signalled (ev_gn0), then GenNeighbours over the second, NeigbourUpdate
+  // and the colour-1 failed list (slot 8).  list_totals: 0..3 sweep lists, 4 WEAK, 5 / 8 failed
+  // colour 0 / 1, 6 GenNeighbours overflow, 9 / 10 split WEAK lists.
+  const bool split = early && DPE_GN_SPLIT;
   int* weak_list = c->lists.p + 4 * list_stride;
   int* failed_list = weak_list + L + 64;             // MODE 2 list (slot 5 of list_totals)
-  k_list_count<1><<<(H + 3) / 4, 256, 0, se>>>(dpc, Bc, c->row_counts.p + 2 * (size_t)H + 2);
-  k_list_scan<1><<<1, 64, 0, se>>>(dpc, c->row_counts.p + 2 * (size_t)H + 2, c->list_totals.p + 4);
-  k_list_fill<1><<<(H + 3) / 4, 256, 0, se>>>(dpc, Bc, c->row_counts.p + 2 * (size_t)H + 2, weak_list, (long)L);
+  int* split_lists = failed_list + list_stride;      // MODE 3 lists, stride L + 64
+  int* failed_list1 = split_lists + 2 * (L + 64);    // MODE 4 list (slot 8)
+  if (split) {
+    k_list_count<3><<<(H + 3) / 4, 256, 0, se>>>(dpc, Bc, c->row_counts.p + 2 * (size_t)H + 2);
+    k_list_scan<3><<<1, 128, 0, se>>>(dpc, c->row_counts.p + 2 * (size_t)H + 2, c->list_totals.p + 9);
+    k_list_fill<3><<<(H + 3) / 4, 256, 0, se>>>(dpc, Bc, c->row_counts.p + 2 * (size_t)H + 2, split_lists, (long)L + 64);
+  } else {
+    k_list_count<1><<<(H + 3) / 4, 256, 0, se>>>(dpc, Bc, c->row_counts.p + 2 * (size_t)H + 2);
+    k_list_scan<1><<<1, 64, 0, se>>>(dpc, c->row_counts.p + 2 * (size_t)H + 2, c->list_totals.p + 4);
+    k_list_fill<1><<<(H + 3) / 4, 256, 0, se>>>(dpc, Bc, c->row_counts.p + 2 * (size_t)H + 2, weak_list, (long)L);
+  }
   // GenNeighbours + NeigbourUpdate only decide which WEAK pixels join the strong lists; nothing the
   // first strong half-sweep (iteration 0, colour 0) or RandomInitialization reads is written by
   // them, and GenNeighbours reads the staged planes, not the ones those two rewrite.  So they run
@@ -769,21 +789,43 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   // forked after RandomInitialization: launched beside it, GenNeighbours' ~4.7 K long waves (all
   // resident at once) starved it of registers (0.86 -> 8.5 ms in a kernel trace of the overlapped pass)
   const DevBufs Bgn = Bc;
+  // GenNeighbours over one list: the scratch-free kernel plus the scratch kernel for its overflow
+  // pixels, or the scratch kernel alone (rotate_time > 4)
+  bool gn_tables = false;
+  auto gn_over = [&](const int* lst, const int* cnt) -> int {
+#if DPE_GN_LDS
+    if (pc.P.rotate_time <= 4) {   // probe slots in the reference's compaction order (dir_index < 32)
+      if (!gn_tables) { k_gn_tables<<<(unsigned)((W + H + 255) / 256), 256, 0, a>>>(dpc, c->gn_tab.p); gn_tables = true; }
+      HIPC(hipMemsetAsync(c->list_totals.p + 6, 0, sizeof(int), a));
+      k_gen_neighbours_lds<<<(unsigned)((L + DPE_GN_BT - 1) / DPE_GN_BT), DPE_GN_BT, 0, a>>>(
+          dpc, Bgn, lst, cnt, c->gn_tab.p, c->gn_ovf.p, c->list_totals.p + 6);
+      k_gen_neighbours<<<(unsigned)((L + 255) / 256), 256, 0, a>>>(dpc, Bgn, c->gn_ovf.p, c->list_totals.p + 6);
+      return 0;
+    }
+#endif
+    k_gen_neighbours<<<(unsigned)((L + 255) / 256), 256, 0, a>>>(dpc, Bgn, lst, cnt);
+    return 0;
+  };
   auto launch_gn = [&]() -> int {
     if (overlap && !early) {
       HIPC(hipEventRecord(c->ev_fork, s));
       HIPC(hipStreamWaitEvent(a, c->ev_fork, 0));
     }
-#if DPE_GN_LDS
-    if (pc.P.rotate_time <= 4) {   // probe slots in the reference's compaction order (dir_index < 32)
-      HIPC(hipMemsetAsync(c->list_totals.p + 6, 0, sizeof(int), a));
-      k_gn_tables<<<(unsigned)((W + H + 255) / 256), 256, 0, a>>>(dpc, c->gn_tab.p);
-      k_gen_neighbours_lds<<<(unsigned)((L + DPE_GN_BT - 1) / DPE_GN_BT), DPE_GN_BT, 0, a>>>(
-          dpc, Bgn, weak_list, c->list_totals.p + 4, c->gn_tab.p, c->gn_ovf.p, c->list_totals.p + 6);
-      k_gen_neighbours<<<(unsigned)((L + 255) / 256), 256, 0, a>>>(dpc, Bgn, c->gn_ovf.p, c->list_totals.p + 6);
-    } else
-#endif
-    k_gen_neighbours<<<(unsigned)((L + 255) / 256), 256, 0, a>>>(dpc, Bgn, weak_list, c->list_totals.p + 4);
+    if (split) {
+      if (gn_over(split_lists, c->list_totals.p + 9)) return 1;
+      k_list_count<2><<<(pc.half_rows + 3) / 4, 256, 0, a>>>(dpc, Bgn, c->row_counts.p);
+      k_list_scan<2><<<1, 64, 0, a>>>(dpc, c->row_counts.p, c->list_totals.p + 5);
+      k_list_fill<2><<<(pc.half_rows + 3) / 4, 256, 0, a>>>(dpc, Bgn, c->row_counts.p, failed_list, list_stride);
+      HIPC(hipEventRecord(c->ev_gn0, a));
+      if (gn_over(split_lists + L + 64, c->list_totals.p + 10)) return 1;
+      k_neighbour_update<<<fg, fb, 0, a>>>(dpc, Bgn);
+      k_list_count<4><<<(pc.half_rows + 3) / 4, 256, 0, a>>>(dpc, Bgn, c->row_counts.p);
+      k_list_scan<4><<<1, 64, 0, a>>>(dpc, c->row_counts.p, c->list_totals.p + 8);
+      k_list_fill<4><<<(pc.half_rows + 3) / 4, 256, 0, a>>>(dpc, Bgn, c->row_counts.p, failed_list1, list_stride);
+      HIPC(hipEventRecord(c->ev_join, a));
+      return 0;
+    }
+    if (gn_over(weak_list, c->list_totals.p + 4)) return 1;
 #ifdef DPE_GN_TWICE   // timing-only sensitivity probe (not the reference's results)
     k_gen_neighbours<<<(unsigned)((L + 255) / 256), 256, 0, a>>>(dpc, Bgn, weak_list, c->list_totals.p + 4);
 #endif
@@ -825,13 +867,19 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
       HIPC(hipMemcpyAsync(B.sel_snap, B.sel, L * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
       Bc = begin(DPE_CLASS_STRONG);
       strong_sweep(Bc, it, c->lists.p + (colour * 2 + 0) * list_stride, c->list_totals.p + colour * 2 + 0);
-      if (overlap && it == 0 && colour == 0) {
-        HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
-        strong_sweep(Bc, it, failed_list, c->list_totals.p + 5);
-        // the sweep lists after NeigbourUpdate (weak_info is fixed from here until DepthToWeak)
-        k_list_count<0><<<(pc.half_rows + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p);
-        k_list_scan<0><<<1, 256, 0, s>>>(dpc, c->row_counts.p, c->list_totals.p);
-        k_list_fill<0><<<(pc.half_rows + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p, c->lists.p, list_stride);
+      if (overlap && it == 0 && (colour == 0 || split)) {
+        // this colour's pixels whose GenNeighbours failed (UNKNOWN after NeigbourUpdate), same snapshot;
+        // split: colour 0 once GenNeighbours has finished the colour-0 grid pixels, colour 1 (whose
+        // pre-GenNeighbours list ran above) at the join
+        const bool last = !split || colour == 1;
+        HIPC(hipStreamWaitEvent(s, last ? c->ev_join : c->ev_gn0, 0));
+        strong_sweep(Bc, it, colour == 0 ? failed_list : failed_list1, c->list_totals.p + (colour == 0 ? 5 : 8));
+        if (last) {
+          // the sweep lists after NeigbourUpdate (weak_info is fixed from here until DepthToWeak)
+          k_list_count<0><<<(pc.half_rows + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p);
+          k_list_scan<0><<<1, 256, 0, s>>>(dpc, c->row_counts.p, c->list_totals.p);
+          k_list_fill<0><<<(pc.half_rows + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p, c->lists.p, list_stride);
+        }
       }
       end();
     }

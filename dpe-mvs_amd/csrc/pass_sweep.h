@@ -24,17 +24,23 @@ namespace dpe {
 // MODE 2: colour-0 pixels of the red/black grid whose GenNeighbours failed (weak_rel == 0; the
 //         pixels NeigbourUpdate turns UNKNOWN), for the iteration-0 colour-0 strong sweep that runs
 //         beside GenNeighbours on the pre-GenNeighbours list (see dpe_pm_execute).
+// MODE 3: the WEAK pixels in two lists, [0] colour 0 of the red/black grid, [1] all others, so that
+//         GenNeighbours can finish the colour-0 pixels first (dpe_pm_execute, DPE_GN_SPLIT).
+// MODE 4: MODE 2 for colour 1.
 // Row-major order; one wave per row; ballot compaction keeps the order deterministic.
-template <int MODE> DEV int list_rows(const PassConst& pc) { return MODE == 1 ? pc.H : pc.half_rows; }
+template <int MODE> constexpr int list_count() { return MODE == 0 ? 4 : (MODE == 3 ? 2 : 1); }
+template <int MODE> DEV int list_rows(const PassConst& pc) { return (MODE == 1 || MODE == 3) ? pc.H : pc.half_rows; }
 template <int MODE> DEV int list_key(const PassConst& pc, const DevBufs& B, int x, int y) {
   if constexpr (MODE == 2) return (((x + y) & 1) == 0 && B.weak_rel[y * pc.W + x] == 0) ? 0 : -1;
+  if constexpr (MODE == 4) return (((x + y) & 1) == 1 && B.weak_rel[y * pc.W + x] == 0) ? 0 : -1;
   const bool wk = B.weak[y * pc.W + x] == DPE_WEAK;
   if constexpr (MODE == 1) return wk ? 0 : -1;
+  else if constexpr (MODE == 3) return wk ? ((((x + y) & 1) == 0 && y < pc.half_rows) ? 0 : 1) : -1;
   else return (((x + y) & 1) << 1) | (wk ? 1 : 0);
 }
 template <int MODE>
 __global__ void k_list_count(const PassConst* __restrict__ pcp, DevBufs B, int* __restrict__ row_counts) {
-  constexpr int NL = MODE ? 1 : 4;
+  constexpr int NL = list_count<MODE>();
   const PassConst& pc = *pcp;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int y = blockIdx.x * 4 + wave, rows = list_rows<MODE>(pc);
@@ -56,7 +62,7 @@ __global__ void k_list_scan(const PassConst* __restrict__ pcp, int* __restrict__
   const PassConst& pc = *pcp;
   const int j = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int rows = list_rows<MODE>(pc);
-  if (j >= (MODE ? 1 : 4)) return;
+  if (j >= list_count<MODE>()) return;
   int acc = 0;
   for (int y0 = 0; y0 < rows; y0 += 64) {
     const int y = y0 + lane;
@@ -75,7 +81,7 @@ __global__ void k_list_scan(const PassConst* __restrict__ pcp, int* __restrict__
 template <int MODE>
 __global__ void k_list_fill(const PassConst* __restrict__ pcp, DevBufs B, const int* __restrict__ row_offsets,
                             int* __restrict__ lists, long list_stride) {
-  constexpr int NL = MODE ? 1 : 4;
+  constexpr int NL = list_count<MODE>();
   const PassConst& pc = *pcp;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int y = blockIdx.x * 4 + wave, rows = list_rows<MODE>(pc);
