@@ -746,6 +746,7 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
     HIPC(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
   }
   k_gen_edge_inform<<<fg, fb, 0, se>>>(dpc, Bc);
+  if (DPE_EDGE_SCAN && pc.P.use_edge) k_edge_rays<<<(unsigned)(3 * (W + H) - 2), 64, 0, se>>>(dpc, Bc);
   if (early) HIPC(hipEventRecord(c->ev_ei, se));
   k_strong_tables_rows<<<(H + 63) / 64, 64, 0, se>>>(dpc, Bc, c->tab_right.p);
   k_strong_tables_cols<<<(W + 63) / 64, 64, 0, se>>>(dpc, Bc, c->tab_down.p);

@@ -32,6 +32,68 @@ namespace dpe {
 // LDS (bit 0 edge, bit 1 label 0, bit 2 inside the image) for r <= kEiTileR; the counts are
 // integers, so the tile changes nothing but the number of global loads (r^2 per pixel -> ~1.6).
 constexpr int kEiTileR = 8, kEiTile = 16 + 2 * kEiTileR;
+// GenEdgeInform's 8 edge rays (DPE.cu:2497-2530: the first edge pixel along each direction, to the
+// image border) as line scans: every pixel lies on one row, one column, one diagonal (x - y const)
+// and one anti-diagonal (x + y const); along a line the ray in one direction is the nearest edge
+// position after the pixel, in the other the nearest before it.  One wave per line, 64 consecutive
+// positions per step: the edge bits of a step by ballot, the nearest set bit above / below each lane
+// by bit arithmetic, the nearest edge beyond the step carried from the steps already done (the
+// lines are walked once from each end).  Same positions as the per-pixel walks, O(L) loads in all.
+#ifndef DPE_EDGE_SCAN
+#define DPE_EDGE_SCAN 1
+#endif
+__global__ void __launch_bounds__(64) k_edge_rays(const PassConst* __restrict__ pcp, DevBufs B) {
+  const PassConst& pc = *pcp;
+  const int W = pc.W, H = pc.H;
+  const int lane = threadIdx.x;
+  int line = blockIdx.x;
+  // family f: 0 rows (kDir 2 / 3), 1 columns (0 / 1), 2 diagonals (4 / 5), 3 anti-diagonals (7 / 6);
+  // position t along the line, pixel (x0 + t * sx, y0 + t * sy), t in [0, len)
+  int f, x0, y0, sx, sy, len, iprev, inext;
+  if (line < H) { f = 0; x0 = 0; y0 = line; sx = 1; sy = 0; len = W; iprev = 2; inext = 3; }
+  else if ((line -= H) < W) { f = 1; x0 = line; y0 = 0; sx = 0; sy = 1; len = H; iprev = 0; inext = 1; }
+  else if ((line -= W) < W + H - 1) {   // x - y = c, c = line - (H - 1), t = y - max(0, -c)
+    f = 2; const int c = line - (H - 1);
+    y0 = c < 0 ? -c : 0; x0 = c + y0; sx = 1; sy = 1; len = MINo(H - y0, W - x0); iprev = 4; inext = 5;
+  } else {                              // x + y = s, t = y - max(0, s - W + 1)
+    line -= W + H - 1; f = 3; const int sm = line;
+    y0 = sm - (W - 1) > 0 ? sm - (W - 1) : 0; x0 = sm - y0; sx = -1; sy = 1; len = MINo(H - y0, x0 + 1); iprev = 7; inext = 6;
+  }
+  (void)f;
+  const unsigned long long below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  const unsigned long long above = lane == 63 ? 0ull : (~0ull << (lane + 1));
+  // forward: nearest edge before t (direction iprev)
+  int carry = -1;
+  for (int t0 = 0; t0 < len; t0 += 64) {
+    const int t = t0 + lane;
+    const int px = x0 + t * sx, py = y0 + t * sy;
+    const bool e = t < len && B.edge[py * W + px] != 0;
+    const unsigned long long m = __ballot(e);
+    const unsigned long long lo = m & below;
+    const int prev = lo ? t0 + 63 - __builtin_clzll(lo) : carry;
+    if (t < len) {
+      B.edge_neigh[(size_t)(py * W + px) * 8 + iprev] =
+          prev < 0 ? make_short2(-1, -1) : make_short2((short)(x0 + prev * sx), (short)(y0 + prev * sy));
+    }
+    if (m) carry = t0 + 63 - __builtin_clzll(m);
+  }
+  // backward: nearest edge after t (direction inext)
+  carry = -1;
+  for (int t0 = ((len - 1) / 64) * 64; t0 >= 0; t0 -= 64) {
+    const int t = t0 + lane;
+    const int px = x0 + t * sx, py = y0 + t * sy;
+    const bool e = t < len && B.edge[py * W + px] != 0;
+    const unsigned long long m = __ballot(e);
+    const unsigned long long hi = m & above;
+    const int next = hi ? t0 + __builtin_ctzll(hi) : carry;
+    if (t < len) {
+      B.edge_neigh[(size_t)(py * W + px) * 8 + inext] =
+          next < 0 ? make_short2(-1, -1) : make_short2((short)(x0 + next * sx), (short)(y0 + next * sy));
+    }
+    if (m) carry = t0 + __builtin_ctzll(m);
+  }
+}
+
 __global__ void __launch_bounds__(256) k_gen_edge_inform(const PassConst* __restrict__ pcp, DevBufs B) {   // DPE.cu:2483-2591
   const PassConst& pc = *pcp;
   __shared__ uint8_t s_tile[kEiTile * kEiTile];
@@ -56,7 +118,7 @@ __global__ void __launch_bounds__(256) k_gen_edge_inform(const PassConst* __rest
   const int W = pc.W, H = pc.H;
   if (pc.P.use_edge) {
     short2* en = B.edge_neigh + (size_t)center * 8;
-    for (int i = 0; i < 8; i++) {
+    for (int i = 0; i < 8 && !DPE_EDGE_SCAN; i++) {   // DPE_EDGE_SCAN: k_edge_rays writes them
       // first edge pixel along the ray; loads in batches of 8 (one latency per batch)
       short2 r = make_short2(-1, -1);
       const int dx = kDir[i][0], dy = kDir[i][1];
