@@ -203,6 +203,9 @@ const char* dpe_last_error(void) { return g_err.c_str(); }
 #ifndef DPE_GN_LDS
 #define DPE_GN_LDS 1   // scratch-free GenNeighbours (pass_kernels.h k_gen_neighbours_lds)
 #endif
+#ifndef DPE_TABLE_SCAN
+#define DPE_TABLE_SCAN 1   // FindNearestStrongPoint's tables by wave line scans (pass_refine.h)
+#endif
 #ifndef DPE_GN_SPLIT
 #define DPE_GN_SPLIT 0   // 1: GenNeighbours of the colour-0 grid pixels first (early fork only; measured slower)
 #endif
@@ -748,8 +751,12 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   k_gen_edge_inform<<<fg, fb, 0, se>>>(dpc, Bc);
   if (DPE_EDGE_SCAN && pc.P.use_edge) k_edge_rays<<<(unsigned)(3 * (W + H) - 2), 64, 0, se>>>(dpc, Bc);
   if (early) HIPC(hipEventRecord(c->ev_ei, se));
-  k_strong_tables_rows<<<(H + 63) / 64, 64, 0, se>>>(dpc, Bc, c->tab_right.p);
-  k_strong_tables_cols<<<(W + 63) / 64, 64, 0, se>>>(dpc, Bc, c->tab_down.p);
+  if (DPE_TABLE_SCAN) {
+    k_strong_tables_scan<<<(unsigned)(W + H), 64, 0, se>>>(dpc, Bc, c->tab_right.p, c->tab_down.p);
+  } else {
+    k_strong_tables_rows<<<(H + 63) / 64, 64, 0, se>>>(dpc, Bc, c->tab_right.p);
+    k_strong_tables_cols<<<(W + 63) / 64, 64, 0, se>>>(dpc, Bc, c->tab_down.p);
+  }
   k_find_nearest_strong<<<fg, fb, 0, se>>>(dpc, Bc, c->tab_right.p, c->tab_down.p);
   // list of all WEAK pixels (list slot 4), then GenNeighbours one thread per WEAK pixel.  With
   // DPE_GN_SPLIT (early fork) the WEAK pixels come as two lists instead (MODE 3: colour 0 of the

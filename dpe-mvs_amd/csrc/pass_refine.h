@@ -548,6 +548,29 @@ __global__ void __launch_bounds__(64 * DPE_BW_LR, DPE_TAP_WAVES) k_local_refine_
 //   next_down [y*W + x] = smallest y' >= y with weak(x, y') == STRONG (H if none)
 // Ring order of the reference: column dx = -r (all dy ascending), then columns -r < dx < r
 // (dy = -r before dy = +r), then column dx = +r -> first hit = same pixel.
+// Both tables as line scans: one wave per row (next_right) or column (next_down), 64 positions per
+// step from the far end, the nearest STRONG position at or after each lane by ballot bit arithmetic,
+// the nearest one beyond the step carried (same tables as the two one-thread-per-line kernels below).
+__global__ void __launch_bounds__(64) k_strong_tables_scan(const PassConst* __restrict__ pcp, DevBufs B,
+                                                           int* __restrict__ next_right, int* __restrict__ next_down) {
+  const PassConst& pc = *pcp;
+  const int W = pc.W, H = pc.H, lane = threadIdx.x;
+  const bool row = (int)blockIdx.x < H;
+  const int line = row ? (int)blockIdx.x : (int)blockIdx.x - H;
+  const int len = row ? W : H;
+  int* out = row ? next_right : next_down;
+  const unsigned long long from = ~0ull << lane;   // bits lane..63
+  int carry = len;
+  for (int t0 = ((len - 1) / 64) * 64; t0 >= 0; t0 -= 64) {
+    const int t = t0 + lane;
+    const int idx = row ? line * W + t : t * W + line;
+    const bool st = t < len && B.weak[idx] == DPE_STRONG;
+    const unsigned long long m = __ballot(st);
+    const unsigned long long ge = m & from;
+    if (t < len) out[idx] = ge ? t0 + __builtin_ctzll(ge) : carry;
+    if (m) carry = t0 + __builtin_ctzll(m);
+  }
+}
 __global__ void k_strong_tables_rows(const PassConst* __restrict__ pcp, DevBufs B, int* __restrict__ next_right) {
   const PassConst& pc = *pcp;
   const int y = blockIdx.x * blockDim.x + threadIdx.x;
