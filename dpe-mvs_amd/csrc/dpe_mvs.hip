@@ -805,8 +805,11 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
     if (pc.P.rotate_time <= 4) {   // probe slots in the reference's compaction order (dir_index < 32)
       if (!gn_tables) { k_gn_tables<<<(unsigned)((W + H + 255) / 256), 256, 0, a>>>(dpc, c->gn_tab.p); gn_tables = true; }
       HIPC(hipMemsetAsync(c->list_totals.p + 6, 0, sizeof(int), a));
-      k_gen_neighbours_lds<<<(unsigned)((L + DPE_GN_BT - 1) / DPE_GN_BT), DPE_GN_BT, 0, a>>>(
-          dpc, Bgn, lst, cnt, c->gn_tab.p, c->gn_ovf.p, c->list_totals.p + 6);
+      const unsigned gg = (unsigned)((L + DPE_GN_BT - 1) / DPE_GN_BT);
+      if (pc.P.rotate_time <= 2)   // at most 16 x rotate_time support points
+        k_gen_neighbours_lds<32><<<gg, DPE_GN_BT, 0, a>>>(dpc, Bgn, lst, cnt, c->gn_tab.p, c->gn_ovf.p, c->list_totals.p + 6);
+      else
+        k_gen_neighbours_lds<64><<<gg, DPE_GN_BT, 0, a>>>(dpc, Bgn, lst, cnt, c->gn_tab.p, c->gn_ovf.p, c->list_totals.p + 6);
       k_gen_neighbours<<<(unsigned)((L + 255) / 256), 256, 0, a>>>(dpc, Bgn, c->gn_ovf.p, c->list_totals.p + 6);
       return 0;
     }

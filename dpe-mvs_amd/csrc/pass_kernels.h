@@ -533,17 +533,17 @@ __global__ void __launch_bounds__(256, DPE_GN_WAVES) k_gen_neighbours(const Pass
 // scratch, re-read from HBM on every RANSAC try).  The support points are appended in probe order,
 // which is the order of the reference's compaction of strong_points[] (dir_index grows through the
 // probe loops, the label extension follows at 32+; rotate_time <= 4), so they go straight into an
-// LDS column per thread: the packed pixel, kGnK slots ([slot][thread], conflict-free, 8 KB per
-// 64-thread workgroup).  A point's depth is re-read from planes0[] and its normalised image
+// LDS column per thread: the packed pixel, K slots ([slot][thread], conflict-free; K = 16 x
+// rotate_time rounded up to 32 / 64 holds the most a pixel can collect: 8 KB / 16 KB per 64-thread
+// workgroup).  A point's depth is re-read from planes0[] and its normalised image
 // coordinates come from per-column / per-row tables (`gtab`, the same expression per coordinate), so
 // nothing else is stored.  The edge tests are recomputed instead of cached (BresenhamLine is a pure
 // function of its end points; the reference's edge_test[][] only saves work), the probe batches
 // re-position the Philox stream by its word index instead of saving its state, and the two sorts
 // become order-statistic selections whose results equal the insertion sorts' whenever no residual
-// or weight is NaN.  A pixel with more than kGnK support points, or a NaN where a sort needs the
+// or weight is NaN.  A pixel with more than K support points, or a NaN where a sort needs the
 // order, writes nothing and is appended to `ovf` for k_gen_neighbours (its Philox stream is
 // addressed by the pixel, so the rerun draws the same numbers).  96 VGPRs, 5 waves per SIMD.
-constexpr int kGnK = 32;
 #ifndef DPE_GN_BT
 #define DPE_GN_BT 64
 #endif
@@ -610,13 +610,14 @@ DEV bool bresenham_short(const PassConst& pc, const DevBufs& B, int Ax, int Ay, 
 #ifndef DPE_GN_MINW
 #define DPE_GN_MINW 1
 #endif
+template <int K>
 __global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(const PassConst* __restrict__ pcp, DevBufs B,
                                                                   const int* __restrict__ list, const int* __restrict__ nlist_p,
                                                                   const float* __restrict__ gtab, int* __restrict__ ovf,
                                                                   int* __restrict__ novf) {   // DPE.cu:2103-2463
-  __shared__ uint32_t s_pt[kGnK][DPE_GN_BT];    // support point (x | y << 16)
+  __shared__ uint32_t s_pt[K][DPE_GN_BT];       // support point (x | y << 16)
 #if DPE_GN_DP
-  __shared__ float s_dp[kGnK][DPE_GN_BT];       // its depth, then (after the RANSAC) its weight
+  __shared__ float s_dp[K][DPE_GN_BT];          // its depth, then (after the RANSAC) its weight
 #endif
   const PassConst& pc = *pcp;
   const int t = threadIdx.x;
@@ -633,7 +634,7 @@ __global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(c
   int valid_count = 0;
   bool overflow = false;
   auto push = [&](short2 np) {
-    if (valid_count < kGnK) s_pt[valid_count][t] = (uint32_t)(uint16_t)np.x | ((uint32_t)(uint16_t)np.y << 16);
+    if (valid_count < K) s_pt[valid_count][t] = (uint32_t)(uint16_t)np.x | ((uint32_t)(uint16_t)np.y << 16);
     else overflow = true;
     valid_count++;
   };
@@ -917,19 +918,19 @@ __global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(c
 #endif
   if (wnan) { defer(); return; }
   short2 out[DPE_NEIGHBOUR_NUM - 1];
-  uint32_t taken = 0;
+  uint64_t taken = 0;
 #pragma unroll
   for (int k = 0; k < DPE_NEIGHBOUR_NUM - 1; ++k) {
     int bi = -1; float bw = 0.0f;
     for (int i = 0; i < valid_count; ++i) {
-      if ((taken >> i) & 1u) continue;
+      if ((taken >> i) & 1ull) continue;
       const float w = weight_at(i);
       if (bi < 0 || w < bw) { bi = i; bw = w; }
     }
 #if DPE_GN_DP
-    if (bi >= 0) { taken |= 1u << bi; out[k] = pt_at(bi); }
+    if (bi >= 0) { taken |= 1ull << bi; out[k] = pt_at(bi); }
 #else
-    if (bi >= 0) { taken |= 1u << bi; out[k] = bw >= ransac_threshold ? make_short2(-1, -1) : pt_at(bi); }
+    if (bi >= 0) { taken |= 1ull << bi; out[k] = bw >= ransac_threshold ? make_short2(-1, -1) : pt_at(bi); }
 #endif
     else out[k] = make_short2(-1, -1);
   }
