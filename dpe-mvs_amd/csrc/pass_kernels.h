@@ -604,6 +604,9 @@ DEV bool bresenham_short(const PassConst& pc, const DevBufs& B, int Ax, int Ay, 
   return !(ea || eb) && hit != 0;
 }
 
+#ifndef DPE_GN_PRECHECK
+#define DPE_GN_PRECHECK 0   // 1: skip the draws of radii none of whose possible targets can pass (slower)
+#endif
 #ifndef DPE_GNL_SPEC
 #define DPE_GNL_SPEC 4   // probe attempts drawn and loaded together (1, 2 or 4)
 #endif
@@ -683,6 +686,48 @@ __global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(c
         const float tpx = (float)x + od.x * radius, tpy = (float)y + od.y * radius;
         if (tpx < 0 || tpy < 0 || tpx >= W || tpy >= H) next = true;
       }
+#if DPE_GN_PRECHECK
+      // An attempt's shifts (rxs, rys) are residues mod shift_range, so at most shift_range^2 targets
+      // are possible at this radius.  When none of them can pass the tests that come before the
+      // Bresenham walk (margin, a STRONG pixel or its nearest STRONG point, the angle), all 4
+      // attempts fail whatever is drawn: the stream skips their 16 words without drawing them.
+      // (Tried for shift_range <= 3, i.e. rotate_time >= 2; 74 % of the reference's attempts fail
+      // on the angle, 2 % succeed.)
+      if (!next && shift_range <= 3) {
+        bool can[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+          const int a = k / 3, b = k % 3;
+          can[k] = false;
+          if (a < shift_range && b < shift_range) {
+            float2 dir = make_float2(od.x * 20 + (float)a, od.y * 20 + (float)b);
+            normalize2(dir);
+            short2 np = make_short2((short)f2i((float)x + dir.x * radius), (short)f2i((float)y + dir.y * radius));
+            const bool in = !(np.x < min_margin || np.y < min_margin || np.x >= W - min_margin || np.y >= H - min_margin);
+            const int npc = in ? np.x + np.y * W : center;
+            const uint8_t wk = B.weak[npc];
+            const short2 nn = B.nearest[npc];
+            if (in) {
+              if (wk != DPE_STRONG) np = nn;
+              if (np.x != -1 && np.y != -1) {
+                float2 td = make_float2((float)(np.x - x), (float)(np.y - y));
+                normalize2(td);
+                can[k] = td.x * od.x + td.y * od.y > threshhold;
+              }
+            }
+          }
+        }
+        bool any = false;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) any = any || can[k];
+        if (!any) {
+          const uint32_t pos = rs.idx == 4 ? rs.ctr * 4u : (rs.ctr - 1u) * 4u + (uint32_t)rs.idx;
+          rng_seek(rs, pos + 16u);
+          radius = MINo(radius * 2, radius + 25);
+          continue;
+        }
+      }
+#endif
       if (!next) {
         bool dir_found = false;
         for (int ra = 0; ra < 4 && !dir_found; ra += DPE_GNL_SPEC) {
