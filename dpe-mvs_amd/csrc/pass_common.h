@@ -861,6 +861,9 @@ DEV uint8_t low_edge_at(const PassConst& pc, const DevBufs& B, int idx) {
 // reference returns at the first edge pixel it meets, so the result is "any edge pixel among the
 // positions the walk visits before it stops".  Positions are generated in batches of 8 and their
 // loads issued together: one memory latency per batch instead of one per step.
+#ifndef DPE_BRES_BATCH
+#define DPE_BRES_BATCH 8
+#endif
 DEV bool bresenham(const PassConst& pc, const DevBufs& B, int Ax, int Ay, int Bx, int By) {
   const int W = pc.W;
   if (B.edge[Ax + Ay * W] || B.edge[Bx + By * W]) return false;
@@ -881,9 +884,9 @@ DEV bool bresenham(const PassConst& pc, const DevBufs& B, int Ax, int Ay, int Bx
     int step = 0;
     bool tagx = true, tagy = true, more = true;
     while (more) {
-      int idx[8];
+      int idx[DPE_BRES_BATCH];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
+      for (int k = 0; k < DPE_BRES_BATCH; ++k) {
         idx[k] = -1;                                  // low_edge_at(-1) == 0
         if (more && (tagx || tagy)) {
           if (x0 == x1) tagx = false;
@@ -900,7 +903,7 @@ DEV bool bresenham(const PassConst& pc, const DevBufs& B, int Ax, int Ay, int Bx
       }
       uint8_t hit = 0;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) hit |= low_edge_at(pc, B, idx[k]);
+      for (int k = 0; k < DPE_BRES_BATCH; ++k) hit |= low_edge_at(pc, B, idx[k]);
       if (hit) return true;
     }
   }

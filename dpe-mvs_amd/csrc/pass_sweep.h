@@ -925,8 +925,11 @@ __host__ __device__ inline int weak_lds_per_pixel(int nv) { return (kWeakFixed +
 
 // CheckerboardPropagationWeak (DPE.cu:1668-1862) + PlaneHypothesisRefinementWeak (:1120-1212).
 // C lanes per pixel, 64/C pixels per wave, blockDim.x/64 waves per workgroup.
+#ifndef DPE_WEAK_WAVES
+#define DPE_WEAK_WAVES DPE_TAP_WAVES
+#endif
 template <int U8, int C>
-__global__ void __launch_bounds__(256, DPE_TAP_WAVES) k_weak_coop(const PassConst* __restrict__ pcp, DevBufs B, int iter,
+__global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassConst* __restrict__ pcp, DevBufs B, int iter,
                                                    const int* __restrict__ list, const int* __restrict__ nlist_p) {
   extern __shared__ float4 lds4[];
   static_assert(C == 16 || C == 32, "the per-pixel phases give lanes 0..8 the patch sums and lanes 8..15 the alias rows");

@@ -161,8 +161,10 @@ int dpe_pm_stage(DpeContext* ctx, const DpePassInput* in, const DpePassState* st
  * Part of the pass runs on the context's second (aux) stream, forked from and joined back into
  * `stream` with events, so all work is complete when `stream` reaches the end of the call's
  * enqueued work (environment DPE_OVERLAP=0, timing or counting keep everything on `stream`).
- * The aux stream runs the setup chain: GenEdgeInform, FindNearestStrongPoint's tables and search,
- * the WEAK-pixel list, GenNeighbours and NeigbourUpdate.  Beside it `stream` runs
+ * The aux stream runs the setup chain: GenEdgeInform and its edge-ray line scans,
+ * FindNearestStrongPoint's tables and search, the WEAK-pixel list, GenNeighbours (the scratch-free
+ * kernel, its coordinate tables and the scratch kernel for its overflow pixels) and NeigbourUpdate.
+ * Beside it `stream` runs
  * RandomInitialization (reads planes/sel/images, writes planes/costs/sel) and the iteration-0
  * colour-0 strong half-sweep, which waits for GenEdgeInform's event only (it reads the edge rays;
  * it must not read nearest, nb, weak_rel or radius, which the aux stream is still writing); every
