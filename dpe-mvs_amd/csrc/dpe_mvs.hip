@@ -155,6 +155,7 @@ struct DpeContext {
   DevArr<int> tab_right, tab_down;   // FindNearestStrongPoint tables
   DevArr<int> gn_ovf;                // GenNeighbours pixels left to the scratch kernel (k_gen_neighbours_lds)
   DevArr<float> gn_tab;              // normalised image coordinates per column / row (k_gn_tables)
+  DevArr<uint8_t> gn_ecache;         // GenNeighbours' edge-test cache, 496 pair bytes per WEAK pixel
   DevArr<int> lists, row_counts, list_totals;   // per-colour pixel lists for the sweeps
   DevBufs bufs;
   // fusion (dpe_fusion_stage / dpe_fusion_candidates)
@@ -202,6 +203,9 @@ const char* dpe_last_error(void) { return g_err.c_str(); }
 
 #ifndef DPE_GN_LDS
 #define DPE_GN_LDS 1   // scratch-free GenNeighbours (pass_kernels.h k_gen_neighbours_lds)
+#endif
+#ifndef DPE_GN_ECACHE
+#define DPE_GN_ECACHE 0   // 1: GenNeighbours' edge-test cache in HBM (pass_kernels.h; measured slower)
 #endif
 #ifndef DPE_TABLE_SCAN
 #define DPE_TABLE_SCAN 1   // FindNearestStrongPoint's tables by wave line scans (pass_refine.h)
@@ -300,7 +304,7 @@ void dpe_destroy(DpeContext* c) {
   c->e_rows.release(); c->e_mag.release(); c->e_itab.release(); c->e_dx.release(); c->e_dy.release();
   c->e_ftab.release(); c->e_stab.release();
   c->cnt.release();
-  c->tab_right.release(); c->tab_down.release(); c->gn_ovf.release(); c->gn_tab.release();
+  c->tab_right.release(); c->tab_down.release(); c->gn_ovf.release(); c->gn_tab.release(); c->gn_ecache.release();
   c->lists.release(); c->row_counts.release(); c->list_totals.release();
   (void)hipStreamSynchronize(c->aux);
   (void)hipEventDestroy(c->ev_fork); (void)hipEventDestroy(c->ev_join); (void)hipEventDestroy(c->ev_ei);
@@ -806,10 +810,18 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
       if (!gn_tables) { k_gn_tables<<<(unsigned)((W + H + 255) / 256), 256, 0, a>>>(dpc, c->gn_tab.p); gn_tables = true; }
       HIPC(hipMemsetAsync(c->list_totals.p + 6, 0, sizeof(int), a));
       const unsigned gg = (unsigned)((L + DPE_GN_BT - 1) / DPE_GN_BT);
+      uint8_t* ec = nullptr;
+      if (DPE_GN_ECACHE && pc.P.use_limit && pc.P.rotate_time <= 2) {   // 32 points: 496 pairs
+        HIPC(c->gn_ecache.ensure((size_t)496 * (L + 64)));
+        HIPC(hipMemsetAsync(c->gn_ecache.p, 0, (size_t)496 * (L + 64), a));
+        ec = c->gn_ecache.p;
+      }
       if (pc.P.rotate_time <= 2)   // at most 16 x rotate_time support points
-        k_gen_neighbours_lds<32><<<gg, DPE_GN_BT, 0, a>>>(dpc, Bgn, lst, cnt, c->gn_tab.p, c->gn_ovf.p, c->list_totals.p + 6);
+        k_gen_neighbours_lds<32><<<gg, DPE_GN_BT, 0, a>>>(dpc, Bgn, lst, cnt, c->gn_tab.p, c->gn_ovf.p, c->list_totals.p + 6,
+                                                          ec, (long)L + 64);
       else
-        k_gen_neighbours_lds<64><<<gg, DPE_GN_BT, 0, a>>>(dpc, Bgn, lst, cnt, c->gn_tab.p, c->gn_ovf.p, c->list_totals.p + 6);
+        k_gen_neighbours_lds<64><<<gg, DPE_GN_BT, 0, a>>>(dpc, Bgn, lst, cnt, c->gn_tab.p, c->gn_ovf.p, c->list_totals.p + 6,
+                                                          nullptr, 0);
       k_gen_neighbours<<<(unsigned)((L + 255) / 256), 256, 0, a>>>(dpc, Bgn, c->gn_ovf.p, c->list_totals.p + 6);
       return 0;
     }

@@ -617,7 +617,8 @@ template <int K>
 __global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(const PassConst* __restrict__ pcp, DevBufs B,
                                                                   const int* __restrict__ list, const int* __restrict__ nlist_p,
                                                                   const float* __restrict__ gtab, int* __restrict__ ovf,
-                                                                  int* __restrict__ novf) {   // DPE.cu:2103-2463
+                                                                  int* __restrict__ novf, uint8_t* __restrict__ ecache,
+                                                                  long estride) {   // DPE.cu:2103-2463
   __shared__ uint32_t s_pt[K][DPE_GN_BT];       // support point (x | y << 16)
 #if DPE_GN_DP
   __shared__ float s_dp[K][DPE_GN_BT];          // its depth, then (after the RANSAC) its weight
@@ -858,9 +859,25 @@ __global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(c
       const short2 pa = pt_at(a), pb = pt_at(b), pcc = pt_at(c);
       if (must_in_triangle && !point_in_triangle(pa, pb, pcc, x, y)) continue;
       if (edge_limit) {
-        const bool eab = crosses(pa.x, pa.y, pb.x, pb.y);
-        const bool ebc = crosses(pb.x, pb.y, pcc.x, pcc.y);
-        const bool eca = crosses(pcc.x, pcc.y, pa.x, pa.y);
+        bool eab, ebc, eca;
+        if (ecache != nullptr && K <= 32) {
+          // the reference's edge_test[a][b] cache (DPE.cu:2307-2331) in HBM, one byte per point pair
+          // ([pair][thread], zeroed per pass: 0 untested, 1 no edge, 2 edge); BresenhamLine is
+          // symmetric in its end points (both directions are walked), so a pair has one entry
+          auto slot = [&](int u, int v) -> uint8_t* {
+            const int lo = MINo(u, v), hi = MAXo(u, v);
+            return ecache + (size_t)(hi * (hi - 1) / 2 + lo) * (size_t)estride + gi;
+          };
+          uint8_t* sab = slot(a, b); uint8_t* sbc = slot(b, c); uint8_t* sca = slot(c, a);
+          const uint8_t vab = *sab, vbc = *sbc, vca = *sca;
+          if (vab) eab = vab == 2; else { eab = crosses(pa.x, pa.y, pb.x, pb.y); *sab = eab ? 2 : 1; }
+          if (vbc) ebc = vbc == 2; else { ebc = crosses(pb.x, pb.y, pcc.x, pcc.y); *sbc = ebc ? 2 : 1; }
+          if (vca) eca = vca == 2; else { eca = crosses(pcc.x, pcc.y, pa.x, pa.y); *sca = eca ? 2 : 1; }
+        } else {
+          eab = crosses(pa.x, pa.y, pb.x, pb.y);
+          ebc = crosses(pb.x, pb.y, pcc.x, pcc.y);
+          eca = crosses(pcc.x, pcc.y, pa.x, pa.y);
+        }
         if (eab || ebc || eca) continue;
       }
       bool normal_consistency = false;
