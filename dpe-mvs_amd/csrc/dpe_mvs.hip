@@ -204,9 +204,6 @@ const char* dpe_last_error(void) { return g_err.c_str(); }
 #ifndef DPE_GN_LDS
 #define DPE_GN_LDS 1   // scratch-free GenNeighbours (pass_kernels.h k_gen_neighbours_lds)
 #endif
-#ifndef DPE_GN_ECACHE
-#define DPE_GN_ECACHE 0   // 1: GenNeighbours' edge-test cache in HBM (pass_kernels.h; measured slower)
-#endif
 #ifndef DPE_TABLE_SCAN
 #define DPE_TABLE_SCAN 1   // FindNearestStrongPoint's tables by wave line scans (pass_refine.h)
 #endif

@@ -604,6 +604,9 @@ DEV bool bresenham_short(const PassConst& pc, const DevBufs& B, int Ax, int Ay, 
   return !(ea || eb) && hit != 0;
 }
 
+#ifndef DPE_GN_ECACHE
+#define DPE_GN_ECACHE 0   // 1: the edge-test cache in HBM (slower: DESIGN.md §8)
+#endif
 #ifndef DPE_GN_PRECHECK
 #define DPE_GN_PRECHECK 0   // 1: skip the draws of radii none of whose possible targets can pass (slower)
 #endif
@@ -860,7 +863,7 @@ __global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(c
       if (must_in_triangle && !point_in_triangle(pa, pb, pcc, x, y)) continue;
       if (edge_limit) {
         bool eab, ebc, eca;
-        if (ecache != nullptr && K <= 32) {
+        if (DPE_GN_ECACHE && K <= 32 && ecache != nullptr) {
           // the reference's edge_test[a][b] cache (DPE.cu:2307-2331) in HBM, one byte per point pair
           // ([pair][thread], zeroed per pass: 0 untested, 1 no edge, 2 edge); BresenhamLine is
           // symmetric in its end points (both directions are walked), so a pair has one entry
