@@ -1,4 +1,4 @@
-# round 4 session A: bit-exact A/B of the fract-weight taps and the scratch-free GenNeighbours
+# round 3 session 2, A: bit-exact A/B of the fract-weight taps and the scratch-free GenNeighbours
 # against the round-3 build, then the parity suite on the scratch-free build
 cd "$GRAFT_REPO_ROOT"
 export PYTHONUNBUFFERED=1
