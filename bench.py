@@ -272,11 +272,22 @@ def main():
     depth_local = torch.empty((Hd, Wd), dtype=torch.float32, device="cuda")
     gathered = [torch.empty_like(depth_local) for _ in range(world)] if world > 1 else None
 
-    def step():
+    # at N > 1 the step's exchange (export_depth + the all-gather) is bracketed by stream events so
+    # that its share of the step is reported beside the pass (events on the pass stream: the
+    # all-gather's completion is ordered into it before the next step)
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)] if world > 1 else None
+
+    def step(k=None):
+        if evs is not None and k is not None:
+            evs[k][0].record(stream)
         ctx.execute(sp)
         if world > 1:
+            if k is not None:
+                evs[k][1].record(stream)
             ctx.export_depth(depth_local.data_ptr(), sp)
             dist.all_gather(gathered, depth_local)
+            if k is not None:
+                evs[k][2].record(stream)
 
     for _ in range(args.warmup):
         step()
@@ -285,8 +296,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    for k in range(args.steps):
+        step(k)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -298,10 +309,27 @@ def main():
         dt = float(t.item())
     ms_per_step = dt / args.steps * 1e3
     value = world * args.steps * Wd * Hd / dt / 1e6
+    exchange = None
+    if world > 1:   # per-step means on this rank, then the max over ranks
+        ex_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
+        pass_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
+        t = torch.tensor([ex_ms, pass_ms], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ex_ms, pass_ms = float(t[0]), float(t[1])
+        exchange = {"allgather_ms": round(ex_ms, 4), "execute_ms": round(pass_ms, 3),
+                    "comm_share": round(ex_ms / ms_per_step, 5), "world": world, "backend": dist.get_backend(),
+                    "ranks_in_group": dist.get_world_size(),
+                    "bytes_per_rank": Wd * Hd * 4, "bytes_gathered": world * Wd * Hd * 4,
+                    "scope": "per step, max over ranks: export_depth + all_gather of the f32 depth maps (stream "
+                             "events on the pass stream); execute_ms = the pass",
+                    "measured_on_hardware": dist.get_backend() == "nccl"}
 
     if args.no_instrument:
         if rank == 0:
-            print(json.dumps({"metric": METRIC, "value": round(value, 4), "unit": "Mpix/s", "ms_per_step": round(ms_per_step, 3)}))
+            line = {"metric": METRIC, "value": round(value, 4), "unit": "Mpix/s", "ms_per_step": round(ms_per_step, 3)}
+            if exchange is not None:
+                line["exchange"] = exchange
+            print(json.dumps(line))
         ctx.close()
         return
     # instrumented (untimed) runs: per-class kernel time (hipEvents on the pass stream) and
@@ -410,6 +438,8 @@ def main():
         "kernel_ms": {k: round(v, 3) for k, v in tim.items()},
         "work": {k: v for k, v in cnt.items() if v["launches"]},
     }
+    if exchange is not None:
+        result["exchange"] = exchange
     if not args.no_pipeline:   # every rank joins (the pipeline all-gathers depth maps between passes)
         ctx.close()
         ctx = None

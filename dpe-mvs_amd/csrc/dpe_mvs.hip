@@ -931,7 +931,7 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   launch_depth_to_weak(c->img8, (long)L, s, dpc, Bc);
   end();
   Bc = begin(DPE_CLASS_LOCAL_REFINE);
-  launch_local_refine(c->img8, (long)L, nv, s, dpc, Bc);
+  launch_local_refine(c->img8, (long)L, W, H, nv, s, dpc, Bc);
   end();
   HIPC(hipGetLastError());
   if (slot_overflow) {   // per-class times would silently miss launches

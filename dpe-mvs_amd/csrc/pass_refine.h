@@ -320,10 +320,42 @@ DEV uint8_t d2w_class(const PassConst& pc, const float* pcs, uint64_t is_peak) {
 #ifndef DPE_D2W_WAVES
 #define DPE_D2W_WAVES DPE_TAP_WAVES
 #endif
-template <int U8>
+// LocalRefine fused into DepthToWeak's epilogue (LR = true).  For an interior pixel LocalRefine's 11
+// hypotheses (p_disp -5..5, DPE.cu:2809-2831) are DepthToWeak's samples 25..35 (:2663-2686): same
+// plane, depth, selected views and weights, so every per-view NCC and geometric term is the same
+// value; only the sums differ (LocalRefine adds ncc*vw and gf*geom*vw as two terms, DepthToWeak
+// (ncc + gf*geom)*vw), so lanes 25..35 keep both sums.  Lane 61 evaluates cost_now at the current
+// depth (:2776-2795), whose sum is DepthToWeak's.  Both kernels read only their own pixel's plane
+// and write only their own pixel (weak_info / plane.w), and the geometric term reads the source
+// depth maps, so doing LocalRefine right after the classification of the same pixel gives the
+// reference's results.  The 6-pixel border, where DepthToWeak stops at once (:2604-2607) but
+// LocalRefine runs, goes to k_local_refine_jobs over the border pixels (border_pixel).
+#ifndef DPE_FUSE_LR
+#define DPE_FUSE_LR 1
+#endif
+constexpr int kD2WMargin = 6;
+// pixels outside DepthToWeak's interior (x or y within kD2WMargin of the edge), enumerated: top rows,
+// bottom rows, then the left and right margins of the rows in between (every pixel if no interior)
+__host__ __device__ inline long border_count(int W, int H) {
+  constexpr int m = kD2WMargin;
+  if (W <= 2 * m || H <= 2 * m) return (long)W * H;
+  return 2L * m * W + 2L * m * (H - 2 * m);
+}
+DEV long border_pixel(long i, int W, int H) {
+  constexpr int m = kD2WMargin;
+  if (W <= 2 * m || H <= 2 * m) return i;
+  const long top = (long)m * W;
+  if (i < top) return i;
+  if (i < 2 * top) return (long)(H - m) * W + (i - top);
+  const long r = i - 2 * top;
+  const int row = m + (int)(r / (2 * m)), c = (int)(r % (2 * m));
+  return (long)row * W + (c < m ? c : W - 2 * m + c);
+}
+template <int U8, bool LR = false>
 __global__ void __launch_bounds__(64 * DPE_BW_D2W, DPE_D2W_WAVES) k_depth_to_weak(const PassConst* __restrict__ pcp, DevBufs B) {   // DPE.cu:2593-2747
   __shared__ float s_patch[DPE_BW_D2W][108];
-  __shared__ float s_pc[DPE_BW_D2W][64];
+  __shared__ float s_pc[DPE_BW_D2W][64];          // [0..60] cost curve, [61] LocalRefine's cost_now
+  __shared__ float s_lr[DPE_BW_D2W][11];          // LocalRefine's hypothesis costs (pd -5..5)
   const PassConst& pc = *pcp;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int W = pc.W, H = pc.H;
@@ -331,7 +363,7 @@ __global__ void __launch_bounds__(64 * DPE_BW_D2W, DPE_D2W_WAVES) k_depth_to_wea
   if (pix >= (long)W * H) return;                 // wave-uniform
   const int x = (int)(pix % W), y = (int)(pix / W);
   const int center = (int)pix;
-  const int min_margin = 6;
+  const int min_margin = kD2WMargin;
   if (x < min_margin || y < min_margin || x >= W - min_margin || y >= H - min_margin) {
     if (lane == 0) B.weak[center] = DPE_UNKNOWN;
     return;
@@ -356,11 +388,13 @@ __global__ void __launch_bounds__(64 * DPE_BW_D2W, DPE_D2W_WAVES) k_depth_to_wea
   if (fast) patch_lds_pre(pw, s_ref, s_rr, s_w);
   PHASE(0);
   const int radius = 30;
-  if (lane < 2 * radius + 1) {
+  constexpr int kNow = 2 * radius + 1;            // lane of LocalRefine's cost_now
+  const bool lr_pix = LR && weight_normal != 0;   // LocalRefine skips the pixel otherwise (:2797)
+  if (lane < 2 * radius + 1 || (lr_pix && lane == kNow)) {
     const int pd = lane - radius;
-    const float p_depth = c0.K[0] * base_line / (disp + (float)pd);
-    float val;
-    if (p_depth < pc.P.depth_min || p_depth > pc.P.depth_max) val = 2.0f;
+    const float p_depth = lane == kNow ? od : c0.K[0] * base_line / (disp + (float)pd);
+    float val, lr = 0.0f;
+    if (lane != kNow && (p_depth < pc.P.depth_min || p_depth > pc.P.depth_max)) val = 2.0f;
     else {
       float4 tp = op;
       tp.w = dist2origin(c0, x, y, p_depth, tp);
@@ -370,17 +404,25 @@ __global__ void __launch_bounds__(64 * DPE_BW_D2W, DPE_D2W_WAVES) k_depth_to_wea
         const int vi = si - 1;
         if (isSet(sel, vi)) {
           float tcst = 0.0f;
-          tcst += ncc_old_any<U8, DPE_D2W_ELIDE>(fast, pw, s_ref, s_rr, s_w, x, y, pc, B, si, tp);
+          const float c = ncc_old_any<U8, DPE_D2W_ELIDE>(fast, pw, s_ref, s_rr, s_w, x, y, pc, B, si, tp);
+          tcst += c;
           PHASE(1);
-          if (pc.P.geom_consistency) tcst += pc.P.geom_factor * geom_cost_at(pc, B, x, y, si, fw);
+          if constexpr (LR) lr += (c * vw[vi]);                       // DPE.cu:2820
+          if (pc.P.geom_consistency) {
+            const float g = pc.P.geom_factor * geom_cost_at(pc, B, x, y, si, fw);
+            tcst += g;
+            if constexpr (LR) lr += (g * vw[vi]);                     // :2822
+          }
           PHASE(2);
           p_cost += (tcst * vw[vi]);
         }
       }
       p_cost /= weight_normal;
-      val = MINo(2.0f, p_cost);
+      val = lane == kNow ? p_cost : MINo(2.0f, p_cost);              // cost_now is not clamped
+      lr /= weight_normal;
     }
     s_pc[wave][lane] = val;
+    if (LR && lane >= radius - 5 && lane <= radius + 5) s_lr[wave][lane - (radius - 5)] = lr;
   }
   wave_sync();
   PHASE(3);
@@ -393,6 +435,16 @@ __global__ void __launch_bounds__(64 * DPE_BW_D2W, DPE_D2W_WAVES) k_depth_to_wea
   PHASE_END(3);
   if (lane != 0) return;
   B.weak[center] = d2w_class(pc, pcs, is_peak);
+  if (!lr_pix) return;
+  // LocalRefine's choice (DPE.cu:2807-2834): the in-range hypothesis of least cost in pd order
+  float min_cost = 2.0f, best_depth = od;
+  for (int pd = -5; pd <= 5; ++pd) {
+    const float p_depth = c0.K[0] * base_line / (disp + (float)pd);
+    if (p_depth < pc.P.depth_min || p_depth > pc.P.depth_max) continue;
+    const float tcv = s_lr[wave][pd + 5];
+    if (tcv < min_cost) { min_cost = tcv; best_depth = p_depth; }
+  }
+  if ((double)(pcs[kNow] - min_cost) > 0.1) B.planes[center].w = best_depth;
 }
 
 // ------------------------------------------------------------------------------ LocalRefine
@@ -405,7 +457,8 @@ constexpr int kLrPix = 4;
 #define DPE_LR_VIEW_MAJOR 1
 #endif
 template <int U8>
-__global__ void __launch_bounds__(64 * DPE_BW_LR, DPE_TAP_WAVES) k_local_refine_jobs(const PassConst* __restrict__ pcp, DevBufs B) {   // DPE.cu:2749-2835
+__global__ void __launch_bounds__(64 * DPE_BW_LR, DPE_TAP_WAVES) k_local_refine_jobs(const PassConst* __restrict__ pcp, DevBufs B,
+                                                                                     int border) {   // DPE.cu:2749-2835
   constexpr int BW = DPE_BW_LR;
   __shared__ float s_patch[BW][kLrPix][108];
   __shared__ float s_sum[BW][kLrPix][3];
@@ -419,8 +472,11 @@ __global__ void __launch_bounds__(64 * DPE_BW_LR, DPE_TAP_WAVES) k_local_refine_
   const PassConst& pc = *pcp;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int W = pc.W;
-  const long L = (long)W * pc.H;
-  const long base = ((long)xcd_remap(blockIdx.x, gridDim.x, B.xcd_rows * 16 * ((pc.W + 4 * kLrPix - 1) / (4 * kLrPix))) * BW + wave) * kLrPix;
+  // border != 0: only the pixels outside DepthToWeak's interior (border_pixel), whose LocalRefine the
+  // fused DepthToWeak does not do; else every pixel
+  const long L = border ? border_count(W, pc.H) : (long)W * pc.H;
+  const long base = border ? ((long)blockIdx.x * BW + wave) * kLrPix
+                           : ((long)xcd_remap(blockIdx.x, gridDim.x, B.xcd_rows * 16 * ((pc.W + BW * kLrPix - 1) / (BW * kLrPix))) * BW + wave) * kLrPix;
   if (base >= L) return;                          // wave-uniform
   const DpeCamera& c0 = pc.cams[0];
   const bool fast = DPE_FAST_PATCH(pc);
@@ -429,8 +485,8 @@ __global__ void __launch_bounds__(64 * DPE_BW_LR, DPE_TAP_WAVES) k_local_refine_
   float* res = s_dyn + (size_t)wave * kLrPix * 12 * nv * 2;   // res[((p * 12 + h) * nv + k) * 2 + {0, 1}]
   // ---- per pixel set-up: 16 lanes per pixel
   const int gp = lane >> 4, gl = lane & 15;
-  const long pix = base + gp;
-  const bool act = pix < L;
+  const bool act = base + gp < L;
+  const long pix = !act ? 0 : border ? border_pixel(base + gp, W, pc.H) : base + gp;
   const int x = act ? (int)(pix % W) : 0, y = act ? (int)(pix / W) : 0;
   float4 op = make_float4(0, 0, 0, 0);
   float od = 0, base_line = 0, weight_normal = 0;

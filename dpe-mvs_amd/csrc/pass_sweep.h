@@ -14,6 +14,7 @@
 #pragma once
 #include "pass_common.h"
 #include "pass_refine.h"
+#include "lds_layout.h"
 
 namespace dpe {
 
@@ -287,17 +288,14 @@ DEV int acmh_candidate(const PassConst& pc, const float* __restrict__ costs, int
 }
 
 // ------------------------------------------------------------------------------ strong sweep
-// LDS floats per wave for P pixels, C candidate lanes each, nv source views (multiple of 4)
-__host__ __device__ inline int strong_lds_base(int P, int C, int nv) {   // floats before the plane table
-  return (P * (165 + 2 * C + (C + 8) * nv) + 3) & ~3;
-}
 #ifndef DPE_TAIL_SPLIT
 #define DPE_TAIL_SPLIT 1
 #endif
 constexpr int kTailJobs = 16;   // a last round of at most this many jobs is split by patch rows
+// the strong sweep's LDS carve per wave (lds_layout.h: P pixels, C candidate lanes, nv source views)
+template <int P, int C> using StrongCarveT = lds::StrongCarve<P, C, DPE_TAIL_SPLIT ? kTailJobs : 0>;
 __host__ __device__ inline int strong_lds_per_wave(int P, int C, int nv) {
-  // + planes [P][C+1] float4 + alias [P][C+1] (+ the split tail's row sums [kTailJobs][6][3])
-  return strong_lds_base(P, C, nv) + P * (C + 1) * 5 + (DPE_TAIL_SPLIT ? kTailJobs * 18 : 0);
+  return P == 4 && C == 16 ? StrongCarveT<4, 16>::total(nv) : StrongCarveT<8, 8>::total(nv);
 }
 
 // Job pools of a wave: the NCCs of all its pixels are dealt round-robin over the 64 lanes, so a
@@ -336,26 +334,27 @@ __global__ void __launch_bounds__(64 * DPE_BW_STRONG, DPE_TAP_WAVES) k_strong_co
   const bool active = gi < nlist;
   const int center = active ? list[gi] : 0;
   const int x = center % W, y = center / W;
-  // ---- LDS carve (per wave; arrays indexed by pixel q where another pixel's data is read)
-  float* wl = lds + (size_t)wave * strong_lds_per_wave(P, C, nv);
-  float4* hyp_all = (float4*)wl;                         // [P][5] float4
-  float* pw_all = wl + P * 20;                           // [P][108] patch
-  float* cost_all = wl + P * 128;                        // [P][C + 1][nv]; slot C = the current plane
-  float* sp = wl + P * (128 + (C + 1) * nv) + ps * nv;   // [P][nv]
-  float* ref_all = wl + P * (128 + (C + 2) * nv);        // [P][5][nv] refinement NCCs
-  float* fc = wl + P * (128 + (C + 7) * nv) + ps * 8;    // [P][8]  final costs
-  float* sums_all = wl + P * (136 + (C + 7) * nv);       // [P][4]  patch sums s_ref, s_rr, s_w
-  uint8_t* vwl = (uint8_t*)(wl + P * (140 + (C + 7) * nv)) + ps * 32;   // [P][32] view weights
-  int* ib_all = (int*)(wl + P * (148 + (C + 7) * nv));
-  const int ibs = 2 * C + 17 + nv;                       // ints per pixel
+  // ---- LDS carve (per wave, lds_layout.h; arrays indexed by pixel q where another pixel's data is read)
+  using SC = StrongCarveT<P, C>;
+  float* wl = lds + (size_t)wave * SC::total(nv);
+  float4* hyp_all = (float4*)(wl + SC::hyp());           // [P][5] float4
+  float* pw_all = wl + SC::patch();                      // [P][108] patch
+  float* cost_all = wl + SC::cost(nv);                   // [P][C + 1][nv]; slot C = the current plane
+  float* sp = wl + SC::sp(nv) + ps * nv;                 // [P][nv]
+  float* ref_all = wl + SC::ref(nv);                     // [P][5][nv] refinement NCCs
+  float* fc = wl + SC::fc(nv) + ps * 8;                  // [P][8]  final costs
+  float* sums_all = wl + SC::sums(nv);                   // [P][4]  patch sums s_ref, s_rr, s_w; wnorm
+  uint8_t* vwl = (uint8_t*)(wl + SC::vw(nv)) + ps * 32;  // [P][32] view weights
+  int* ib_all = (int*)(wl + SC::ib(nv));
+  const int ibs = SC::ib_ints(nv);                       // ints per pixel
   int* ib = ib_all + ps * ibs;
-  int* posl = ib;                                        // [C] candidate positions (-1 = none)
-  int* fin = ib + C;                                     // [8] final slot of direction d (-1 = zero vector)
-  int* misc = ib + C + 8;                                // [8] 0: nsel, 1: job slots (candidates + current)
-  int* sel_list = ib + C + 16;                           // [nv]
-  int* slots = ib + C + 16 + nv;                         // [C + 1] cost-vector jobs: candidate slots, then C
-  float4* cpl_all = (float4*)(wl + strong_lds_base(P, C, nv));   // [P][C + 1] candidate planes, slot C = current
-  int* alias_all = (int*)(wl + strong_lds_base(P, C, nv) + P * (C + 1) * 4);   // [P][C + 1]
+  int* posl = ib + SC::IB_POS;                           // [C] candidate positions (-1 = none)
+  int* fin = ib + SC::IB_FIN;                            // [8] final slot of direction d (-1 = zero vector)
+  int* misc = ib + SC::IB_MISC;                          // [8] 0: nsel, 1: job slots (candidates + current)
+  int* sel_list = ib + SC::IB_SEL;                       // [nv]
+  int* slots = ib + SC::ib_slots(nv);                    // [C + 1] cost-vector jobs: candidate slots, then C
+  float4* cpl_all = (float4*)(wl + SC::cpl(nv));         // [P][C + 1] candidate planes, slot C = current
+  int* alias_all = (int*)(wl + SC::alias(nv));           // [P][C + 1]
   float4* cpl = cpl_all + ps * (C + 1);
   int* alias = alias_all + ps * (C + 1);
   float4* hyp = hyp_all + ps * 5;
@@ -435,7 +434,7 @@ __global__ void __launch_bounds__(64 * DPE_BW_STRONG, DPE_TAP_WAVES) k_strong_co
       for (int k = 0; k <= C; ++k) if (alias[k] == k) slots[n++] = k;
       if (fast) patch_lds_pre(pw, sums_all[ps * 4 + 0], sums_all[ps * 4 + 1], sums_all[ps * 4 + 2]);
     }
-    misc[1] = n;
+    misc[SC::MI_JOBS] = n;
   }
   wave_sync();
   PHASE(2);
@@ -444,7 +443,7 @@ __global__ void __launch_bounds__(64 * DPE_BW_STRONG, DPE_TAP_WAVES) k_strong_co
     // view-major order: the lanes of one round gather from the same source image (cache locality)
     int cnt[P], S = 0;
 #pragma unroll
-    for (int q = 0; q < P; ++q) { cnt[q] = ib_all[q * ibs + C + 8 + 1]; S += cnt[q]; }
+    for (int q = 0; q < P; ++q) { cnt[q] = ib_all[q * ibs + SC::IB_MISC + 1]; S += cnt[q]; }
     int q, r;
     const int total = S * nv, tail = total & 63;
     // a last round with at most kTailJobs jobs: each job's 6 patch rows go to 64 / tail lanes (rows
@@ -454,7 +453,7 @@ __global__ void __launch_bounds__(64 * DPE_BW_STRONG, DPE_TAP_WAVES) k_strong_co
     for (int j = lane; j < jend; j += 64) {
       job_decode<P>(cnt, j % S, q, r);
       const int* iq = ib_all + q * ibs;
-      const int slot = iq[C + 16 + nv + r], v = j / S + 1;
+      const int slot = iq[SC::ib_slots(nv) + r], v = j / S + 1;
       const int cq = list[wbase + q];
       const int qx = cq % W, qy = cq / W;
       const float4 pl = cpl_all[q * (C + 1) + slot];
@@ -463,12 +462,12 @@ __global__ void __launch_bounds__(64 * DPE_BW_STRONG, DPE_TAP_WAVES) k_strong_co
           ncc_old_any<U8, DPE_STRONG_ELIDE>(fast, pw_all + q * 108, sm[0], sm[1], sm[2], qx, qy, pc, B, v, pl);
     }
     if (split) {
-      float* tb = wl + strong_lds_per_wave(P, C, nv) - kTailJobs * 18;   // [job][row][3]
+      float* tb = wl + SC::tail(nv);                     // [job][row][3]
       const int rpp = 64 / tail >= 6 ? 1 : 2, npc = 6 / rpp;            // rows per lane, lanes per job
       if (lane < tail * npc) {
         const int j = jend + lane / npc, a0 = (lane % npc) * rpp;
         job_decode<P>(cnt, j % S, q, r);
-        const int slot = ib_all[q * ibs + C + 16 + nv + r], v = j / S + 1;
+        const int slot = ib_all[q * ibs + SC::ib_slots(nv) + r], v = j / S + 1;
         const int cq = list[wbase + q];
         const int qx = cq % W, qy = cq / W;
         const Homog H = make_homography(pc, v, cpl_all[q * (C + 1) + slot]);
@@ -485,7 +484,7 @@ __global__ void __launch_bounds__(64 * DPE_BW_STRONG, DPE_TAP_WAVES) k_strong_co
       if (lane < tail) {
         const int j = jend + lane;
         job_decode<P>(cnt, j % S, q, r);
-        const int slot = ib_all[q * ibs + C + 16 + nv + r], v = j / S + 1;
+        const int slot = ib_all[q * ibs + SC::ib_slots(nv) + r], v = j / S + 1;
         const int cq = list[wbase + q];
         const Homog H = make_homography(pc, v, cpl_all[q * (C + 1) + slot]);
         float cst = 2.0f;
@@ -582,11 +581,11 @@ __global__ void __launch_bounds__(64 * DPE_BW_STRONG, DPE_TAP_WAVES) k_strong_co
       for (int i = 0; i < nv; ++i) if (vwl[i] > 0) { setBit(tsv, i); wnorm += vwl[i]; sel_list[ns++] = i; }
       sums_all[ps * 4 + 3] = wnorm;
     }
-    misc[0] = ns;
+    misc[SC::MI_NSEL] = ns;
   }
   wave_sync();
   PHASE(7);
-  const int nsel = active ? misc[0] : 0;
+  const int nsel = active ? misc[SC::MI_NSEL] : 0;
   // ---- phase 5: final costs of the 8 directions
   if (active && c < 8) {
     float wn = 0.0f;
@@ -638,7 +637,7 @@ __global__ void __launch_bounds__(64 * DPE_BW_STRONG, DPE_TAP_WAVES) k_strong_co
   {
     int cnt[P];
 #pragma unroll
-    for (int q = 0; q < P; ++q) cnt[q] = 5 * ib_all[q * ibs + C + 8];
+    for (int q = 0; q < P; ++q) cnt[q] = 5 * ib_all[q * ibs + SC::IB_MISC];
     int q, r;
     for (int j = lane; job_decode<P>(cnt, j, q, r); j += 64) {
       const int* iq = ib_all + q * ibs;
@@ -646,7 +645,7 @@ __global__ void __launch_bounds__(64 * DPE_BW_STRONG, DPE_TAP_WAVES) k_strong_co
       const int cq = list[wbase + q];
       const float* sm = sums_all + q * 4;
       ref_all[(q * 5 + h) * nv + k] = ncc_old_any<U8, DPE_STRONG_ELIDE>(fast, pw_all + q * 108, sm[0], sm[1], sm[2], cq % W, cq / W, pc,
-                                                      B, iq[C + 16 + k] + 1, hyp_all[q * 5 + h]);
+                                                      B, iq[SC::IB_SEL + k] + 1, hyp_all[q * 5 + h]);
     }
   }
   wave_sync();
@@ -659,14 +658,14 @@ __global__ void __launch_bounds__(64 * DPE_BW_STRONG, DPE_TAP_WAVES) k_strong_co
     for (int k = 0; k < nsel; ++k) tc += vwl[sel_list[k]] * ref[h * nv + k];
     tc /= sums_all[ps * 4 + 3];
     fc[h] = tc;
-    misc[2 + h] = __float_as_int(depth_from_plane(c0, hyp[h], x, y));
+    misc[SC::MI_DEPTH + h] = __float_as_int(depth_from_plane(c0, hyp[h], x, y));
   }
   wave_sync();
   PHASE(13);
   if (active && c == 0) {
     const float dmin = pc.P.depth_min, dmax = pc.P.depth_max;
     for (int h = 0; h < 5; ++h) {
-      const float tc = fc[h], db = __int_as_float(misc[2 + h]);
+      const float tc = fc[h], db = __int_as_float(misc[SC::MI_DEPTH + h]);
       if (db >= dmin && db <= dmax && tc < cost_now) { depth_now = db; pnow = hyp[h]; cost_now = tc; }
     }
     if (pc.P.state == DPE_REFINE_INIT) {
@@ -918,10 +917,12 @@ DEV float ncc_new_tab(const PassConst& pc, const DevBufs& B, const WeakTab& T, i
 #ifndef DPE_WEAK_POOL
 #define DPE_WEAK_POOL 1
 #endif
-// LDS floats per weak pixel (fixed part kWeakFixed, see the carve in k_weak_coop); multiple of 4.
-// At 9 source views a pixel takes 636 floats, so four 4-wave workgroups (4 x 40.7 KB) fit a CU's LDS.
-constexpr int kWeakFixed = 480;
-__host__ __device__ inline int weak_lds_per_pixel(int nv) { return (kWeakFixed + 17 * nv + 3) & ~3; }
+// LDS floats per weak pixel (lds_layout.h WeakCarve: fixed part, then [8][nv] costs, [nv] sampling
+// probabilities, [nv] selected views, [7][nv] hypothesis values; multiple of 4).  At 9 source views a
+// pixel takes 636 floats, so four 4-wave workgroups (4 x 40.7 KB) fit a CU's LDS.
+using WC = lds::WeakCarve;
+constexpr int kWeakFixed = WC::FIXED;
+__host__ __device__ inline int weak_lds_per_pixel(int nv) { return WC::per_pixel(nv); }
 
 // CheckerboardPropagationWeak (DPE.cu:1668-1862) + PlaneHypothesisRefinementWeak (:1120-1212).
 // C lanes per pixel, 64/C pixels per wave, blockDim.x/64 waves per workgroup.
@@ -947,29 +948,28 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
   const bool active = gi < nlist;
   const int center = active ? list[gi] : 0;
   const int x = center % W, y = center / W;
-  // ---- LDS carve (per pixel, floats)
+  // ---- LDS carve (per pixel, floats; lds_layout.h WeakCarve)
   const int S = weak_lds_per_pixel(nv);
   float* pb = (float*)lds4 + (size_t)(wave * P + ps) * S;
-  float* pw = pb;                                        // [108] Old-NCC patch (patch_lds_build)
-  float* tcp = pb + 108;                                 // centre patch table, pairs [36][2]
-  float* tnp = pb + 180;                                 // neighbour patch tables, pairs [8][9][2]
-  float* sums = pb + 324;                                // [9][3]
-  float* osum = pb + 352;                                // [3] Old-NCC patch sums
-  float4* cpl = (float4*)(pb + 356);                     // [8] candidate planes
-  float4* hyp = (float4*)(pb + 388);                     // [7] refinement hypotheses / final plane
-  float* fc = pb + 416;                                  // [8] final candidate costs
-  int* misc = (int*)(pb + 424);                          // 0 nsel, 1..3 + 6 header, 4 wnorm, 5 candidate mask, 8..15 flags
-  short2* nbl = (short2*)(pb + 440);                     // [9]
-  uint32_t* nsv = (uint32_t*)(pb + 452);                 // [9]
-  int* alias = (int*)(pb + 464);                         // [8] earlier row with a bitwise-identical plane
-  uint8_t* vwl = (uint8_t*)(pb + 472);                   // [32] view weights
-  // the pixel's header, read by the lanes of other pixels in the pooled phases, sits in free slots
-  // of the carve: misc[1] rad_c, misc[2] inc_c, misc[3] n_c, misc[6] nb3; nbox at [449..451], [461];
-  // grey level at [351]; fit plane in hyp[6]
-  float* cost = pb + kWeakFixed;                         // [8][nv]
-  float* sp = cost + 8 * nv;                             // [nv]
-  int* sel_list = (int*)(sp + nv);                       // [nv]
-  float* hv = (float*)(sel_list + nv);                   // [7][nv] hypothesis x selected-view values
+  float* pw = pb + WC::PW;                               // [108] Old-NCC patch (patch_lds_build)
+  float* tcp = pb + WC::TC;                              // centre patch table, pairs [36][2]
+  float* tnp = pb + WC::TN;                              // neighbour patch tables, pairs [8][9][2]
+  float* sums = pb + WC::SUMS;                           // [9][3]
+  float* osum = pb + WC::OSUM;                           // [3] Old-NCC patch sums
+  float4* cpl = (float4*)(pb + WC::CPL);                 // [8] candidate planes
+  float4* hyp = (float4*)(pb + WC::HYP);                 // [7] refinement hypotheses / final plane
+  float* fc = pb + WC::FC;                               // [8] final candidate costs
+  int* misc = (int*)(pb + WC::MISC);                     // WC::M_* slots (nsel, header, wnorm, candidate mask, flags)
+  short2* nbl = (short2*)(pb + WC::NBL);                 // [9]
+  uint32_t* nsv = (uint32_t*)(pb + WC::NSV);             // [9]
+  int* alias = (int*)(pb + WC::ALIAS);                   // [8] earlier row with a bitwise-identical plane
+  uint8_t* vwl = (uint8_t*)(pb + WC::VWL);               // [32] view weights
+  // the pixel's header, read by the lanes of other pixels in the pooled phases: misc[M_RADC / M_INCC /
+  // M_NC / M_NB3], the grey level at RC, nbox at NBOX_A[0..2] and NBOX_B; fit plane in hyp[6]
+  float* cost = pb + WC::cost(nv);                       // [8][nv]
+  float* sp = pb + WC::sp(nv);                           // [nv]
+  int* sel_list = (int*)(pb + WC::sel(nv));              // [nv]
+  float* hv = pb + WC::hv(nv);                           // [7][nv] hypothesis x selected-view values
 
   const bool geom = pc.P.geom_consistency;
   const float gf = pc.P.geom_factor;
@@ -991,15 +991,15 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
   auto pix = [&](int q) -> float* { return (float*)lds4 + (size_t)(wave * P + q) * S; };
   auto tab_of = [&](int q) -> WeakTab {
     const float* qb = pix(q);
-    const int* h = (const int*)(qb + 424);
+    const int* h = (const int*)(qb + WC::MISC);
     WeakTab t;
-    t.rad_c = h[1]; t.inc_c = h[2]; t.n_c = h[3]; t.nb3 = h[6] != 0;
+    t.rad_c = h[WC::M_RADC]; t.inc_c = h[WC::M_INCC]; t.n_c = h[WC::M_NC]; t.nb3 = h[WC::M_NB3] != 0;
     t.rad_n = T.rad_n; t.inc_n = T.inc_n; t.n_n = T.n_n; t.tab_n = T.tab_n;
     t.tab_c = t.n_c >= 1 && t.n_c <= 6;
-    t.rc = qb[351];
-    t.nbox[0] = qb[449]; t.nbox[1] = qb[450]; t.nbox[2] = qb[451]; t.nbox[3] = qb[461];
-    t.tc = qb + 108; t.tn = qb + 180; t.sums = qb + 324;
-    t.nbl = (const short2*)(qb + 440); t.nsv = (const uint32_t*)(qb + 452);
+    t.rc = qb[WC::RC];
+    t.nbox[0] = qb[WC::NBOX_A]; t.nbox[1] = qb[WC::NBOX_A + 1]; t.nbox[2] = qb[WC::NBOX_A + 2]; t.nbox[3] = qb[WC::NBOX_B];
+    t.tc = qb + WC::TC; t.tn = qb + WC::TN; t.sums = qb + WC::SUMS;
+    t.nbl = (const short2*)(qb + WC::NBL); t.nsv = (const uint32_t*)(qb + WC::NSV);
     return t;
   };
   int pcnt[P];
@@ -1031,7 +1031,7 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
     for (int i = c; i < 8; i += C) {
       const short2 np = nbg[i + 1];
       const bool fl = !(np.x == -1 || np.y == -1) && B.weak[np.x + np.y * W] == DPE_STRONG;
-      misc[8 + i] = fl ? 1 : 0;
+      misc[WC::M_FLAGS + i] = fl ? 1 : 0;
       if (fl) cpl[i] = B.planes[np.x + np.y * W];
       else for (int v = 0; v < nv; ++v) cost[i * nv + v] = (i == 0 && v == 0) ? 2.0f : 0.0f;
     }
@@ -1056,9 +1056,9 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
   // ---- phase 1b: reference sums of every tabulated patch (tap order of patch_ncc_generic)
   if (active) {
     if (c == C - 2) {
-      misc[1] = T.rad_c; misc[2] = T.inc_c; misc[3] = T.n_c; misc[6] = T.nb3 ? 1 : 0;
-      pb[449] = T.nbox[0]; pb[450] = T.nbox[1]; pb[451] = T.nbox[2]; pb[461] = T.nbox[3];
-      pb[351] = T.rc;
+      misc[WC::M_RADC] = T.rad_c; misc[WC::M_INCC] = T.inc_c; misc[WC::M_NC] = T.n_c; misc[WC::M_NB3] = T.nb3 ? 1 : 0;
+      pb[WC::NBOX_A] = T.nbox[0]; pb[WC::NBOX_A + 1] = T.nbox[1]; pb[WC::NBOX_A + 2] = T.nbox[2]; pb[WC::NBOX_B] = T.nbox[3];
+      pb[WC::RC] = T.rc;
     }
     for (int k = c; k < 9; k += C) {
       const short2 np = nbl[k];
@@ -1084,10 +1084,10 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
     // with the same plane (lanes 8..15; lanes 0..8 build the sums above)
     for (int i = c - 8; i >= 0 && i < 8; i += C) {
       int a = i;
-      if (misc[8 + i]) {
+      if (misc[WC::M_FLAGS + i]) {
         const float4 me = cpl[i];
         for (int t = 0; t < i; ++t)
-          if (misc[8 + t] && __float_as_uint(cpl[t].x) == __float_as_uint(me.x) &&
+          if (misc[WC::M_FLAGS + t] && __float_as_uint(cpl[t].x) == __float_as_uint(me.x) &&
               __float_as_uint(cpl[t].y) == __float_as_uint(me.y) && __float_as_uint(cpl[t].z) == __float_as_uint(me.z) &&
               __float_as_uint(cpl[t].w) == __float_as_uint(me.w)) { a = t; break; }
       }
@@ -1100,8 +1100,8 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
 #if DPE_WEAK_POOL
   if (active && c == 0) {
     uint32_t um = 0;
-    for (int i = 0; i < 8; ++i) if (misc[8 + i] && alias[i] == i) um |= 1u << i;
-    misc[5] = (int)um;
+    for (int i = 0; i < 8; ++i) if (misc[WC::M_FLAGS + i] && alias[i] == i) um |= 1u << i;
+    misc[WC::M_CMASK] = (int)um;
   }
   wave_sync();
   {
@@ -1117,17 +1117,17 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
       job_decode<P>(pcnt, j % Sj, q, r);
       const int v = j / Sj + 1;
       float* qb = pix(q);
-      uint32_t m = (uint32_t)((const int*)(qb + 424))[5];
+      uint32_t m = (uint32_t)((const int*)(qb + WC::MISC))[WC::M_CMASK];
       for (; r > 0; --r) m &= m - 1;
       const int i = __builtin_ctz(m);
       const int cq = list[wbase + q];
-      (qb + kWeakFixed)[i * nv + v - 1] = ncc_new_tab<U8>(pc, B, tab_of(q), cq % W, cq / W, v, ((const float4*)(qb + 356))[i]);
+      (qb + WC::cost(nv))[i * nv + v - 1] = ncc_new_tab<U8>(pc, B, tab_of(q), cq % W, cq / W, v, ((const float4*)(qb + WC::CPL))[i]);
     }
   }
 #else
   if (active) {
     uint32_t um = 0;
-    for (int i = 0; i < 8; ++i) if (misc[8 + i] && alias[i] == i) um |= 1u << i;
+    for (int i = 0; i < 8; ++i) if (misc[WC::M_FLAGS + i] && alias[i] == i) um |= 1u << i;
     const int ncand = __builtin_popcount(um);
     for (int j = c; j < ncand * nv; j += C) {
       uint32_t m = um;
@@ -1146,7 +1146,7 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
   PHASE(2);
   if (active)
     for (int i = c; i < 8; i += C)
-      if (misc[8 + i] && alias[i] != i)
+      if (misc[WC::M_FLAGS + i] && alias[i] != i)
         for (int v = 0; v < nv; ++v) cost[i * nv + v] = cost[alias[i] * nv + v];
   wave_sync();
   PHASE(3);
@@ -1174,16 +1174,16 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
     rng_seek(rs, 15);
     int ns = 0;
     for (int i = 0; i < nv; ++i) if (vwl[i] > 0) { setBit(tsv, i); wnorm += vwl[i]; sel_list[ns++] = i; }
-    misc[0] = ns;
-    misc[4] = __float_as_int(wnorm);
+    misc[WC::M_NSEL] = ns;
+    misc[WC::M_WNORM] = __float_as_int(wnorm);
 #if DPE_WEAK_POOL
     hyp[6] = B.fit_plane[center];
 #endif
   }
   wave_sync();
   PHASE(5);
-  const int nsel = active ? misc[0] : 0;
-  const float wn = active ? __int_as_float(misc[4]) : 1.0f;
+  const int nsel = active ? misc[WC::M_NSEL] : 0;
+  const float wn = active ? __int_as_float(misc[WC::M_WNORM]) : 1.0f;
   const float4 cur = active ? B.planes[center] : make_float4(0, 0, 0, 1);
   const float4 fp = active ? B.fit_plane[center] : make_float4(0, 0, 0, 0);
   const bool has_fit = !(fp.x == 0 && fp.y == 0 && fp.z == 0);
@@ -1211,10 +1211,10 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
     int q, r;
     for (int j = lane; job_decode<P>(pcnt, j, q, r); j += 64) {
       float* qb = pix(q);
-      const int ns = ((const int*)(qb + 424))[0];
+      const int ns = ((const int*)(qb + WC::MISC))[WC::M_NSEL];
       const int h = r / ns, k = r % ns;
-      const int v = ((const int*)(qb + kWeakFixed + 9 * nv))[k] + 1;
-      (qb + kWeakFixed + 10 * nv)[h * nv + k] = hyp_val_q(q, v, h ? ((const float4*)(qb + 388))[6] : B.planes[list[wbase + q]]);
+      const int v = ((const int*)(qb + WC::sel(nv)))[k] + 1;
+      (qb + WC::hv(nv))[h * nv + k] = hyp_val_q(q, v, h ? ((const float4*)(qb + WC::HYP))[6] : B.planes[list[wbase + q]]);
     }
   }
   if (active) {
@@ -1227,7 +1227,7 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
     }
 #endif
     for (int i = c; i < 8; i += C) {
-      const bool fl = misc[8 + i] != 0;
+      const bool fl = misc[WC::M_FLAGS + i] != 0;
       const float3 fwi = (geom && fl) ? geom_point(pc, x, y, cpl[i]) : make_float3(0.0f, 0.0f, 0.0f);
       float f = 0.0f;
       for (int j = 0; j < nv; ++j) {
@@ -1257,7 +1257,7 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
     cost_now /= wnorm;
     cost_written = cost_now;
     depth_now = depth_from_plane(c0, cur, x, y);
-    if (misc[8 + mi]) {
+    if (misc[WC::M_FLAGS + mi]) {
       const float4 cand_pl = cpl[mi];
       const float db = depth_from_plane(c0, cand_pl, x, y);
       if (db >= dmin && db <= dmax && fc[mi] < cost_now) {
@@ -1294,10 +1294,10 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
     int q, r;
     for (int j = lane; job_decode<P>(pcnt, j, q, r); j += 64) {
       float* qb = pix(q);
-      const int ns = ((const int*)(qb + 424))[0];
+      const int ns = ((const int*)(qb + WC::MISC))[WC::M_NSEL];
       const int h = r / ns, k = r % ns;
-      const int v = ((const int*)(qb + kWeakFixed + 9 * nv))[k] + 1;
-      (qb + kWeakFixed + 10 * nv)[(2 + h) * nv + k] = hyp_val_q(q, v, ((const float4*)(qb + 388))[h]);
+      const int v = ((const int*)(qb + WC::sel(nv)))[k] + 1;
+      (qb + WC::hv(nv))[(2 + h) * nv + k] = hyp_val_q(q, v, ((const float4*)(qb + WC::HYP))[h]);
     }
   }
   if (false) {
@@ -1343,9 +1343,9 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
     for (int j = lane; job_decode<P>(pcnt, j, q, r); j += 64) {
       float* qb = pix(q);
       const int cq = list[wbase + q];
-      const int v = ((const int*)(qb + kWeakFixed + 9 * nv))[r] + 1;
-      (qb + kWeakFixed + 10 * nv)[r] = ncc_old_any<U8, true>(fast_old, qb, qb[352], qb[353], qb[354], cq % W, cq / W, pc, B, v,
-                                                      ((const float4*)(qb + 388))[5]);
+      const int v = ((const int*)(qb + WC::sel(nv)))[r] + 1;
+      (qb + WC::hv(nv))[r] = ncc_old_any<U8, true>(fast_old, qb + WC::PW, qb[WC::OSUM], qb[WC::OSUM + 1], qb[WC::OSUM + 2], cq % W,
+                                                   cq / W, pc, B, v, ((const float4*)(qb + WC::HYP))[5]);
     }
   }
   if (false) {

@@ -47,8 +47,10 @@ constexpr int kTexD2W = DPE_TEX_D2W, kTexLR = DPE_TEX_LR;
 // else 8 x 8); the grid and dynamic LDS are the caller's (strong_lds_per_wave).
 void launch_strong(bool edge, bool img8, unsigned grid, size_t lds, hipStream_t s, const PassConst* dpc,
                    const DevBufs& B, int it, const int* list, const int* count);
-// DepthToWeak over the L pixels of the pass (one wave per pixel)
+// DepthToWeak over the L pixels of the pass (one wave per pixel), with LocalRefine fused into its
+// epilogue for interior pixels when DPE_FUSE_LR (default)
 void launch_depth_to_weak(bool img8, long L, hipStream_t s, const PassConst* dpc, const DevBufs& B);
-// LocalRefine over the L pixels (kLrPix pixels per wave), nv source views
-void launch_local_refine(bool img8, long L, int nv, hipStream_t s, const PassConst* dpc, const DevBufs& B);
+// LocalRefine (kLrPix pixels per wave), nv source views: over the L = W x H pixels, or with the
+// fused DepthToWeak (DPE_FUSE_LR) over the border pixels it leaves
+void launch_local_refine(bool img8, long L, int W, int H, int nv, hipStream_t s, const PassConst* dpc, const DevBufs& B);
 }  // namespace dpe

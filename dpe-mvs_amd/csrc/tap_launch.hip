@@ -40,12 +40,17 @@ void launch_strong(bool edge, bool img8, unsigned grid, size_t lds, hipStream_t 
 
 void launch_depth_to_weak(bool img8, long L, hipStream_t s, const PassConst* dpc, const DevBufs& B) {
   const unsigned g = (unsigned)((L + DPE_BW_D2W - 1) / DPE_BW_D2W);
-  if (img8) k_depth_to_weak<kTexD2W><<<g, 64 * DPE_BW_D2W, 0, s>>>(dpc, B);
-  else k_depth_to_weak<TEX_F32><<<g, 64 * DPE_BW_D2W, 0, s>>>(dpc, B);
+  constexpr bool LR = DPE_FUSE_LR != 0;
+  if (img8) k_depth_to_weak<kTexD2W, LR><<<g, 64 * DPE_BW_D2W, 0, s>>>(dpc, B);
+  else k_depth_to_weak<TEX_F32, LR><<<g, 64 * DPE_BW_D2W, 0, s>>>(dpc, B);
 }
 
-void launch_local_refine(bool img8, long L, int nv, hipStream_t s, const PassConst* dpc, const DevBufs& B) {
+void launch_local_refine(bool img8, long L, int W, int H, int nv, hipStream_t s, const PassConst* dpc, const DevBufs& B) {
+  // with the fused DepthToWeak only its border pixels are left
+  const int border = DPE_FUSE_LR ? 1 : 0;
+  if (border) L = border_count(W, H);
   const unsigned g = (unsigned)((L + DPE_BW_LR * kLrPix - 1) / (DPE_BW_LR * kLrPix));
+  if (g == 0) return;
   const size_t lds = (size_t)DPE_BW_LR * kLrPix * 12 * nv * 2 * sizeof(float);
   if (lds > 65536) {
     static bool once = false;
@@ -55,8 +60,8 @@ void launch_local_refine(bool img8, long L, int nv, hipStream_t s, const PassCon
       (void)hipFuncSetAttribute((const void*)k_local_refine_jobs<TEX_F32>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     }
   }
-  if (img8) k_local_refine_jobs<kTexLR><<<g, 64 * DPE_BW_LR, lds, s>>>(dpc, B);
-  else k_local_refine_jobs<TEX_F32><<<g, 64 * DPE_BW_LR, lds, s>>>(dpc, B);
+  if (img8) k_local_refine_jobs<kTexLR><<<g, 64 * DPE_BW_LR, lds, s>>>(dpc, B, border);
+  else k_local_refine_jobs<TEX_F32><<<g, 64 * DPE_BW_LR, lds, s>>>(dpc, B, border);
 }
 
 }  // namespace dpe

@@ -1,8 +1,12 @@
 // bindings.cpp — the `DPE_MVS._dpe` pybind11 module: `dpe_mvs(...)` with the signature and error
 // behaviour of the reference's binding (csrc/bindings.cpp:31-43): returns 0, raises RuntimeError
 // on a nonzero pipeline result.  The pipeline itself is libdpe_host (C++), the GIL is released
-// while it runs.
+// while it runs.  std::cout / std::cerr go to Python's sys.stdout / sys.stderr as in the reference
+// (csrc/bindings.cpp:23-24); pybind's pythonbuf takes the GIL back on each flush.
+#include <pybind11/iostream.h>
 #include <pybind11/pybind11.h>
+
+#include <iostream>
 
 #include <stdexcept>
 #include <string>
@@ -18,6 +22,8 @@ static int dpe_mvs(const std::string& dense_folder, int gpu_index, bool verbose,
   o.gpu_index = gpu_index;
   o.verbose = verbose; o.fusion = fusion; o.viz = viz;
   o.depth = depth; o.normal = normal; o.weak = weak; o.edge = edge;
+  py::scoped_ostream_redirect out(std::cout);
+  py::scoped_ostream_redirect err(std::cerr, py::module_::import("sys").attr("stderr"));
   int rc;
   {
     py::gil_scoped_release release;

@@ -18,6 +18,7 @@
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -34,24 +35,29 @@ namespace {
 struct Rccl {
   ncclComm_t comm = nullptr;
   hipStream_t stream = nullptr;
-  float* dsend = nullptr;
+  float* dsend = nullptr;   // host all-gather staging, kStageFloats per rank
   float* drecv = nullptr;
-  size_t cap = 0;
   int world = 1;
 };
 
+// Host buffers (the per-exchange status flags, the runner-hook path, fusion's one-off exchange).
+// Every call enters the same collectives on every rank whatever fails locally, so a peer is never
+// left waiting in ncclAllGather: the staging buffers are allocated once at start-up (rccl_init,
+// before the rendezvous) and a count beyond them goes in chunks of that fixed size, which every
+// rank derives the same way.
+constexpr size_t kStageFloats = 1u << 20;   // 4 MB send + world x 4 MB receive
 int rccl_allgather(void* user, const float* send, size_t count, float* recv) {
   Rccl* r = static_cast<Rccl*>(user);
-  if (count > r->cap) {
-    if (r->dsend) { (void)hipFree(r->dsend); (void)hipFree(r->drecv); }
-    if (hipMalloc(&r->dsend, count * sizeof(float)) != hipSuccess) return -1;
-    if (hipMalloc(&r->drecv, count * sizeof(float) * r->world) != hipSuccess) return -1;
-    r->cap = count;
+  bool ok = true;
+  for (size_t off = 0; off < count; off += kStageFloats) {
+    const size_t n = std::min(kStageFloats, count - off);
+    ok = hipMemcpyAsync(r->dsend, send + off, n * sizeof(float), hipMemcpyHostToDevice, r->stream) == hipSuccess && ok;
+    ok = ncclAllGather(r->dsend, r->drecv, n, ncclFloat, r->comm, r->stream) == ncclSuccess && ok;
+    ok = hipMemcpy2DAsync(recv + off, count * sizeof(float), r->drecv, n * sizeof(float), n * sizeof(float), r->world,
+                          hipMemcpyDeviceToHost, r->stream) == hipSuccess && ok;
+    ok = hipStreamSynchronize(r->stream) == hipSuccess && ok;
   }
-  if (hipMemcpyAsync(r->dsend, send, count * sizeof(float), hipMemcpyHostToDevice, r->stream) != hipSuccess) return -1;
-  if (ncclAllGather(r->dsend, r->drecv, count, ncclFloat, r->comm, r->stream) != ncclSuccess) return -1;
-  if (hipMemcpyAsync(recv, r->drecv, count * sizeof(float) * r->world, hipMemcpyDeviceToHost, r->stream) != hipSuccess) return -1;
-  return hipStreamSynchronize(r->stream) == hipSuccess ? 0 : -1;
+  return ok ? 0 : -1;
 }
 
 // device buffers on both sides: the depth maps go from HBM to HBM over xGMI with no host copy
@@ -64,6 +70,9 @@ int rccl_allgather_dev(void* user, const float* dsend, size_t count, float* drec
 bool rccl_init(Rccl& r, int rank, int world, int device) {
   r.world = world;
   if (hipSetDevice(device) != hipSuccess) return false;
+  // the host all-gather's staging buffers, before any rank commits to a collective
+  if (hipMalloc(&r.dsend, kStageFloats * sizeof(float)) != hipSuccess) return false;
+  if (hipMalloc(&r.drecv, kStageFloats * sizeof(float) * world) != hipSuccess) return false;
   ncclUniqueId id;
   std::memset(&id, 0, sizeof(id));
   if (rank == 0 && ncclGetUniqueId(&id) != ncclSuccess) return false;

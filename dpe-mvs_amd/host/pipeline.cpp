@@ -26,10 +26,12 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <filesystem>
 #include <fstream>
+#include <iostream>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -436,7 +438,7 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
     }
     const int nt = (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
     std::string perr;
-    if (!cache.prefetch(ids, nt, perr)) { err = "Images may error, check it! " + perr; std::fprintf(stderr, "Images may error, check it!\n"); return 1; }
+    if (!cache.prefetch(ids, nt, perr)) { err = "Images may error, check it! " + perr; std::cerr << "Images may error, check it!\n"; return 1; }
   }
   {   // CheckImages (main.cpp:310-329)
     int w0 = 0, h0 = 0;
@@ -447,7 +449,7 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
       else if (i == 0) { w0 = w; h0 = h; }
       else if (w != w0 || h != h0) ok = false;
     }
-    if (!ok) { err = "Images may error, check it! " + err; std::fprintf(stderr, "Images may error, check it!\n"); return 1; }
+    if (!ok) { err = "Images may error, check it! " + err; std::cerr << "Images may error, check it!\n"; return 1; }
   }
   const int n = (int)problems.size();
   // every rank reads the same pair.txt, so every rank takes this exit together (no collective yet)
@@ -483,6 +485,31 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
     }
     return true;
   };
+  // the ranks' failure flags, one float each over the host hook; false (err set) when any rank failed
+  auto status_exchange = [&]() -> bool {
+    float flag = failed ? 1.0f : 0.0f;
+    std::vector<float> all(world, 0.0f);
+    if (opt.allgather(opt.allgather_user, &flag, 1, all.data()) != 0) { err = "all-gather failed"; return false; }
+    for (int r = 0; r < world; ++r)
+      if (all[r] != 0.0f) { err = r == rank ? first_err : "rank " + std::to_string(r) + " failed"; return false; }
+    return true;
+  };
+  // DPE_FAULT_INJECT="before:R" / "after:R" (tests): rank R fails locally just before / after the
+  // first resident depth exchange's collectives
+  static const std::pair<int, int> fault = [] {
+    const char* e = std::getenv("DPE_FAULT_INJECT");
+    if (!e) return std::make_pair(-1, -1);
+    const std::string v(e);
+    const size_t c = v.find(':');
+    if (c == std::string::npos) return std::make_pair(-1, -1);
+    return std::make_pair(v.compare(0, c, "before") == 0 ? 0 : (v.compare(0, c, "after") == 0 ? 1 : -1), std::atoi(v.c_str() + c + 1));
+  }();
+  bool fault_done = false;
+  auto fault_at = [&](int when, int r) -> bool {
+    if (fault_done || fault.first != when || fault.second != r) return false;
+    fault_done = true;
+    return true;
+  };
   Runner runner;
   if (opt.runner) { runner.fn = opt.runner; runner.user = opt.runner_user; }
   else {
@@ -497,9 +524,10 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
   while (max_size > 800) { max_size /= 2; round_num++; }
   round_num = std::max(round_num, 2);
   if (opt.verbose && rank == 0) {
-    std::printf("There are %d images to be processed!\n", n);
-    std::printf("There are %d resolution stages for coarse-to-fine processing!\n", round_num);
-    std::printf("Iteration nums: %d\n", round_num * 4);
+    // std::cout as main.cpp:489, 504 (the pybind module redirects it into sys.stdout)
+    std::cout << "There are " << n << " images to be processed!" << std::endl;
+    std::cout << "There are " << round_num << " resolution stages for coarse-to-fine processing!" << std::endl;
+    std::cout << "Iteration nums: " << round_num * 4 << std::endl;
   }
   g_times[1] = now_s() - t_mark;
   t_mark = now_s();
@@ -577,13 +605,17 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
       }
       if (world == 1 && failed) { err = first_err; return 1; }
       if (world > 1 && resident) {   // all-gather of the depth maps from / into the HBM-resident states
-        // Every rank joins the collective with the same count (nmax maps + a status float) whatever
-        // happened locally: a local error sets the status float and the rank sends from a host
-        // buffer through the host hook (the hooks are the same all-gather, so it matches the others'
-        // device-hook call), and every rank then fails together at this exchange.
+        // Two collectives per exchange, both joined by every rank whatever happened locally:
+        //  1. the ranks' status flags over the host hook (one float each).  A local error before it
+        //     (the pass, the exchange buffers, the export) raises the flag and every rank returns 1
+        //     at this exchange;
+        //  2. the depth maps (nmax maps per rank), device to device, or one device -> host -> device
+        //     hop through the host hook.  An error after (1) can no longer stop the others, who are
+        //     committed to (2): the rank still joins (2), records the error and reports it at the
+        //     next exchange's (1) or at the final status exchange after the passes.
         size_t nmax = 0;
         for (auto& b : blocks) nmax = std::max(nmax, b.size());
-        const size_t per = (size_t)pw * ph, cnt = nmax * per + 1;   // + the status float
+        const size_t per = (size_t)pw * ph, cnt = nmax * per;
         float* dsend = dpe_device_buffer(runner.ctx, 0, cnt);
         float* drecv = dsend ? dpe_device_buffer(runner.ctx, 1, cnt * world) : nullptr;
         bool dev_ok = drecv != nullptr;
@@ -591,43 +623,24 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
         for (size_t k = 0; dev_ok && !failed && k < blocks[rank].size(); ++k)
           if (dpe_state_export_depth(runner.ctx, problems[blocks[rank][k]].ref_image_id, dsend + k * per, nullptr) != 0)
             fail(dpe_last_error());
-        float flag = failed ? 1.0f : 0.0f;
-        if (dev_ok && dpe_device_copy(runner.ctx, dsend + nmax * per, &flag, sizeof(float), 0) != 0) {
-          fail(dpe_last_error());
-          dev_ok = false;
-        }
-        std::vector<float> status(world, 0.0f), hr;
-        if (dev_ok && opt.allgather_device) {
+        if (fault_at(0, rank)) fail("injected fault before the exchange");
+        if (!status_exchange()) return 1;
+        if (opt.allgather_device) {
           if (opt.allgather_device(opt.allgather_device_user, dsend, cnt, drecv) != 0) { err = "all-gather failed"; return 1; }
-          for (int r = 0; r < world; ++r)
-            if (dpe_device_copy(runner.ctx, &status[r], drecv + (size_t)r * cnt + nmax * per, sizeof(float), 1) != 0) {
-              fail(dpe_last_error());   // the collective itself completed: every rank is past it
-              status[r] = 1.0f;
-            }
-        } else {   // host hook: one device -> host -> device hop of the packed maps (or a failure flag)
-          std::vector<float> hs(cnt, 0.0f);
-          if (dev_ok && dpe_device_copy(runner.ctx, hs.data(), dsend, cnt * sizeof(float), 1) != 0) {
-            fail(dpe_last_error());
-            dev_ok = false;
-          }
-          if (failed) hs[nmax * per] = 1.0f;
-          hr.assign(cnt * world, 0.0f);
+        } else {   // host hook: one device -> host -> device hop of the packed maps
+          std::vector<float> hs(cnt, 0.0f), hr(cnt * world, 0.0f);
+          if (dpe_device_copy(runner.ctx, hs.data(), dsend, cnt * sizeof(float), 1) != 0) fail(dpe_last_error());
           if (opt.allgather(opt.allgather_user, hs.data(), cnt, hr.data()) != 0) { err = "all-gather failed"; return 1; }
-          for (int r = 0; r < world; ++r) status[r] = hr[(size_t)r * cnt + nmax * per];
-          if (dev_ok && !failed && dpe_device_copy(runner.ctx, drecv, hr.data(), hr.size() * sizeof(float), 0) != 0) {
+          if (!failed && dpe_device_copy(runner.ctx, drecv, hr.data(), hr.size() * sizeof(float), 0) != 0)
             fail(dpe_last_error());
-          }
         }
-        int bad = -1;
-        for (int r = 0; r < world; ++r) if (bad < 0 && status[r] != 0.0f) bad = r;
-        if (bad < 0 && failed) bad = rank;   // a local error after the collective
-        if (bad >= 0) { err = bad == rank ? first_err : "rank " + std::to_string(bad) + " failed"; return 1; }
+        if (fault_at(1, rank)) fail("injected fault after the exchange");
         for (int r = 0; r < world; ++r) {
           if (r == rank) continue;
           for (size_t k = 0; k < blocks[r].size(); ++k)
             if (!failed && dpe_state_import_depth(runner.ctx, problems[blocks[r][k]].ref_image_id, pw, ph,
                                                   drecv + (size_t)r * cnt + k * per, nullptr) != 0)
-              fail(dpe_last_error());   // reported at the next exchange (or the end): the others are past this one
+              fail(dpe_last_error());   // reported at the next exchange's status step
         }
       } else if (world > 1) {   // all-gather of the depth maps (the pass's only cross-image data)
         size_t nmax = 0;
@@ -645,7 +658,7 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
             depth_cur[problems[blocks[r][k]].ref_image_id] = DepthMap{pw, ph, std::vector<float>(src, src + per)};
           }
       }
-      if (opt.verbose && rank == 0) std::printf("Iteration %d / %d done\n", iteration_index + 1, round_num * 4);
+      if (opt.verbose && rank == 0) std::cout << "Iteration " << iteration_index + 1 << " / " << round_num * 4 << " done" << std::endl;
       iteration_index++;
     }
   }
@@ -671,7 +684,10 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
     for (auto& th : pool) th.join();
     for (auto& e : werr) if (!e.empty()) { fail(e); break; }
   }
-  if (failed && !(world > 1 && opt.fusion)) { err = first_err; return 1; }   // else reported at the exchange
+  // every rank learns here whether any rank failed after its last exchange (a rank returning alone
+  // would leave the others' next collective, or their success, inconsistent with it)
+  if (world > 1 && !status_exchange()) return 1;
+  if (failed) { err = first_err; return 1; }
   if (opt.fusion) {   // RunFusion (main.cpp:578-580)
     std::map<int, ImageState> all;
     for (int pi : blocks[rank]) all[problems[pi].ref_image_id] = states[problems[pi].ref_image_id];
@@ -765,7 +781,7 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
         return 1;
       }
       if (!export_point_cloud((fs::path(dense) / kOutName / "DPE.ply").string(), cloud, err)) return 1;
-      if (opt.verbose) std::printf("Fused %zu points\n", cloud.size());
+      if (opt.verbose) std::cout << "Fused " << cloud.size() << " points" << std::endl;
     }
   }
   if (!opt.keep_intermediate)   // the reference's clean-up (main.cpp:581-595)
@@ -775,7 +791,7 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
         fs::remove(fs::path(problems[pi].result_folder) / ("edges_" + std::to_string(j) + ".dmb"), ec2);
         fs::remove(fs::path(problems[pi].result_folder) / ("labels_" + std::to_string(j) + ".dmb"), ec2);
       }
-  if (opt.verbose && rank == 0) std::printf("All done\n");
+  if (opt.verbose && rank == 0) std::cout << "All done" << std::endl;
   g_times[4] = now_s() - t_mark;
   g_times[0] = now_s() - t_start;
   return 0;

@@ -4,10 +4,16 @@
 #pragma once
 #include <arpa/inet.h>
 #include <netdb.h>
+#include <fcntl.h>
 #include <netinet/in.h>
+#include <poll.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <cerrno>
+#include <vector>
+
+#include <algorithm>
 #include <chrono>
 #include <cstdint>
 #include <cstdlib>
@@ -36,9 +42,12 @@ inline bool recv_all(int fd, void* p, size_t n) {
   return true;
 }
 
-// The hello a rank sends before rank 0 hands it the id: magic, rank and a run token (a hash of
-// TORCHELASTIC_RUN_ID, else of MASTER_ADDR:MASTER_PORT), so that a port scan, a health probe or a
-// leftover rank of another job cannot take a slot or receive this job's communicator id.
+// The hello a rank sends before rank 0 hands it the id: magic, rank and a run token, so that a port
+// scan, a health probe or a leftover rank of another job cannot take a slot or receive this job's
+// communicator id.  The token hashes DPE_RDZV_SECRET when the launcher sets one (a random value handed
+// to every rank of the job: then only holders of the secret get the id, i.e. the rendezvous is
+// authenticated); without it the token hashes TORCHELASTIC_RUN_ID, else MASTER_ADDR:MASTER_PORT, which
+// are not secret: that token tells jobs apart, it does not authenticate a peer.
 struct Hello {
   uint32_t magic;
   int32_t rank;
@@ -47,8 +56,9 @@ struct Hello {
 constexpr uint32_t kHelloMagic = 0x44504531u;   // "DPE1"
 
 inline uint64_t run_token() {
+  const char* sec = std::getenv("DPE_RDZV_SECRET");
   const char* id = std::getenv("TORCHELASTIC_RUN_ID");
-  std::string t = id ? std::string("run:") + id : std::string();
+  std::string t = sec && *sec ? std::string("secret:") + sec : (id ? std::string("run:") + id : std::string());
   if (t.empty()) {
     const char* a = std::getenv("MASTER_ADDR");
     const char* p = std::getenv("MASTER_PORT");
@@ -59,10 +69,15 @@ inline uint64_t run_token() {
   return h;
 }
 
-// Rank 0 listens on MASTER_ADDR (not INADDR_ANY) and serves the id to each rank 1..world-1 once,
-// after checking its hello; connections that fail the check are dropped and do not use up a slot.
-// The others connect (retrying for up to 120 s while rank 0 starts).  Every socket call is
-// bounded, so a missing peer ends in an error, not a hang.
+// Rank 0 listens on MASTER_ADDR and serves the id to each rank 1..world-1 once, after checking its
+// hello; connections that fail the check are dropped and do not use up a slot.  Pending connections
+// are served concurrently (poll), each with a 2 s budget for its hello, so connections that send
+// nothing cannot use up the 120 s window of the legitimate ranks.  If MASTER_ADDR resolves to a
+// loopback address while some ranks may run on other hosts (LOCAL_WORLD_SIZE unset or below the
+// world size; /etc/hosts often maps a host's own name to 127.0.1.1), rank 0 listens on every
+// interface instead (the hello check still filters peers).  The others connect (retrying for up to
+// 120 s while rank 0 starts).  Every socket call is bounded, so a missing peer ends in an error,
+// not a hang.
 inline bool exchange_blob(void* id, size_t id_bytes, int rank, int world) {
   const char* addr = std::getenv("MASTER_ADDR");
   const char* rp = std::getenv("DPE_RDZV_PORT");
@@ -74,32 +89,68 @@ inline bool exchange_blob(void* id, size_t id_bytes, int rank, int world) {
   hints.ai_family = AF_INET;
   hints.ai_socktype = SOCK_STREAM;
   if (::getaddrinfo(addr ? addr : "127.0.0.1", std::to_string(port).c_str(), &hints, &res) != 0 || !res) return false;
-  const auto t0 = std::chrono::steady_clock::now();
-  const auto left = [&]() { return std::chrono::seconds(120) - (std::chrono::steady_clock::now() - t0); };
+  using clock = std::chrono::steady_clock;
+  const auto t0 = clock::now();
+  const auto left = [&]() { return std::chrono::seconds(120) - (clock::now() - t0); };
   if (rank == 0) {
     const int srv = ::socket(AF_INET, SOCK_STREAM, 0);
     if (srv < 0) { ::freeaddrinfo(res); return false; }
     const int one = 1;
     ::setsockopt(srv, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
-    ::setsockopt(srv, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
-    bool ok = ::bind(srv, res->ai_addr, res->ai_addrlen) == 0 && ::listen(srv, world) == 0;
+    sockaddr_in sa;
+    std::memcpy(&sa, res->ai_addr, sizeof(sa));
     ::freeaddrinfo(res);
+    const char* lws = std::getenv("LOCAL_WORLD_SIZE");
+    const bool all_local = lws && std::atoi(lws) >= world;
+    if ((ntohl(sa.sin_addr.s_addr) >> 24) == 127 && !all_local) sa.sin_addr.s_addr = htonl(INADDR_ANY);
+    bool ok = ::bind(srv, (const sockaddr*)&sa, sizeof(sa)) == 0 && ::listen(srv, 64) == 0 &&
+              ::fcntl(srv, F_SETFL, ::fcntl(srv, F_GETFL) | O_NONBLOCK) == 0;
+    struct Pending { int fd; clock::time_point deadline; Hello h; size_t got; };
+    std::vector<Pending> pend;
     std::string seen((size_t)world, '\0');
     int served = 0;
+    const timeval sv{2, 0};
     while (ok && served < world - 1 && left().count() > 0) {
-      const int c = ::accept(srv, nullptr, nullptr);   // SO_RCVTIMEO bounds the wait
-      if (c < 0) { ok = false; break; }
-      timeval hv{5, 0};                                  // a silent peer cannot stall the others long
-      ::setsockopt(c, SOL_SOCKET, SO_RCVTIMEO, &hv, sizeof(hv));
-      ::setsockopt(c, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof(tv));
-      Hello h{};
-      if (recv_all(c, &h, sizeof(h)) && h.magic == kHelloMagic && h.token == token && h.rank > 0 && h.rank < world &&
-          !seen[(size_t)h.rank] && send_all(c, id, id_bytes)) {
-        seen[(size_t)h.rank] = 1;
-        ++served;
+      std::vector<pollfd> fds(1 + pend.size());
+      fds[0] = {srv, POLLIN, 0};
+      auto wait = std::chrono::duration_cast<std::chrono::milliseconds>(left());
+      for (size_t i = 0; i < pend.size(); ++i) {
+        fds[1 + i] = {pend[i].fd, POLLIN, 0};
+        wait = std::min(wait, std::chrono::duration_cast<std::chrono::milliseconds>(pend[i].deadline - clock::now()));
       }
-      ::close(c);
+      if (::poll(fds.data(), fds.size(), (int)std::max<long long>(0, std::min<long long>(wait.count(), 1000))) < 0 && errno != EINTR) {
+        ok = false;
+        break;
+      }
+      for (size_t i = 0; i < pend.size(); ++i) {   // hellos in progress
+        Pending& q = pend[i];
+        bool done = false;
+        if (fds[1 + i].revents) {
+          const ssize_t k = ::recv(q.fd, reinterpret_cast<char*>(&q.h) + q.got, sizeof(Hello) - q.got, MSG_DONTWAIT);
+          if (k > 0) q.got += (size_t)k;
+          else if (k == 0 || (errno != EAGAIN && errno != EWOULDBLOCK)) done = true;
+          if (q.got == sizeof(Hello)) {
+            const Hello& h = q.h;
+            if (h.magic == kHelloMagic && h.token == token && h.rank > 0 && h.rank < world && !seen[(size_t)h.rank]) {
+              ::setsockopt(q.fd, SOL_SOCKET, SO_SNDTIMEO, &sv, sizeof(sv));
+              const int fl = ::fcntl(q.fd, F_GETFL);
+              ::fcntl(q.fd, F_SETFL, fl & ~O_NONBLOCK);
+              if (send_all(q.fd, id, id_bytes)) { seen[(size_t)h.rank] = 1; ++served; }
+            }
+            done = true;
+          }
+        }
+        if (done || clock::now() >= q.deadline) { ::close(q.fd); q.fd = -1; }
+      }
+      pend.erase(std::remove_if(pend.begin(), pend.end(), [](const Pending& q) { return q.fd < 0; }), pend.end());
+      if (fds[0].revents & POLLIN)   // new connections: each gets 2 s to say hello
+        for (int c; (c = ::accept(srv, nullptr, nullptr)) >= 0;) {
+          ::fcntl(c, F_SETFL, ::fcntl(c, F_GETFL) | O_NONBLOCK);
+          if (pend.size() >= 256) { ::close(c); continue; }
+          pend.push_back(Pending{c, clock::now() + std::chrono::seconds(2), Hello{}, 0});
+        }
     }
+    for (Pending& q : pend) ::close(q.fd);
     ::close(srv);
     return ok && served == world - 1;
   }

@@ -40,6 +40,14 @@
 #include "oracle_math.h"
 #include "../include/dpe_mvs.h"
 
+// ORACLE_LITERAL (build/liboracle_dpe_literal*.so, tests/test_literal_drift.py only): restatement
+// choices 3 and 7 switched off, i.e. ComputeHomography / ComputeCorrespondingPoint / tex2D(pt + 0.5f)
+// as the reference writes them, to measure what those choices move over whole passes.  1: IEEE
+// division; 2: a * (1 / b) for every division there (a model of --use_fast_math's approximate one).
+#ifndef ORACLE_LITERAL
+#define ORACLE_LITERAL 0
+#endif
+
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -264,8 +272,7 @@ static inline uint32_t TexU(float Q, float iz, int lim) {
   uint32_t u; std::memcpy(&u, &tc, 4);
   return u - 0x4B400000u;
 }
-static inline float OracleSampleQ(const Pass& S, const std::vector<float>& im, float Qx, float Qy, float iz) {
-  const uint32_t ux = TexU(Qx, iz, S.W), uy = TexU(Qy, iz, S.H);
+static inline float OracleSampleU(const Pass& S, const std::vector<float>& im, uint32_t ux, uint32_t uy) {
   const float ax = (float)(ux & 255u) * 0.00390625f;
   const float ay = (float)(uy & 255u) * 0.00390625f;
   const int ix = (int)(ux >> 8) - 1, iy = (int)(uy >> 8) - 1;
@@ -279,6 +286,22 @@ static inline float OracleSampleQ(const Pass& S, const std::vector<float>& im, f
   float r1 = fmaf(ax, t11 - t01, t01);
   return fmaf(ay, r1 - r0, r0);
 }
+static inline float OracleSampleQ(const Pass& S, const std::vector<float>& im, float Qx, float Qy, float iz) {
+  return OracleSampleU(S, im, TexU(Qx, iz, S.W), TexU(Qy, iz, S.H));
+}
+#if ORACLE_LITERAL
+// Literal texture coordinate (ORACLE_LITERAL builds): tex2D(img, s + 0.5f) as DPE.cu:734-736 writes it
+// (the float add rounded), then the CUDA guide's linear filter: x_B = x - 0.5 (rounded in float),
+// 8 fractional bits taken as round-to-nearest of 256 x_B, clamp addressing; same U convention as
+// TexU (texel (U >> 8) - 1, weight (U & 255) / 256, U clamped to [0, 256 lim + 256], NaN -> 0).
+static inline uint32_t TexULiteral(float s, int lim) {
+  const float xb = (s + 0.5f) - 0.5f;
+  if (std::isnan(xb)) return 0;
+  double u = std::floor((double)xb * 256.0 + 0.5) + 256.0;
+  u = u < 0.0 ? 0.0 : (u > 256.0 * (lim + 1) ? 256.0 * (lim + 1) : u);
+  return (uint32_t)u;
+}
+#endif
 // tex2D<float>(depth, (int)x + 0.5f, (int)y + 0.5f) (DPE.cu:936): texel at the truncated coordinate.
 static inline float DepthTexel(const Pass& S, const std::vector<float>& im, float x, float y) {
   int ix = o_f2i(x), iy = o_f2i(y);
@@ -329,6 +352,50 @@ static void ComputeViewConstants(Pass& S) {
 
 struct Homog { float h[9]; };
 
+#if ORACLE_LITERAL
+// float division of the literal builds: IEEE (ORACLE_LITERAL 1) or a * (1 / b), a model of the
+// approximate division --use_fast_math selects (ORACLE_LITERAL 2)
+static inline float LDiv(float a, float b) { return ORACLE_LITERAL == 2 ? a * (1.0f / b) : a / b; }
+// ComputeHomography (DPE.cu:453-513) statement by statement in float32, per call
+static inline Homog MakeHomography(const Pass& S, int v, const float4_& pl) {
+  const DpeCamera& rc = S.cams[0];
+  const DpeCamera& sc = S.cams[v];
+  float refC[3], srcC[3], Rr[9], Cr[3], tr[3], H[9], tmp[9];
+  refC[0] = -(rc.R[0] * rc.t[0] + rc.R[3] * rc.t[1] + rc.R[6] * rc.t[2]);
+  refC[1] = -(rc.R[1] * rc.t[0] + rc.R[4] * rc.t[1] + rc.R[7] * rc.t[2]);
+  refC[2] = -(rc.R[2] * rc.t[0] + rc.R[5] * rc.t[1] + rc.R[8] * rc.t[2]);
+  srcC[0] = -(sc.R[0] * sc.t[0] + sc.R[3] * sc.t[1] + sc.R[6] * sc.t[2]);
+  srcC[1] = -(sc.R[1] * sc.t[0] + sc.R[4] * sc.t[1] + sc.R[7] * sc.t[2]);
+  srcC[2] = -(sc.R[2] * sc.t[0] + sc.R[5] * sc.t[1] + sc.R[8] * sc.t[2]);
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c)
+      Rr[r * 3 + c] = sc.R[r * 3 + 0] * rc.R[c * 3 + 0] + sc.R[r * 3 + 1] * rc.R[c * 3 + 1] + sc.R[r * 3 + 2] * rc.R[c * 3 + 2];
+  for (int j = 0; j < 3; ++j) Cr[j] = refC[j] - srcC[j];
+  for (int r = 0; r < 3; ++r) tr[r] = sc.R[r * 3 + 0] * Cr[0] + sc.R[r * 3 + 1] * Cr[1] + sc.R[r * 3 + 2] * Cr[2];
+  const float pv[3] = {pl.x, pl.y, pl.z};
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c) H[r * 3 + c] = Rr[r * 3 + c] - LDiv(tr[r] * pv[c], pl.w);
+  for (int r = 0; r < 3; ++r) {
+    tmp[r * 3 + 0] = LDiv(H[r * 3 + 0], rc.K[0]);
+    tmp[r * 3 + 1] = LDiv(H[r * 3 + 1], rc.K[4]);
+    tmp[r * 3 + 2] = LDiv(-H[r * 3 + 0] * rc.K[2], rc.K[0]) - LDiv(H[r * 3 + 1] * rc.K[5], rc.K[4]) + H[r * 3 + 2];
+  }
+  Homog o;
+  for (int c = 0; c < 3; ++c) {
+    o.h[0 + c] = sc.K[0] * tmp[0 + c] + sc.K[2] * tmp[6 + c];
+    o.h[3 + c] = sc.K[4] * tmp[3 + c] + sc.K[5] * tmp[6 + c];
+    o.h[6 + c] = sc.K[8] * tmp[6 + c];
+  }
+  return o;
+}
+// ComputeCorrespondingPoint (DPE.cu:515-522) as written: h0*x + h1*y + h2, then X / Z
+static inline float2_ Project(const Homog& H, float x, float y) {
+  const float X = H.h[0] * x + H.h[1] * y + H.h[2];
+  const float Y = H.h[3] * x + H.h[4] * y + H.h[5];
+  const float Z = H.h[6] * x + H.h[7] * y + H.h[8];
+  float2_ r; r.x = LDiv(X, Z); r.y = LDiv(Y, Z); return r;
+}
+#else
 static inline Homog MakeHomography(const Pass& S, int v, const float4_& pl) {
   const float iw = 1.0f / pl.w;
   const float qx = pl.x * iw, qy = pl.y * iw, qz = pl.z * iw;
@@ -349,6 +416,7 @@ static inline float2_ Project(const Homog& H, float x, float y) {
   float iz = 1.0f / pz;
   float2_ r; r.x = px * iz; r.y = py * iz; return r;
 }
+#endif
 
 // ComputeBilateralWeight (DPE.cu:550-555)
 static inline float BilateralWeight(const Pass& S, int i, int j, float pix, float cpix) {
@@ -372,10 +440,16 @@ static inline float PatchNCC(const Pass& S, const std::vector<float>& src, const
       const int x = cx + i, y = cy + j;
       const float rp = RefTexel(S, ref, x, y);
       const float xf = (float)x, yf = (float)y;
+#if ORACLE_LITERAL
+      (void)h1s; (void)h4s;
+      const float2_ st = Project(H, xf, yf);
+      const float sp = OracleSampleU(S, src, TexULiteral(st.x, S.W), TexULiteral(st.y, S.H));
+#else
       const float Qx = fmaf(h1s, yf, fmaf(H.h[0], xf, H.h[2]) * 256.0f);
       const float Qy = fmaf(h4s, yf, fmaf(H.h[3], xf, H.h[5]) * 256.0f);
       const float iz = 1.0f / fmaf(H.h[7], yf, fmaf(H.h[6], xf, H.h[8]));
       const float sp = OracleSampleQ(S, src, Qx, Qy, iz);
+#endif
       const float w = BilateralWeight(S, i, j, rp, ref_center_pix);
       const float wr = w * rp;
       r_ref = r_ref + wr;

@@ -28,10 +28,10 @@ def build():
     subprocess.run(["make", "-C", HERE], check=True, stdout=subprocess.DEVNULL)
 
 
-def _load():
-    if not os.path.exists(LIB):
+def _load(path: str = LIB):
+    if not os.path.exists(path):
         build()
-    lib = C.CDLL(LIB)
+    lib = C.CDLL(path)
     lib.oracle_pm_run.argtypes = [C.POINTER(_abi.DpePassInput), C.POINTER(_abi.DpePassState), C.c_int]
     lib.oracle_pm_run.restype = C.c_int
     lib.oracle_last_error.restype = C.c_char_p
@@ -91,6 +91,17 @@ def lib():
     return _lib
 
 
+_literal = {}
+
+
+def literal_lib(mode: int):
+    """The ORACLE_LITERAL build (dpe_oracle.cpp): 1 = ComputeHomography / ComputeCorrespondingPoint /
+    tex2D(pt + 0.5f) as written with IEEE division, 2 = the same with a * (1 / b) divisions."""
+    if mode not in _literal:
+        _literal[mode] = _load(os.path.join(HERE, "build", f"liboracle_dpe_literal{mode}.so"))
+    return _literal[mode]
+
+
 def host_threads() -> int:
     """Host threads this process may use: OMP_NUM_THREADS when set (the GPU box sets it to its CPU
     share), else the affinity mask."""
@@ -103,14 +114,15 @@ def host_threads() -> int:
         return os.cpu_count() or 1
 
 
-def run_pass(pass_input: dict, state: dict, threads: int = 0) -> dict:
-    """One PatchMatch pass on the CPU (same semantics as dpe_pm_run)."""
+def run_pass(pass_input: dict, state: dict, threads: int = 0, library=None) -> dict:
+    """One PatchMatch pass on the CPU (same semantics as dpe_pm_run); `library`: a literal_lib()."""
     if threads <= 0:
         threads = host_threads()
+    L = library or lib()
     b = _abi.PassBuffers(pass_input, state)
-    rc = lib().oracle_pm_run(C.byref(b.inp), C.byref(b.st), int(threads))
+    rc = L.oracle_pm_run(C.byref(b.inp), C.byref(b.st), int(threads))
     if rc != 0:
-        raise RuntimeError("oracle_pm_run: " + lib().oracle_last_error().decode())
+        raise RuntimeError("oracle_pm_run: " + L.oracle_last_error().decode())
     return {k: v.copy() for k, v in b.outputs().items()}
 
 

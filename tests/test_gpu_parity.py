@@ -78,6 +78,8 @@ CASES = [
     (72, 56, 3, "weak_generic"),
     (23, 131, 3, "refine_iter"),         # tall, narrow: W < one block, ragged in both axes
     (193, 29, 3, "first"),               # W = 3*64+1: one pixel into a fourth wave-width column
+    (12, 40, 3, "refine_iter"),          # no DepthToWeak interior: LocalRefine over every pixel (border kernel)
+    (40, 13, 3, "refine_iter"),          # one interior row: fused DepthToWeak+LocalRefine beside the border kernel
 ]
 
 

@@ -522,7 +522,14 @@ def _literal_patch(ref_img, src_img, point, cx, cy, center, radius, increment, s
 def literal_ncc_old(ref_img, src_img, ref, src, plane, px, py, radius=5, increment=2, ss=5.0, sc=3.0):
     """ComputeBilateralNCCOld + ComputeBilateralWeight (DPE.cu:550-555, 692-778) statement by
     statement in float32 (each operation rounded once), the homography and projection of
-    DPE.cu:453-522 (literal_homography / literal_point's expressions) and literal_tex2d."""
+    DPE.cu:453-522 (literal_homography / literal_point's expressions) and literal_tex2d.
+
+    Deviation from the reference's arithmetic, stated: the reference is built --use_fast_math
+    (CMakeLists.txt:72, 113), i.e. approximate division, __expf and flush-to-zero; this
+    transcription uses IEEE division and np.exp, and the texture unit's 8-fractional-bit rounding
+    is taken as round-to-nearest.  The 1/256 tap-coordinate rounding of restatement choice 7 is
+    therefore not pinned by any reference fixture; tests/test_literal_drift.py measures what choices
+    3 and 7 move over whole passes, with a * (1 / b) as a model of the approximate division."""
     point = _literal_point_fn(ref, src, plane)
     ptx, pty = point(px, py)
     if ptx >= src.width or ptx < 0 or pty >= src.height or pty < 0:

@@ -285,7 +285,31 @@ def test_cli_usage():
     assert main(["DPE"]) == 1
 
 
+def test_pybind_streams_go_to_python(tmp_path, dense4, capsys):
+    # the reference binding routes std::cout / std::cerr into sys.stdout / sys.stderr
+    # (csrc/bindings.cpp:23-24); an unreadable image ends the run on the host, before any device work
+    d = _copy(dense4, tmp_path, "broken")
+    os.remove(os.path.join(d, "images", "00000002.jpg"))
+    from DPE_MVS import dpe_mvs
+    with pytest.raises(RuntimeError, match="Images may error"):
+        dpe_mvs(d, 0, True, False, False, True, False, False, False)
+    assert "Images may error, check it!" in capsys.readouterr().err
+
+
 # ------------------------------------------------------------------------------ GPU
+@pytest.mark.gpu
+def test_pybind_verbose_lines_reach_sys_stdout(tmp_path, dense4, capsys):
+    # config-1-sized run through the pybind entry with verbose=True: main.cpp:489, 504's progress
+    # lines and the per-iteration lines arrive on Python's sys.stdout
+    a = _copy(dense4, tmp_path, "verbose")
+    from DPE_MVS import dpe_mvs
+    assert dpe_mvs(a, 0, True, False, False, True, False, False, False) == 0
+    out = capsys.readouterr().out
+    assert "There are 4 images to be processed!" in out
+    assert "resolution stages for coarse-to-fine processing!" in out
+    assert "Iteration 1 / 8 done" in out and "All done" in out
+
+
 @pytest.mark.gpu
 def test_pipeline_hip_matches_oracle(tmp_path, dense4):
     a = _copy(dense4, tmp_path, "hip")

@@ -83,3 +83,38 @@ def test_other_job_cannot_take_a_slot(driver):
     assert mine.stdout.strip() == EXPECTED and r0_out.strip() == EXPECTED
     other.kill()
     other.wait()
+
+
+def test_silent_connections_do_not_starve_the_ranks(driver):
+    # connections that never send a hello are served concurrently with a 2 s budget each, so the
+    # real ranks get the id at once instead of after 5 s per silent peer
+    port = _free_port()
+    r0 = subprocess.Popen([driver, "0", "3"], env=_env(port), stdout=subprocess.PIPE, text=True)
+    silent = [_connect(port) for _ in range(12)]
+    t0 = time.time()
+    outs = [subprocess.Popen([driver, str(r), "3"], env=_env(port), stdout=subprocess.PIPE, text=True) for r in (1, 2)]
+    res = [o.communicate(timeout=60)[0].strip() for o in outs]
+    r0_out, _ = r0.communicate(timeout=60)
+    took = time.time() - t0
+    for s in silent:
+        s.close()
+    assert res == [EXPECTED, EXPECTED] and r0_out.strip() == EXPECTED
+    assert took < 6.0, took
+
+
+def test_shared_secret_authenticates(driver):
+    # with DPE_RDZV_SECRET set on the job's ranks, a peer that knows the run id but not the secret
+    # gets nothing and takes no slot
+    port = _free_port()
+    env = _env(port)
+    env["DPE_RDZV_SECRET"] = "s3cr3t-nonce"
+    r0 = subprocess.Popen([driver, "0", "2"], env=env, stdout=subprocess.PIPE, text=True)
+    time.sleep(0.2)
+    nosecret = subprocess.Popen([driver, "1", "2"], env=_env(port), stdout=subprocess.PIPE, text=True)
+    time.sleep(1.0)
+    assert r0.poll() is None, "rank 0 served a peer without the secret"
+    mine = subprocess.run([driver, "1", "2"], env=env, capture_output=True, text=True, timeout=60)
+    r0_out, _ = r0.communicate(timeout=60)
+    assert mine.stdout.strip() == EXPECTED and r0_out.strip() == EXPECTED
+    nosecret.kill()
+    nosecret.wait()

@@ -88,15 +88,17 @@ def test_resident_two_ranks_match_one_rank_jacobi(tmp_path, dense4):
     _same(_outputs(one, 4), _outputs(two, 4))
 
 
-def _rank_main_devhook(rank, world, port, folder, flag_rank, q):
+def _rank_main_devhook(rank, world, port, folder, fault, q):
     """A rank whose device all-gather hook is a host hop over gloo (so the device exchange path of
-    host/pipeline.cpp -- dsend packing, the status float at nmax * per, the import offsets
-    r * cnt + k * per -- runs on one GPU).  flag_rank >= 0: that rank's hook raises its status
-    float before gathering, as a rank whose pass failed does."""
+    host/pipeline.cpp -- dsend packing, the import offsets r * cnt + k * per -- runs on one GPU).
+    `fault` ("before:R" / "after:R", DPE_FAULT_INJECT): rank R fails locally just before the first
+    resident exchange's status all-gather, or just after its depth all-gather."""
     import torch
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    if fault:
+        os.environ["DPE_FAULT_INJECT"] = fault
     dist.init_process_group("gloo", rank=rank, world_size=world)
     calls = [0]
 
@@ -104,11 +106,8 @@ def _rank_main_devhook(rank, world, port, folder, flag_rank, q):
         calls[0] += 1
         s = torch.as_tensor(pipeline._DeviceArray(send, count), device="cuda")
         r = torch.as_tensor(pipeline._DeviceArray(recv, world * count), device="cuda")
-        h = s.cpu()
-        if rank == flag_rank:
-            h[-1] = 1.0
         out = torch.empty(world * count, dtype=torch.float32)
-        dist.all_gather_into_tensor(out, h)
+        dist.all_gather_into_tensor(out, s.cpu())
         r.copy_(out.to("cuda"))
         torch.cuda.synchronize()
         return 0
@@ -122,22 +121,28 @@ def _rank_main_devhook(rank, world, port, folder, flag_rank, q):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("flag_rank", [-1, 1])
-def test_resident_device_hook_path(tmp_path, dense4, flag_rank):
+@pytest.mark.parametrize("fault", ["", "before:1", "after:1"])
+def test_resident_device_hook_path(tmp_path, dense4, fault):
     import torch.multiprocessing as mp
     one = _copy(dense4, tmp_path, "one")
     two = _copy(dense4, tmp_path, "two")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    mp.start_processes(_rank_main_devhook, args=(2, _free_port(), two, flag_rank, q), nprocs=2, join=True,
+    mp.start_processes(_rank_main_devhook, args=(2, _free_port(), two, fault, q), nprocs=2, join=True,
                        start_method="spawn")
     got = {r: (msg, n) for r, msg, n in (q.get(timeout=10) for _ in range(2))}
-    assert all(n > 0 for _, n in got.values()), got          # the device hook carried the exchange
-    if flag_rank < 0:
+    if not fault:
+        assert all(n > 0 for _, n in got.values()), got          # the device hook carried the exchange
         assert all(msg == "ok" for msg, _ in got.values()), got
         assert pipeline.run_dpe_pipeline(one, runner=oracle_runner(), schedule="jacobi", normal=True, weak=True,
                                          verbose=False) == 0
         _same(_outputs(one, 4), _outputs(two, 4))
-    else:   # every rank ends at the same exchange with the flagged rank's failure
-        assert got[0][0] == "rank 1 failed" and got[0][1] == 1, got
-        assert got[1][1] == 1 and got[1][0] != "ok", got
+    elif fault.startswith("before"):
+        # every rank ends at the first exchange's status all-gather, before any depth all-gather
+        assert got[0] == ("rank 1 failed", 0), got
+        assert got[1] == ("injected fault before the exchange", 0), got
+    else:
+        # rank 1 fails after the first depth all-gather, which every rank completed; the others are
+        # not left behind: every rank ends at the next exchange's status all-gather
+        assert got[0] == ("rank 1 failed", 1), got
+        assert got[1] == ("injected fault after the exchange", 1), got
