@@ -16,6 +16,8 @@ FIRST_INIT, REFINE_INIT, REFINE_ITER = 0, 1, 2          # main.h:66-70 RunState
 WEAK, STRONG, UNKNOWN = 0, 1, 2                          # main.h:72-76 PixelState
 
 DPE_OK = 0
+DPE_OPT_GN_SLOTS = 1          # dpe_set_option: GenNeighbours support-point slots (include/dpe_mvs.h)
+DPE_STAT_GN_DEFERRED = 1      # dpe_pm_last_stat: WEAK pixels handed to the scratch GenNeighbours
 
 
 class DpeCamera(C.Structure):

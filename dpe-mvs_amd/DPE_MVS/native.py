@@ -59,6 +59,10 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.dpe_set_counting.restype = None
     lib.dpe_pm_last_counts.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_int]
     lib.dpe_pm_last_counts.restype = C.c_int
+    lib.dpe_set_option.argtypes = [C.c_void_p, C.c_int, C.c_int]
+    lib.dpe_set_option.restype = C.c_int
+    lib.dpe_pm_last_stat.argtypes = [C.c_void_p, C.c_int]
+    lib.dpe_pm_last_stat.restype = C.c_longlong
     lib.dpe_fusion_stage.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
     lib.dpe_fusion_stage.restype = C.c_int
     lib.dpe_fusion_candidates.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
@@ -167,6 +171,12 @@ class PatchMatchContext:
 
     def set_counting(self, on: bool):
         _LIB.dpe_set_counting(self._ctx, 1 if on else 0)
+
+    def set_option(self, option: int, value: int):
+        _check(_LIB.dpe_set_option(self._ctx, int(option), int(value)), "dpe_set_option")
+
+    def last_stat(self, stat: int) -> int:
+        return int(_LIB.dpe_pm_last_stat(self._ctx, int(stat)))
 
     def timings(self) -> dict:
         """{'total': ms, <class>: summed kernel ms} of the last execute (timing enabled)."""

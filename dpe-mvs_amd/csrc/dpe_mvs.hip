@@ -122,6 +122,7 @@ struct DpeContext {
   bool staged = false;
   bool timing = false;
   bool counting = false;
+  int gn_slots = 0;                  // DPE_OPT_GN_SLOTS (0 = by rotate_time)
   float timings[DPE_NUM_CLASSES + 1] = {0};
   int launches[DPE_NUM_CLASSES + 1] = {0};
   unsigned long long counts[DPE_NUM_CLASSES * 4] = {0};
@@ -813,7 +814,10 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
         HIPC(hipMemsetAsync(c->gn_ecache.p, 0, (size_t)496 * (L + 64), a));
         ec = c->gn_ecache.p;
       }
-      if (pc.P.rotate_time <= 2)   // at most 16 x rotate_time support points
+      if (c->gn_slots == 8)   // test setting: most pixels overflow into the scratch kernel
+        k_gen_neighbours_lds<8><<<gg, DPE_GN_BT, 0, a>>>(dpc, Bgn, lst, cnt, c->gn_tab.p, c->gn_ovf.p, c->list_totals.p + 6,
+                                                         nullptr, 0);
+      else if (pc.P.rotate_time <= 2 && c->gn_slots != 64)   // at most 16 x rotate_time support points
         k_gen_neighbours_lds<32><<<gg, DPE_GN_BT, 0, a>>>(dpc, Bgn, lst, cnt, c->gn_tab.p, c->gn_ovf.p, c->list_totals.p + 6,
                                                           ec, (long)L + 64);
       else
@@ -1401,6 +1405,23 @@ extern "C" int dpe_pm_last_timings(DpeContext* c, float* out, int n) {
 }
 
 extern "C" void dpe_set_counting(DpeContext* c, int enable) { if (c) c->counting = enable != 0; }
+
+extern "C" int dpe_set_option(DpeContext* c, int option, int value) {
+  g_err.clear();
+  if (!c) { g_err = "dpe_set_option: null context"; return DPE_ERR_ARG; }
+  if (option == DPE_OPT_GN_SLOTS && (value == 0 || value == 8 || value == 32 || value == 64)) { c->gn_slots = value; return DPE_OK; }
+  g_err = "dpe_set_option: unknown option or value";
+  return DPE_ERR_ARG;
+}
+
+extern "C" long long dpe_pm_last_stat(DpeContext* c, int stat) {
+  if (!c || !c->staged || stat != DPE_STAT_GN_DEFERRED || !c->list_totals.p) return -1;
+  int v = 0;
+  if (hipSetDevice(c->device) != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpy(&v, c->list_totals.p + 6, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  return v;
+}
 
 extern "C" int dpe_pm_last_counts(DpeContext* c, unsigned long long* out, int n) {
   if (!c || !out) return 0;

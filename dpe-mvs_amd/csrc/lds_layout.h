@@ -54,7 +54,8 @@ struct StrongCarve {
   LDS_HD static constexpr int cpl(int nv) { return base(nv); }                // [P][C + 1] float4 candidate planes
   LDS_HD static constexpr int alias(int nv) { return base(nv) + P * (C + 1) * 4; }   // [P][C + 1] ints
   LDS_HD static constexpr int tail(int nv) { return alias(nv) + P * (C + 1); }       // [TAIL_JOBS][6][3] row sums
-  LDS_HD static constexpr int total(int nv) { return tail(nv) + TAIL_JOBS * 18; }
+  LDS_HD static constexpr int rnd(int nv) { return tail(nv) + TAIL_JOBS * 18; }      // [P][12] refinement draws
+  LDS_HD static constexpr int total(int nv) { return rnd(nv) + P * 12; }
   // ints of a pixel's ib block
   static constexpr int IB_POS = 0;            // [C] candidate positions (-1 = none)
   static constexpr int IB_FIN = C;            // [8] final slot of direction d
@@ -67,7 +68,8 @@ struct StrongCarve {
     const Region r[] = {{hyp(), P * 20, 4},        {patch(), P * kPatch, 1}, {cost(nv), P * (C + 1) * nv, 1},
                         {sp(nv), P * nv, 1},       {ref(nv), P * 5 * nv, 1}, {fc(nv), P * 8, 1},
                         {sums(nv), P * 4, 1},      {vw(nv), P * 8, 1},       {ib(nv), P * ib_ints(nv), 1},
-                        {cpl(nv), P * (C + 1) * 4, 4}, {alias(nv), P * (C + 1), 1}, {tail(nv), TAIL_JOBS * 18, 1}};
+                        {cpl(nv), P * (C + 1) * 4, 4}, {alias(nv), P * (C + 1), 1}, {tail(nv), TAIL_JOBS * 18, 1},
+                        {rnd(nv), P * 12, 1}};
     // the sampling counts (view_sample_coop) reuse a pixel's ref block as nv ints; the ib block's
     // sub-arrays must fit its ints
     return regions_ok(r, total(nv)) && ib_slots(nv) + C + 1 == ib_ints(nv) && P * C == 64 && MI_DEPTH + 5 <= 8;

@@ -204,6 +204,63 @@ DEV float4 perturbed_normal(const DpeCamera& c, int px, int py, const float4& no
   return np;
 }
 
+// The refinement draws of PlaneHypothesisRefinement (DPE.cu:1081-1093: a uniform depth,
+// GenerateRandomNormal, a uniform perturbed depth, GeneratePerturbedNormal's three angles) sit at
+// fixed stream positions from word w0 on: the rejection loop's length depends on the draws only.
+// So their data-independent part can be evaluated on other lanes, ahead of the data-dependent rest
+// (the view-direction flips, the rotation of the accepted plane, normalisation): same values, same
+// order of operations as random_normal / perturbed_normal.
+struct RefineDraws {
+  float u_depth;          // uniform of the random depth
+  float n[3];             // random normal before the view-direction flip
+  float u_pert;           // uniform of the perturbed depth
+  uint32_t w_angles;      // stream word of the first angle
+};
+DEV RefineDraws refine_draws(const Rng& rs, uint32_t w0) {
+  RefineDraws d;
+  d.u_depth = u32_to_uniform(rng_word(rs, w0));
+  uint32_t w = w0 + 1;
+  float q1 = 1.0f, q2 = 1.0f, s = 2.0f;
+  while (s >= 1.0f) {
+    q1 = 2.0f * u32_to_uniform(rng_word(rs, w)) - 1.0f;
+    q2 = 2.0f * u32_to_uniform(rng_word(rs, w + 1)) - 1.0f;
+    s = q1 * q1 + q2 * q2;
+    w += 2;
+  }
+  const float sq = __builtin_sqrtf(1.0f - s);
+  d.n[0] = 2.0f * q1 * sq; d.n[1] = 2.0f * q2 * sq; d.n[2] = 1.0f - 2.0f * s;
+  d.u_pert = u32_to_uniform(rng_word(rs, w));
+  d.w_angles = w + 1;
+  return d;
+}
+// angle k (0..2) of GeneratePerturbedNormal: its sine and cosine
+DEV void refine_angle(const Rng& rs, uint32_t w_angles, int k, float pert, float* s, float* c) {
+  const float a = (u32_to_uniform(rng_word(rs, w_angles + (uint32_t)k)) - 0.5f) * pert;
+  d_sincosf(a, s, c);
+}
+// random_normal from its pre-flip normal
+DEV float4 random_normal_from(const DpeCamera& c, int px, int py, const float* n0, float depth) {
+  float4 n = make_float4(n0[0], n0[1], n0[2], 0.0f);
+  const float4 vd = view_direction(c, px, py, depth);
+  if (n.x * vd.x + n.y * vd.y + n.z * vd.z > 0.0f) { n.x = -n.x; n.y = -n.y; n.z = -n.z; }
+  normalize3(n);
+  return n;
+}
+// perturbed_normal from the angles' sines and cosines sc = {s1, c1, s2, c2, s3, c3}
+DEV float4 perturbed_normal_from(const DpeCamera& c, int px, int py, const float4& normal, const float* sc) {
+  const float4 vd = view_direction(c, px, py, 1.0f);
+  const float s1 = sc[0], c1 = sc[1], s2 = sc[2], c2 = sc[3], s3 = sc[4], c3 = sc[5];
+  const float R0 = c2 * c3, R1 = c3 * s1 * s2 - c1 * s3, R2 = s1 * s3 + c1 * c3 * s2;
+  const float R3 = c2 * s3, R4 = c1 * c3 + s1 * s2 * s3, R5 = c1 * s2 * s3 - c3 * s1;
+  const float R6 = -s2, R7 = c2 * s1, R8 = c1 * c2;
+  float4 np = make_float4(R0 * normal.x + R1 * normal.y + R2 * normal.z,
+                          R3 * normal.x + R4 * normal.y + R5 * normal.z,
+                          R6 * normal.x + R7 * normal.y + R8 * normal.z, normal.w);
+  if (np.x * vd.x + np.y * vd.y + np.z * vd.z >= 0.0f) np = normal;
+  normalize3(np);
+  return np;
+}
+
 // ------------------------------------------------------------------------------ homography
 // H = M_v - b_v g^T, g = Kref^-T (n/w) (restatement of ComputeHomography, DPE.cu:453-513).
 struct Homog { float h[9]; };

@@ -291,6 +291,9 @@ DEV int acmh_candidate(const PassConst& pc, const float* __restrict__ costs, int
 #ifndef DPE_TAIL_SPLIT
 #define DPE_TAIL_SPLIT 1
 #endif
+#ifndef DPE_STRONG_PRE
+#define DPE_STRONG_PRE 0   // 1: refinement draws on lanes 1..4 beside lane 0's acceptance (A/B)
+#endif
 constexpr int kTailJobs = 16;   // a last round of at most this many jobs is split by patch rows
 // the strong sweep's LDS carve per wave (lds_layout.h: P pixels, C candidate lanes, nv source views)
 template <int P, int C> using StrongCarveT = lds::StrongCarve<P, C, DPE_TAIL_SPLIT ? kTailJobs : 0>;
@@ -355,6 +358,7 @@ __global__ void __launch_bounds__(64 * DPE_BW_STRONG, DPE_TAP_WAVES) k_strong_co
   int* slots = ib + SC::ib_slots(nv);                    // [C + 1] cost-vector jobs: candidate slots, then C
   float4* cpl_all = (float4*)(wl + SC::cpl(nv));         // [P][C + 1] candidate planes, slot C = current
   int* alias_all = (int*)(wl + SC::alias(nv));           // [P][C + 1]
+  float* rnd = wl + SC::rnd(nv) + ps * 12;               // [P][12] refinement draws (DPE_STRONG_PRE)
   float4* cpl = cpl_all + ps * (C + 1);
   int* alias = alias_all + ps * (C + 1);
   float4* hyp = hyp_all + ps * 5;
@@ -599,6 +603,16 @@ __global__ void __launch_bounds__(64 * DPE_BW_STRONG, DPE_TAP_WAVES) k_strong_co
   // ---- serial: propagation acceptance + refinement hypotheses (DPE.cu:1617-1654, 1065-1095)
   float cost_now = 0.0f, cost_written = 0.0f, depth_now = 0.0f;
   float4 pnow = make_float4(0, 0, 0, 0);
+  const float pert = (float)(0.02f * 3.14159265358979323846);
+#if DPE_STRONG_PRE
+  // lanes 1..4 evaluate the refinement draws (refine_draws: stream words 15.. after the view
+  // sampling) while lane 0 runs the acceptance; lane 0 then finishes the hypotheses from them
+  if (active && c >= 1 && c <= 4) {
+    const RefineDraws d = refine_draws(rs, 15u);
+    if (c == 1) { rnd[0] = d.u_depth; rnd[1] = d.n[0]; rnd[2] = d.n[1]; rnd[3] = d.n[2]; rnd[4] = d.u_pert; }
+    else refine_angle(rs, d.w_angles, c - 2, pert, &rnd[5 + 2 * (c - 2)], &rnd[6 + 2 * (c - 2)]);
+  }
+#endif
   if (active && c == 0) {
     int mi = 0; float mcost = fc[0];
     for (int i = 1; i < 8; ++i) if (fc[i] <= mcost) { mcost = fc[i]; mi = i; }
@@ -617,12 +631,31 @@ __global__ void __launch_bounds__(64 * DPE_BW_STRONG, DPE_TAP_WAVES) k_strong_co
         depth_now = db; pnow = cand; cost_now = fc[mi]; B.sel[center] = tsv;
       }
     }
+#if !DPE_STRONG_PRE
     const float dmin = pc.P.depth_min, dmax = pc.P.depth_max;
     const float depth_rand = rng_uniform(rs) * (dmax - dmin) + dmin;
     const float4 prand = random_normal(c0, x, y, rs, depth_now);
     const float dminp = (1 - 0.02f) * depth_now, dmaxp = (1 + 0.02f) * depth_now;
     const float depth_perturbed = rng_uniform(rs) * (dmaxp - dminp) + dminp;
-    const float4 ppert = perturbed_normal(c0, x, y, pnow, rs, (float)(0.02f * 3.14159265358979323846));
+    const float4 ppert = perturbed_normal(c0, x, y, pnow, rs, pert);
+    float4 h0 = pnow, h1 = prand, h2 = prand, h3 = ppert, h4 = pnow;
+    h0.w = dist2origin(c0, x, y, depth_rand, h0);
+    h1.w = dist2origin(c0, x, y, depth_now, h1);
+    h2.w = dist2origin(c0, x, y, depth_rand, h2);
+    h3.w = dist2origin(c0, x, y, depth_now, h3);
+    h4.w = dist2origin(c0, x, y, depth_perturbed, h4);
+    hyp[0] = h0; hyp[1] = h1; hyp[2] = h2; hyp[3] = h3; hyp[4] = h4;
+#endif
+  }
+#if DPE_STRONG_PRE
+  wave_sync();
+  if (active && c == 0) {
+    const float dmin = pc.P.depth_min, dmax = pc.P.depth_max;
+    const float depth_rand = rnd[0] * (dmax - dmin) + dmin;
+    const float4 prand = random_normal_from(c0, x, y, rnd + 1, depth_now);
+    const float dminp = (1 - 0.02f) * depth_now, dmaxp = (1 + 0.02f) * depth_now;
+    const float depth_perturbed = rnd[4] * (dmaxp - dminp) + dminp;
+    const float4 ppert = perturbed_normal_from(c0, x, y, pnow, rnd + 5);
     float4 h0 = pnow, h1 = prand, h2 = prand, h3 = ppert, h4 = pnow;
     h0.w = dist2origin(c0, x, y, depth_rand, h0);
     h1.w = dist2origin(c0, x, y, depth_now, h1);
@@ -631,6 +664,7 @@ __global__ void __launch_bounds__(64 * DPE_BW_STRONG, DPE_TAP_WAVES) k_strong_co
     h4.w = dist2origin(c0, x, y, depth_perturbed, h4);
     hyp[0] = h0; hyp[1] = h1; hyp[2] = h2; hyp[3] = h3; hyp[4] = h4;
   }
+#endif
   wave_sync();
   PHASE(9);
   // ---- phase 6: refinement NCCs, one flat pool of (pixel, hypothesis, selected view)

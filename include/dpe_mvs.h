@@ -268,6 +268,19 @@ int dpe_pm_last_timings(DpeContext* ctx, float* ms, int n);
 void dpe_set_counting(DpeContext* ctx, int enable);
 int dpe_pm_last_counts(DpeContext* ctx, unsigned long long* out, int n);
 
+/* Diagnostic knobs and statistics of the pass (not part of the reference's surface; tests).
+ * DPE_OPT_GN_SLOTS: support-point slots per WEAK pixel of the scratch-free GenNeighbours
+ *   (k_gen_neighbours_lds): 0 = by rotate_time (32 up to 2, else 64, enough for every pixel), 8 = a
+ *   test setting that sends every pixel with more points through the overflow path (the scratch
+ *   kernel).  Results are the same for every setting.
+ * DPE_STAT_GN_DEFERRED: WEAK pixels the scratch-free GenNeighbours of the last execute handed to the
+ *   scratch kernel (more points than slots, or a NaN in its sorts).  Synchronises with the pass.
+ * dpe_set_option returns DPE_OK or DPE_ERR_ARG; dpe_pm_last_stat returns the value or -1. */
+enum { DPE_OPT_GN_SLOTS = 1 };
+enum { DPE_STAT_GN_DEFERRED = 1 };
+int dpe_set_option(DpeContext* ctx, int option, int value);
+long long dpe_pm_last_stat(DpeContext* ctx, int stat);
+
 /*
  * RunFusion (DPE.cpp:1220-1370): the per-(pixel, source view) projection tests on the GPU.  The
  * order-dependent rest (the masks of already fused pixels, the angle test, the consistency weights,

@@ -93,6 +93,34 @@ def test_gpu_matches_oracle(ctx, W, H, N, kind):
     assert_same(ctx.run(inp, st), oracle.run_pass(inp, st), f"{W}x{H}x{N} {kind}")
 
 
+@pytest.mark.parametrize("W,H,N,kind", [(128, 96, 6, "refine_iter"), (96, 72, 4, "refine_init"), (88, 66, 4, "no_limit")])
+def test_gpu_gen_neighbours_overflow_path(W, H, N, kind):
+    # GenNeighbours' deferral path (DPE.cu:2281-2307 point collection, :2367-2449 sorts): with 8
+    # support-point slots (DPE_OPT_GN_SLOTS) the scratch-free kernel hands every pixel with more points
+    # to the scratch kernel (k_gen_neighbours over the overflow list).  The neighbours, weak_reliable
+    # and complex it writes feed NeigbourUpdate and every NCC-New of the weak sweep, so the pass
+    # outputs must stay the oracle's bit for bit; the deferred count must be > 0.  With the default
+    # slots nothing is deferred at these sizes.
+    from DPE_MVS import native
+    sc = synthetic.make_scene(W, H, N)
+    p = _params(kind)
+    st = synthetic.gt_state(sc, seed=W + H)
+    inp = synthetic.pass_input(sc, p, depths=synthetic.src_depths(sc) if p.geom_consistency else None, seed=W * 7 + N)
+    want = oracle.run_pass(inp, st)
+    c = native.PatchMatchContext(0)
+    try:
+        got_default = c.run(inp, st)
+        assert c.last_stat(_abi.DPE_STAT_GN_DEFERRED) == 0
+        c.set_option(_abi.DPE_OPT_GN_SLOTS, 8)
+        got = c.run(inp, st)
+        deferred = c.last_stat(_abi.DPE_STAT_GN_DEFERRED)
+    finally:
+        c.close()
+    assert deferred > 0, deferred
+    assert_same(got_default, want, f"{W}x{H}x{N} {kind} default slots")
+    assert_same(got, want, f"{W}x{H}x{N} {kind} 8 slots ({deferred} pixels deferred)")
+
+
 def test_gpu_many_views(ctx):
     # 32 images = the reference's MAX_IMAGES (31 source views, 32-bit view masks)
     sc = synthetic.make_scene(48, 36, 32)

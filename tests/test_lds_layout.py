@@ -16,7 +16,7 @@ def _compile(tmp_path, body):
 
 
 def test_layouts_hold(tmp_path):
-    r = _compile(tmp_path, "static_assert(dpe::lds::StrongCarve<4, 16, 16>::total(9) == 1652 + 4 * 17 * 5 + 288, \"\");\n"
+    r = _compile(tmp_path, "static_assert(dpe::lds::StrongCarve<4, 16, 16>::total(9) == 1652 + 4 * 17 * 5 + 288 + 4 * 12, \"\");\n"
                            "static_assert(dpe::lds::WeakCarve::per_pixel(9) == 636, \"\");")
     assert r.returncode == 0, r.stderr
 
