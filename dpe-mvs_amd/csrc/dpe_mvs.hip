@@ -1165,6 +1165,15 @@ extern "C" float* dpe_device_buffer(DpeContext* c, int slot, size_t count) {
   return c->xbuf[slot].p;
 }
 
+extern "C" int dpe_sync(DpeContext* c) {
+  g_err.clear();
+  if (!c) { g_err = "dpe_sync: null context"; return DPE_ERR_ARG; }
+  HIPC(hipSetDevice(c->device));
+  HIPC(wait_pending(c));
+  HIPC(hipStreamSynchronize(c->stream));
+  return DPE_OK;
+}
+
 extern "C" int dpe_device_copy(DpeContext* c, void* dst, const void* src, size_t bytes, int kind) {
   g_err.clear();
   if (!c || !dst || !src || kind < 0 || kind > 2) { g_err = "dpe_device_copy: bad argument"; return DPE_ERR_ARG; }

@@ -82,8 +82,12 @@ struct StrongCarve {
 
 // ------------------------------------------------------------------ weak sweep (k_weak_coop)
 // Per pixel, a fixed part (tables, planes, header) and an nv-dependent tail.  The header the pooled
-// phases read from other pixels' blocks has named slots.
-struct WeakCarve {
+// phases read from other pixels' blocks has named slots.  PRE: the layout of the DPE_WEAK_PRE build,
+// whose refinement draws (12 floats, RND) reuse the alias rows once the cost vectors are shared
+// (ALIAS is dead from phase 3 on) plus 4 more floats; ALIAS and VWL trade places so that the 12
+// floats are contiguous.
+template <bool PRE>
+struct WeakCarveT {
   static constexpr int PW = 0;          // [108] Old-NCC patch (patch_lds_build)
   static constexpr int TC = 108;        // centre patch table, (w, w*grey) pairs [36][2]
   static constexpr int TN = 180;        // neighbour patch tables, pairs [8][9][2]
@@ -98,9 +102,10 @@ struct WeakCarve {
   static constexpr int NBOX_A = 449;    // nbox[0..2] (header)
   static constexpr int NSV = 452;       // [9] u32 selected views of the neighbours
   static constexpr int NBOX_B = 461;    // nbox[3] (header)
-  static constexpr int ALIAS = 464;     // [8] ints
-  static constexpr int VWL = 472;       // [32] u8 view weights
-  static constexpr int FIXED = 480;
+  static constexpr int ALIAS = PRE ? 472 : 464;   // [8] ints (phases 1b-3)
+  static constexpr int VWL = PRE ? 464 : 472;     // [32] u8 view weights
+  static constexpr int RND = 472;       // PRE: [12] refinement draws (phase 7), over ALIAS and 4 more floats
+  static constexpr int FIXED = PRE ? 484 : 480;
   // misc ints
   static constexpr int M_NSEL = 0, M_RADC = 1, M_INCC = 2, M_NC = 3, M_WNORM = 4, M_CMASK = 5, M_NB3 = 6, M_FLAGS = 8;
   // nv-dependent tail
@@ -111,28 +116,34 @@ struct WeakCarve {
   LDS_HD static constexpr int per_pixel(int nv) { return (FIXED + 17 * nv + 3) & ~3; }
 
   static constexpr bool ok(int nv) {
+    // ALIAS lies inside RND in the PRE layout (a deliberate reuse, listed as the one region RND)
     const Region r[] = {{PW, 108, 1},   {TC, 72, 1},      {TN, 144, 1},    {SUMS, 27, 1},       {RC, 1, 1},
                         {OSUM, 3, 1},   {CPL, 32, 4},     {HYP, 28, 4},    {FC, 8, 1},          {MISC, 16, 1},
-                        {NBL, 9, 1},    {NBOX_A, 3, 1},   {NSV, 9, 1},     {NBOX_B, 1, 1},      {ALIAS, 8, 1},
+                        {NBL, 9, 1},    {NBOX_A, 3, 1},   {NSV, 9, 1},     {NBOX_B, 1, 1},
+                        {PRE ? RND : ALIAS, PRE ? 12 : 8, 1},
                         {VWL, 8, 1},    {cost(nv), 8 * nv, 1}, {sp(nv), nv, 1}, {sel(nv), nv, 1}, {hv(nv), 7 * nv, 1}};
-    return regions_ok(r, per_pixel(nv)) && per_pixel(nv) % 4 == 0 && M_FLAGS + 8 <= 16;
+    return regions_ok(r, per_pixel(nv)) && per_pixel(nv) % 4 == 0 && M_FLAGS + 8 <= 16 &&
+           (!PRE || (ALIAS >= RND && ALIAS + 8 <= RND + 12));
   }
   static constexpr bool ok_all() {
     for (int nv = 1; nv <= kMaxViews; ++nv) if (!ok(nv)) return false;
     return true;
   }
 };
+using WeakCarve = WeakCarveT<false>;
 
 static_assert(StrongCarve<4, 16, 16>::ok_all(), "strong-sweep LDS carve (edge mode): overlap, alignment or bounds");
 static_assert(StrongCarve<8, 8, 16>::ok_all(), "strong-sweep LDS carve (ACMH mode): overlap, alignment or bounds");
-static_assert(WeakCarve::ok_all(), "weak-sweep LDS carve: overlap, alignment or bounds");
+static_assert(WeakCarveT<false>::ok_all(), "weak-sweep LDS carve: overlap, alignment or bounds");
+static_assert(WeakCarveT<true>::ok_all(), "weak-sweep LDS carve (DPE_WEAK_PRE): overlap, alignment or bounds");
 // LDS budgets (160 KB per CU on gfx950).  Strong sweep: 4 waves per workgroup at the largest view
 // count must fit one workgroup per CU at least (the dynamic-LDS attribute raises the 64 KB default).
 static_assert(4 * StrongCarve<4, 16, 16>::total(kMaxViews) * 4 <= 160 * 1024, "strong-sweep workgroup LDS (edge)");
 static_assert(4 * StrongCarve<8, 8, 16>::total(kMaxViews) * 4 <= 160 * 1024, "strong-sweep workgroup LDS (ACMH)");
 // Weak sweep: at the headline 9 source views four 4-wave workgroups of 4 pixels per wave must fit
 // a CU (4 resident waves per SIMD), i.e. <= 40 KB per workgroup.
-static_assert(4 * (4 * 4 * WeakCarve::per_pixel(9) * 4) <= 160 * 1024, "weak-sweep LDS: 4 workgroups per CU at 9 views");
+static_assert(4 * (4 * 4 * WeakCarveT<false>::per_pixel(9) * 4) <= 160 * 1024, "weak-sweep LDS: 4 workgroups per CU at 9 views");
+static_assert(4 * (4 * 4 * WeakCarveT<true>::per_pixel(9) * 4) <= 160 * 1024, "weak-sweep LDS (DPE_WEAK_PRE): 4 workgroups per CU at 9 views");
 
 }  // namespace lds
 }  // namespace dpe

@@ -954,7 +954,10 @@ DEV float ncc_new_tab(const PassConst& pc, const DevBufs& B, const WeakTab& T, i
 // LDS floats per weak pixel (lds_layout.h WeakCarve: fixed part, then [8][nv] costs, [nv] sampling
 // probabilities, [nv] selected views, [7][nv] hypothesis values; multiple of 4).  At 9 source views a
 // pixel takes 636 floats, so four 4-wave workgroups (4 x 40.7 KB) fit a CU's LDS.
-using WC = lds::WeakCarve;
+#ifndef DPE_WEAK_PRE
+#define DPE_WEAK_PRE 0   // 1: refinement draws on lanes 1..4 beside lane 0's acceptance (A/B)
+#endif
+using WC = lds::WeakCarveT<DPE_WEAK_PRE != 0>;
 constexpr int kWeakFixed = WC::FIXED;
 __host__ __device__ inline int weak_lds_per_pixel(int nv) { return WC::per_pixel(nv); }
 
@@ -1284,6 +1287,17 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
   float cost_now = 0.0f, cost_written = 0.0f, depth_now = 0.0f;
   float4 pnow = cur;
   const float dmin = pc.P.depth_min, dmax = pc.P.depth_max;
+  const float pert = (float)(0.02f * 3.14159265358979323846);
+#if DPE_WEAK_PRE
+  // lanes 1..4 evaluate the refinement draws (refine_draws: stream words 15.. after the view
+  // sampling) while lane 0 runs the acceptance; lane 0 then finishes the hypotheses from them
+  float* rnd = pb + WC::RND;
+  if (active && has_fit && c >= 1 && c <= 4) {
+    const RefineDraws d = refine_draws(rs, 15u);
+    if (c == 1) { rnd[0] = d.u_depth; rnd[1] = d.n[0]; rnd[2] = d.n[1]; rnd[3] = d.n[2]; rnd[4] = d.u_pert; }
+    else refine_angle(rs, d.w_angles, c - 2, pert, &rnd[5 + 2 * (c - 2)], &rnd[6 + 2 * (c - 2)]);
+  }
+#endif
   if (active && c == 0) {
     int mi = 0; float mcost = fc[0];
     for (int i = 1; i < 8; ++i) if (fc[i] <= mcost) { mcost = fc[i]; mi = i; }
@@ -1304,11 +1318,12 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
       tc /= wnorm;
       const float db = depth_from_plane(c0, fp, x, y);
       if (db >= dmin && db <= dmax && tc < cost_now) { depth_now = db; pnow = fp; cost_now = tc; }
+#if !DPE_WEAK_PRE
       const float depth_rand = rng_uniform(rs) * (dmax - dmin) + dmin;
       const float4 prand = random_normal(c0, x, y, rs, depth_now);
       const float dminp = (1 - 0.02f) * depth_now, dmaxp = (1 + 0.02f) * depth_now;
       const float depth_perturbed = rng_uniform(rs) * (dmaxp - dminp) + dminp;
-      const float4 ppert = perturbed_normal(c0, x, y, pnow, rs, (float)(0.02f * 3.14159265358979323846));
+      const float4 ppert = perturbed_normal(c0, x, y, pnow, rs, pert);
       float4 h0 = pnow, h1 = prand, h2 = prand, h3 = ppert, h4 = pnow;
       h0.w = dist2origin(c0, x, y, depth_rand, h0);
       h1.w = dist2origin(c0, x, y, depth_now, h1);
@@ -1316,8 +1331,26 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
       h3.w = dist2origin(c0, x, y, depth_now, h3);
       h4.w = dist2origin(c0, x, y, depth_perturbed, h4);
       hyp[0] = h0; hyp[1] = h1; hyp[2] = h2; hyp[3] = h3; hyp[4] = h4;
+#endif
     }
   }
+#if DPE_WEAK_PRE
+  wave_sync();
+  if (active && c == 0 && has_fit) {
+    const float depth_rand = rnd[0] * (dmax - dmin) + dmin;
+    const float4 prand = random_normal_from(c0, x, y, rnd + 1, depth_now);
+    const float dminp = (1 - 0.02f) * depth_now, dmaxp = (1 + 0.02f) * depth_now;
+    const float depth_perturbed = rnd[4] * (dmaxp - dminp) + dminp;
+    const float4 ppert = perturbed_normal_from(c0, x, y, pnow, rnd + 5);
+    float4 h0 = pnow, h1 = prand, h2 = prand, h3 = ppert, h4 = pnow;
+    h0.w = dist2origin(c0, x, y, depth_rand, h0);
+    h1.w = dist2origin(c0, x, y, depth_now, h1);
+    h2.w = dist2origin(c0, x, y, depth_rand, h2);
+    h3.w = dist2origin(c0, x, y, depth_now, h3);
+    h4.w = dist2origin(c0, x, y, depth_perturbed, h4);
+    hyp[0] = h0; hyp[1] = h1; hyp[2] = h2; hyp[3] = h3; hyp[4] = h4;
+  }
+#endif
   wave_sync();
   PHASE(7);
   // ---- phase 5: refinement NCCs, jobs (hypothesis, selected view)

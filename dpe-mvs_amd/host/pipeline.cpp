@@ -623,6 +623,8 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
         for (size_t k = 0; dev_ok && !failed && k < blocks[rank].size(); ++k)
           if (dpe_state_export_depth(runner.ctx, problems[blocks[rank][k]].ref_image_id, dsend + k * per, nullptr) != 0)
             fail(dpe_last_error());
+        // the exports run on the context's stream; the collective reads dsend from another one
+        if (dev_ok && !failed && dpe_sync(runner.ctx) != 0) fail(dpe_last_error());
         if (fault_at(0, rank)) fail("injected fault before the exchange");
         if (!status_exchange()) return 1;
         if (opt.allgather_device) {

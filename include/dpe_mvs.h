@@ -224,6 +224,9 @@ void dpe_state_clear(DpeContext* ctx);
  * context: the exchange buffers of the multi-rank schedule without HIP in the caller. */
 float* dpe_device_buffer(DpeContext* ctx, int slot, size_t count);
 int dpe_device_copy(DpeContext* ctx, void* dst, const void* src, size_t bytes, int kind);
+/* Blocks until every operation queued on the context (pass, state exports / imports) has finished,
+ * e.g. before a caller's collective reads a buffer an export filled.  DPE_OK or an error code. */
+int dpe_sync(DpeContext* ctx);
 
 /*
  * EdgeSegment's data-parallel stages on the device (DPE.cpp:129-291 calls them through OpenCV; the
