@@ -381,6 +381,11 @@ extern "C" void dpe_dbg_line_stats_main(unsigned long long out[16], int reset) {
   if (reset) { unsigned long long z[16] = {}; (void)hipMemcpyToSymbol(HIP_SYMBOL(dpe::g_lstat), z, sizeof(z)); }
 }
 #endif
+#if DPE_GN_TIMES
+extern "C" void dpe_dbg_gn_times(unsigned int* out, int n) {
+  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(dpe::g_gntime), sizeof(unsigned int) * (size_t)(n < (2 << 20) ? n : (2 << 20)));
+}
+#endif
 #if DPE_WEAK_STATS
 extern "C" void dpe_dbg_weak_stats(unsigned long long out[24], int reset) {
   (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(dpe::g_wstat), sizeof(dpe::g_wstat));

@@ -905,6 +905,24 @@ DEV float geom_cost_at(const PassConst& pc, const DevBufs& B, int px, int py, in
   const float cc = __builtin_sqrtf(dc * dc + dr * dr);
   return __builtin_fminf(3.0f, cc);
 }
+// geom_cost_at in two halves, so that a caller can issue the source-depth gather before other work
+// (same operations, same result): geom_fetch projects and loads, geom_finish completes
+struct GeomFetch { float2 sp; float depth; };
+DEV GeomFetch geom_fetch(const PassConst& pc, const DevBufs& B, int v, const float3& fw) {
+  GeomFetch g;
+  g.sp = project_cam(fw, pc.cams[v]);
+  g.depth = depth_texel(B.depth[v], pc.W, pc.H, g.sp.x, g.sp.y);
+  return g;
+}
+DEV float geom_finish(const PassConst& pc, const DevBufs& B, int px, int py, int v, const GeomFetch& g) {
+  if (B.cnt) atomicAdd(B.cnt + 2, 1ull);
+  if (g.depth == 0.0f) return 3.0f;
+  const float3 s3 = world_point(g.sp.x, g.sp.y, g.depth, pc.cams[v]);
+  const float2 bp = project_cam(s3, pc.cams[0]);
+  const float dc = (float)px - bp.x, dr = (float)py - bp.y;
+  const float cc = __builtin_sqrtf(dc * dc + dr * dr);
+  return __builtin_fminf(3.0f, cc);
+}
 DEV float geom_cost(const PassConst& pc, const DevBufs& B, int px, int py, int v, const float4& pl) {
   return geom_cost_at(pc, B, px, py, v, geom_point(pc, px, py, pl));
 }

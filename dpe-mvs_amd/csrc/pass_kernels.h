@@ -616,6 +616,20 @@ DEV bool bresenham_short(const PassConst& pc, const DevBufs& B, int Ax, int Ay, 
 #ifndef DPE_GN_MINW
 #define DPE_GN_MINW 1
 #endif
+// Per-pixel durations of the scratch-free GenNeighbours (build with -DDPE_GN_TIMES=1;
+// tools/gn_times.py): shader clocks from the start to the end of the probes and to the pixel's end,
+// at the pixel's list index (one wave = 64 consecutive indices).  Off in the product.
+#ifndef DPE_GN_TIMES
+#define DPE_GN_TIMES 0
+#endif
+#if DPE_GN_TIMES
+static __device__ uint32_t g_gntime[2 << 20];
+#define GN_T0() const uint64_t gn_t0_ = __builtin_readcyclecounter()
+#define GN_T(k) do { if (gi < (1 << 20)) g_gntime[2 * gi + (k)] = (uint32_t)(__builtin_readcyclecounter() - gn_t0_); } while (0)
+#else
+#define GN_T0() do {} while (0)
+#define GN_T(k) do {} while (0)
+#endif
 template <int K>
 __global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(const PassConst* __restrict__ pcp, DevBufs B,
                                                                   const int* __restrict__ list, const int* __restrict__ nlist_p,
@@ -638,6 +652,7 @@ __global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(c
   const DpeCamera& camera = pc.cams[0];
   Rng rs; rng_init(rs, (uint32_t)center, pc.seed32, STREAM_GEN_NEIGHBOURS, pc.salt);
   PHASE_BEGIN();
+  GN_T0();
   int valid_count = 0;
   bool overflow = false;
   auto push = [&](short2 np) {
@@ -816,8 +831,10 @@ __global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(c
     }
   }
   PHASE(1);
-  auto defer = [&]() { ovf[atomicAdd(novf, 1)] = center; PHASE_END_ALL(2); };
+  GN_T(0);
+  auto defer = [&]() { ovf[atomicAdd(novf, 1)] = center; PHASE_END_ALL(2); GN_T(1); };
   auto finish_fail = [&]() {
+    GN_T(1);
     if (complex_new >= 0.0f) B.complex_[center] = complex_new;
     short2* nb = B.nb + (size_t)center * 9;
     nb[0] = make_short2((short)x, (short)y);
@@ -1007,6 +1024,7 @@ __global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(c
   B.weak_rel[center] = 1;
   PHASE(4);
   PHASE_END_ALL(2);
+  GN_T(1);
 }
 
 // ------------------------------------------------------------------------------ NeigbourUpdate

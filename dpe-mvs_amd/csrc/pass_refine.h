@@ -330,6 +330,9 @@ DEV uint8_t d2w_class(const PassConst& pc, const float* pcs, uint64_t is_peak) {
 // depth maps, so doing LocalRefine right after the classification of the same pixel gives the
 // reference's results.  The 6-pixel border, where DepthToWeak stops at once (:2604-2607) but
 // LocalRefine runs, goes to k_local_refine_jobs over the border pixels (border_pixel).
+#ifndef DPE_GEOM_EARLY
+#define DPE_GEOM_EARLY 0   // 1: DepthToWeak issues the geometric term's depth gather before the NCC (A/B)
+#endif
 #ifndef DPE_FUSE_LR
 #define DPE_FUSE_LR 1
 #endif
@@ -404,12 +407,20 @@ __global__ void __launch_bounds__(64 * DPE_BW_D2W, DPE_D2W_WAVES) k_depth_to_wea
         const int vi = si - 1;
         if (isSet(sel, vi)) {
           float tcst = 0.0f;
+#if DPE_GEOM_EARLY   // the source-depth gather in flight during the NCC
+          GeomFetch gfe;
+          if (pc.P.geom_consistency) gfe = geom_fetch(pc, B, si, fw);
+#endif
           const float c = ncc_old_any<U8, DPE_D2W_ELIDE>(fast, pw, s_ref, s_rr, s_w, x, y, pc, B, si, tp);
           tcst += c;
           PHASE(1);
           if constexpr (LR) lr += (c * vw[vi]);                       // DPE.cu:2820
           if (pc.P.geom_consistency) {
+#if DPE_GEOM_EARLY
+            const float g = pc.P.geom_factor * geom_finish(pc, B, x, y, si, gfe);
+#else
             const float g = pc.P.geom_factor * geom_cost_at(pc, B, x, y, si, fw);
+#endif
             tcst += g;
             if constexpr (LR) lr += (g * vw[vi]);                     // :2822
           }

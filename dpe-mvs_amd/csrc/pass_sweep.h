@@ -292,7 +292,7 @@ DEV int acmh_candidate(const PassConst& pc, const float* __restrict__ costs, int
 #define DPE_TAIL_SPLIT 1
 #endif
 #ifndef DPE_STRONG_PRE
-#define DPE_STRONG_PRE 0   // 1: refinement draws on lanes 1..4 beside lane 0's acceptance (A/B)
+#define DPE_STRONG_PRE 1   // refinement draws on lanes 1..4 beside lane 0's acceptance (0: all on lane 0)
 #endif
 constexpr int kTailJobs = 16;   // a last round of at most this many jobs is split by patch rows
 // the strong sweep's LDS carve per wave (lds_layout.h: P pixels, C candidate lanes, nv source views)
@@ -955,7 +955,7 @@ DEV float ncc_new_tab(const PassConst& pc, const DevBufs& B, const WeakTab& T, i
 // probabilities, [nv] selected views, [7][nv] hypothesis values; multiple of 4).  At 9 source views a
 // pixel takes 636 floats, so four 4-wave workgroups (4 x 40.7 KB) fit a CU's LDS.
 #ifndef DPE_WEAK_PRE
-#define DPE_WEAK_PRE 0   // 1: refinement draws on lanes 1..4 beside lane 0's acceptance (A/B)
+#define DPE_WEAK_PRE 1   // refinement draws on lanes 1..4 beside lane 0's acceptance (0: all on lane 0)
 #endif
 using WC = lds::WeakCarveT<DPE_WEAK_PRE != 0>;
 constexpr int kWeakFixed = WC::FIXED;
