@@ -38,6 +38,19 @@ KERNEL(k_mul_hi, asm volatile("v_mul_hi_u32 %0, %0, %1" : "+v"(a[i]) : "v"(b)))
 KERNEL(k_mul_lo, asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(a[i]) : "v"(b)))
 KERNEL(k_mul_u24, asm volatile("v_mul_u32_u24 %0, %0, %1" : "+v"(a[i]) : "v"(b)))
 KERNEL(k_xor, asm volatile("v_xor_b32 %0, %0, %1" : "+v"(a[i]) : "v"(b)))
+// 32 x 32 -> 64-bit product (both halves of a Philox round's product in one instruction)
+__global__ void __launch_bounds__(256) k_mad64(float* out, float seed) {
+  unsigned long long a[CHAINS];
+  for (int i = 0; i < CHAINS; ++i) a[i] = (unsigned long long)(seed + threadIdx.x + i);
+  const unsigned b = (unsigned)seed | 1u;
+  for (int r = 0; r < REP; ++r) {
+#pragma unroll
+    for (int i = 0; i < CHAINS; ++i) asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(a[i]) : "v"((unsigned)a[i]), "v"(b) : "vcc");
+  }
+  unsigned long long s = 0;
+  for (int i = 0; i < CHAINS; ++i) s += a[i];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = (float)s;
+}
 KERNEL(k_xad, asm volatile("v_xad_u32 %0, %0, %1, %2" : "+v"(a[i]) : "v"(b), "v"(c)))
 KERNEL(k_sqrt, asm volatile("v_sqrt_f32 %0, %0" : "+v"(a[i])))
 KERNEL(k_cvt_u32, asm volatile("v_cvt_u32_f32 %0, %0" : "+v"(a[i])))
@@ -73,7 +86,7 @@ int main() {
       {"v_cvt_i32_f32", k_cvt_i32}, {"v_cvt_f32_ubyte0", k_cvt_ubyte}, {"v_lshrrev_b32", k_lshr},
       {"v_mad_u32_u24", k_mad24}, {"v_lshl_add_u32", k_lshl_add}, {"v_fma_mix_f32", k_fma_mix},
       {"v_rcp_f32", k_rcp}, {"v_and_b32", k_and}, {"v_cndmask_b32", k_cndmask},
-      {"v_mul_hi_u32", k_mul_hi}, {"v_mul_lo_u32", k_mul_lo}, {"v_mul_u32_u24", k_mul_u24}, {"v_xor_b32", k_xor},
+      {"v_mul_hi_u32", k_mul_hi}, {"v_mul_lo_u32", k_mul_lo}, {"v_mul_u32_u24", k_mul_u24}, {"v_xor_b32", k_xor}, {"v_mad_u64_u32", k_mad64},
       {"v_xad_u32", k_xad}, {"v_sqrt_f32", k_sqrt}, {"v_cvt_u32_f32", k_cvt_u32}, {"v_min_u32", k_min_u32},
       {"v_pk_fma_f32", k_pk_fma}, {"v_pk_mul_f32", k_pk_mul}, {"v_pk_add_f32", k_pk_add}};
   hipEvent_t e0, e1;
