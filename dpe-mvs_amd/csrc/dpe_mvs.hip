@@ -362,6 +362,10 @@ static void compute_pass_constants(PassConst& pc) {
   const double sr = tan((double)(angle / 2.0f) * M_PI / 180.0f) * 20;
   const int sri = (sr != sr) ? 0 : (int)sr;
   pc.gn_shift = sri < 1 ? 1 : sri;
+  // mul_hi(x, m) undershoots x / d by less than 1 for every 32-bit x (x (2^32 / d - m) / 2^32 < 1),
+  // so x - d mul_hi(x, m) lies in [0, 2d) and one conditional subtract gives x % d (gn_mod; checked
+  // for all 2^32 x and d <= 8 by tools/check_gn_mod.c)
+  pc.gn_shift_m = pc.gn_shift == 1 ? 0xFFFFFFFFu : (uint32_t)((1ull << 32) / (uint64_t)pc.gn_shift);
   pc.half_rows = std::min(pc.H, 2 * 16 * (((pc.H / 2) + 15) / 16));
 }
 
@@ -384,6 +388,9 @@ extern "C" void dpe_dbg_line_stats_main(unsigned long long out[16], int reset) {
 #if DPE_GN_TIMES
 extern "C" void dpe_dbg_gn_times(unsigned int* out, int n) {
   (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(dpe::g_gntime), sizeof(unsigned int) * (size_t)(n < (2 << 20) ? n : (2 << 20)));
+}
+extern "C" void dpe_dbg_gn_counts(unsigned int* out, int n) {
+  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(dpe::g_gncnt), sizeof(unsigned int) * (size_t)(n < (6 << 20) ? n : (6 << 20)));
 }
 #endif
 #if DPE_WEAK_STATS
@@ -644,7 +651,7 @@ static int stage_impl(DpeContext* c, const DpePassInput* in, const StageSrc& src
   HIPC(c->nb.ensure(L * 9)); HIPC(c->nearest.ensure(L)); HIPC(c->edge_neigh.ensure(L * 8)); HIPC(c->lab_bound.ensure(L * 8));
   HIPC(c->radius.ensure(L));
   HIPC(c->tab_right.ensure(L)); HIPC(c->tab_down.ensure(L));
-  HIPC(c->gn_ovf.ensure(L + 64)); HIPC(c->gn_tab.ensure((size_t)W + H));
+  HIPC(c->gn_ovf.ensure(L + 64)); HIPC(c->gn_tab.ensure((size_t)W + H + kGnTabExtra));
   HIPC(c->lists.ensure(6 * (L / 2 + 64) + 3 * (L + 64))); HIPC(c->row_counts.ensure(4 * (size_t)H + 4)); HIPC(c->list_totals.ensure(16));
   B.planes = c->planes.p; B.planes_snap = c->planes_snap.p; B.fit_plane = c->fit_plane.p;
   B.planes0 = c->planes0.p;
@@ -810,7 +817,7 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   auto gn_over = [&](const int* lst, const int* cnt) -> int {
 #if DPE_GN_LDS
     if (pc.P.rotate_time <= 4) {   // probe slots in the reference's compaction order (dir_index < 32)
-      if (!gn_tables) { k_gn_tables<<<(unsigned)((W + H + 255) / 256), 256, 0, a>>>(dpc, c->gn_tab.p); gn_tables = true; }
+      if (!gn_tables) { k_gn_tables<<<(unsigned)((W + H + 8 + 255) / 256), 256, 0, a>>>(dpc, c->gn_tab.p); gn_tables = true; }
       HIPC(hipMemsetAsync(c->list_totals.p + 6, 0, sizeof(int), a));
       const unsigned gg = (unsigned)((L + DPE_GN_BT - 1) / DPE_GN_BT);
       uint8_t* ec = nullptr;

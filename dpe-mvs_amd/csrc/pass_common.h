@@ -29,6 +29,7 @@ struct PassConst {
   float kinv0, kinv4, kc2, kc5;
   float gn_cos, gn_sin, gn_thr;
   int gn_shift;
+  uint32_t gn_shift_m;       // floor(2^32 / gn_shift) (2^32 - 1 for 1): x % gn_shift as a multiply (gn_mod)
   DpePatchMatchParams P;
   DpeCamera cams[DPE_MAX_IMAGES];
   ViewConst vc[DPE_MAX_IMAGES];

@@ -554,12 +554,59 @@ __global__ void __launch_bounds__(256, DPE_GN_WAVES) k_gen_neighbours(const Pass
 #define DPE_GN_SHORT 0   // 1: one-round-trip Bresenham walks for max_step <= 16 (more registers, slower)
 #endif
 // table of the normalised image coordinates: gtab[x] = (x - K[2]) / K[0], gtab[W + y] = (y - K[5]) / K[4]
+// + the direction walks' unit vectors (DPE.cu:2166-2190), pixel-independent: od of origin direction oi
+// after ri rotations at gtab[W + H + 2 (oi * 4 + ri)], and the attempt direction
+// normalize(20 od + (a, b)) for the shift residues a, b < gn_shift at
+// gtab[W + H + 64 + 2 (((oi * 4 + ri) * 8 + a) * 8 + b)]: the same operations as the per-attempt code
+constexpr int kGnDirOfs = 64, kGnTabExtra = 64 + 2 * 32 * 64;
 __global__ void k_gn_tables(const PassConst* __restrict__ pcp, float* __restrict__ gtab) {
   const PassConst& pc = *pcp;
   const DpeCamera& camera = pc.cams[0];
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < pc.W) gtab[i] = ((float)i - camera.K[2]) / camera.K[0];
   else if (i < pc.W + pc.H) gtab[i] = ((float)(i - pc.W) - camera.K[5]) / camera.K[4];
+  else if (i < pc.W + pc.H + 8 && pc.P.rotate_time <= 4) {
+    const int oi = i - pc.W - pc.H;
+    float* t = gtab + pc.W + pc.H;
+    const int k = oi < 4 ? oi : oi + 1;          // odx -1..1 outer, ody -1..1 inner, (0, 0) skipped
+    float2 od = make_float2((float)(k / 3 - 1), (float)(k % 3 - 1));
+    normalize2(od);
+    for (int ri = 0; ri < pc.P.rotate_time; ++ri) {
+      if (ri > 0) {
+        float2 rd = make_float2(od.x * pc.gn_cos - od.y * pc.gn_sin, od.x * pc.gn_sin + od.y * pc.gn_cos);
+        normalize2(rd);
+        od = rd;
+      }
+      t[2 * (oi * 4 + ri)] = od.x; t[2 * (oi * 4 + ri) + 1] = od.y;
+      for (int a = 0; a < pc.gn_shift && a < 8; ++a)
+        for (int b = 0; b < pc.gn_shift && b < 8; ++b) {
+          float2 dir = make_float2(od.x * 20 + (float)a, od.y * 20 + (float)b);
+          normalize2(dir);
+          float* d = t + kGnDirOfs + 2 * (((oi * 4 + ri) * 8 + a) * 8 + b);
+          d[0] = dir.x; d[1] = dir.y;
+        }
+    }
+  }
+}
+// x % gn_shift (DPE.cu:2182's `% shift`) as a multiply by the per-pass constant gn_shift_m
+DEV uint32_t gn_mod(const PassConst& pc, uint32_t x) {
+  const uint32_t d = (uint32_t)pc.gn_shift;
+  const uint32_t r = x - __umulhi(x, pc.gn_shift_m) * d;
+  return r >= d ? r - d : r;
+}
+// the angle test of a probe, td = normalize(np - p), td . od > thr (DPE.cu:2196-2199): decided from
+// an approximate reciprocal square root unless the approximate dot product lies within 1e-5 of thr
+// (its error is below 1e-6: |td|, |od| <= 1, v_rsq_f32 within 1 ulp), else from the exact one
+DEV bool gn_angle_ok(float dxf, float dyf, float2 od, float thr) {
+#if DPE_GN_FASTANGLE
+  const float n2 = dxf * dxf + dyf * dyf;
+  const float ia = __builtin_amdgcn_rsqf(n2);
+  const float caa = (dxf * ia) * od.x + (dyf * ia) * od.y;
+  if (__builtin_fabsf(caa - thr) > 1e-5f) return caa > thr;
+#endif
+  float2 td = make_float2(dxf, dyf);
+  normalize2(td);
+  return td.x * od.x + td.y * od.y > thr;
 }
 // BresenhamLine for walks of at most 16 steps per direction (high-resolution images: max_step =
 // round(max(LH, LW) / 60)): all positions of both directions generated first and their low-res edge
@@ -622,13 +669,29 @@ DEV bool bresenham_short(const PassConst& pc, const DevBufs& B, int Ax, int Ay, 
 #ifndef DPE_GN_TIMES
 #define DPE_GN_TIMES 0
 #endif
+// direction walks from the per-pass tables and a fast angle test (k_gn_tables, gn_angle_ok, gn_mod)
+#ifndef DPE_GN_DIRTAB
+#define DPE_GN_DIRTAB 0
+#endif
+#ifndef DPE_GN_FASTANGLE
+#define DPE_GN_FASTANGLE 0
+#endif
 #if DPE_GN_TIMES
+// + per-pixel counts: [0] radius steps of the direction walks, [1] Bresenham walks of the probes,
+// [2] RANSAC tries, [3] Bresenham walks of the RANSAC, [4] / [5] shader clocks in the probes' / the
+// RANSAC's Bresenham walks
 static __device__ uint32_t g_gntime[2 << 20];
-#define GN_T0() const uint64_t gn_t0_ = __builtin_readcyclecounter()
-#define GN_T(k) do { if (gi < (1 << 20)) g_gntime[2 * gi + (k)] = (uint32_t)(__builtin_readcyclecounter() - gn_t0_); } while (0)
+static __device__ uint32_t g_gncnt[6 << 20];
+#define GN_T0() const uint64_t gn_t0_ = __builtin_readcyclecounter(); uint32_t gn_c_[6] = {0, 0, 0, 0, 0, 0}
+#define GN_T(k) do { if (gi < (1 << 20)) { g_gntime[2 * gi + (k)] = (uint32_t)(__builtin_readcyclecounter() - gn_t0_); \
+                       if ((k) == 1) for (int q_ = 0; q_ < 6; ++q_) g_gncnt[6 * gi + q_] = gn_c_[q_]; } } while (0)
+#define GN_C(k, n) (gn_c_[k] += (n))
+#define GN_CLK() __builtin_readcyclecounter()
 #else
 #define GN_T0() do {} while (0)
 #define GN_T(k) do {} while (0)
+#define GN_C(k, n) do {} while (0)
+#define GN_CLK() 0ull
 #endif
 template <int K>
 __global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(const PassConst* __restrict__ pcp, DevBufs B,
@@ -701,6 +764,7 @@ __global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(c
     float2 od = origin_od(0);
     while (oi < 8) {
       bool next = radius > 4096;
+      GN_C(0, 1);
       if (!next) {
         const float tpx = (float)x + od.x * radius, tpy = (float)y + od.y * radius;
         if (tpx < 0 || tpy < 0 || tpx >= W || tpy >= H) next = true;
@@ -757,11 +821,18 @@ __global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(c
 #pragma unroll
           for (int q = 0; q < DPE_GNL_SPEC; ++q) {
             const uint32_t r1 = rng_u32(rs); const uint32_t r2 = rng_u32(rs);
-            const int rxs = (int)(((r1 % 2 == 0) ? 1u : 0xFFFFFFFFu) * r2 % (uint32_t)shift_range);
             const uint32_t r3 = rng_u32(rs); const uint32_t r4 = rng_u32(rs);
-            const int rys = (int)(((r3 % 2 == 0) ? 1u : 0xFFFFFFFFu) * r4 % (uint32_t)shift_range);
-            float2 dir = make_float2(od.x * 20 + (float)rxs, od.y * 20 + (float)rys);
-            normalize2(dir);
+            float2 dir;
+            if (DPE_GN_DIRTAB && shift_range <= 8) {   // the table holds residues < 8 only
+              const uint32_t rxs = gn_mod(pc, ((r1 % 2 == 0) ? 1u : 0xFFFFFFFFu) * r2);
+              const uint32_t rys = gn_mod(pc, ((r3 % 2 == 0) ? 1u : 0xFFFFFFFFu) * r4);
+              dir = ((const float2*)(gtab + W + H + kGnDirOfs))[((oi * 4 + ri) * 8 + rxs) * 8 + rys];
+            } else {
+              const int rxs = (int)(((r1 % 2 == 0) ? 1u : 0xFFFFFFFFu) * r2 % (uint32_t)shift_range);
+              const int rys = (int)(((r3 % 2 == 0) ? 1u : 0xFFFFFFFFu) * r4 % (uint32_t)shift_range);
+              dir = make_float2(od.x * 20 + (float)rxs, od.y * 20 + (float)rys);
+              normalize2(dir);
+            }
             const short2 np = make_short2((short)f2i((float)x + dir.x * radius), (short)f2i((float)y + dir.y * radius));
             inm[q] = !(np.x < min_margin || np.y < min_margin || np.x >= W - min_margin || np.y >= H - min_margin);
             const int npc = inm[q] ? np.x + np.y * W : center;
@@ -777,10 +848,12 @@ __global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(c
               np = nnv[q];
               if (np.x == -1 || np.y == -1) continue;
             }
-            float2 td = make_float2((float)(np.x - x), (float)(np.y - y));
-            normalize2(td);
-            const float ca = td.x * od.x + td.y * od.y;
-            if (ca > threshhold && (!edge_limit || !crosses(x, y, np.x, np.y))) {
+            const bool ang = gn_angle_ok((float)(np.x - x), (float)(np.y - y), od, threshhold);
+            if (ang && edge_limit) GN_C(1, 1);
+            const uint64_t gn_b0_ = GN_CLK(); (void)gn_b0_;
+            const bool pass_ = ang && (!edge_limit || !crosses(x, y, np.x, np.y));
+            GN_C(4, (uint32_t)(GN_CLK() - gn_b0_));
+            if (pass_) {
               push(np);
               dir_found = true;
               rng_seek(rs, pos0 + 4u * (uint32_t)(q + 1));
@@ -872,6 +945,7 @@ __global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(c
     bool must_in_triangle = (pc.P.use_label && B.label[center] > 0 && edge_limit) ? false : true;
     while (iteration > 0 && max_iter > 0) {
       max_iter--;
+      GN_C(2, 1);
       const int a = (int)(rng_u32(rs) % (uint32_t)valid_count);
       const int b = (int)(rng_u32(rs) % (uint32_t)valid_count);
       const int c = (int)(rng_u32(rs) % (uint32_t)valid_count);
@@ -894,9 +968,12 @@ __global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(c
           if (vbc) ebc = vbc == 2; else { ebc = crosses(pb.x, pb.y, pcc.x, pcc.y); *sbc = ebc ? 2 : 1; }
           if (vca) eca = vca == 2; else { eca = crosses(pcc.x, pcc.y, pa.x, pa.y); *sca = eca ? 2 : 1; }
         } else {
+          const uint64_t gn_b1_ = GN_CLK(); (void)gn_b1_;
           eab = crosses(pa.x, pa.y, pb.x, pb.y);
           ebc = crosses(pb.x, pb.y, pcc.x, pcc.y);
           eca = crosses(pcc.x, pcc.y, pa.x, pa.y);
+          GN_C(3, 3);
+          GN_C(5, (uint32_t)(GN_CLK() - gn_b1_));
         }
         if (eab || ebc || eca) continue;
       }

@@ -31,7 +31,7 @@ res = {path: [] for path in libs}
 ref = None
 for rnd in range(int(os.environ.get("AB_ROUNDS", "3"))):
     for path, lib, ctx, bufs in ctxs:
-        assert lib.dpe_pm_execute(ctx, None) == 0
+        assert lib.dpe_pm_execute(ctx, None) == 0, (path, lib.dpe_last_error())
         assert lib.dpe_pm_fetch(ctx, C.byref(bufs.st)) == 0
         out = b''.join(a.tobytes() for a in (bufs.planes, bufs.weak, bufs.sel, bufs.costs))
         if ref is None:
@@ -51,7 +51,7 @@ for rnd in range(int(os.environ.get("AB_ROUNDS", "3"))):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(5):
-            assert lib.dpe_pm_execute(ctx, None) == 0
+            assert lib.dpe_pm_execute(ctx, None) == 0, (path, lib.dpe_last_error())
         assert lib.dpe_pm_fetch(ctx, C.byref(bufs.st)) == 0
         torch.cuda.synchronize()
         wall[path].append((time.perf_counter() - t0) / 5 * 1e3)

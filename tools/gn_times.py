@@ -51,4 +51,15 @@ srt = np.sort(wmax)[::-1]
 for k in (1, 10, 100, 1000):
     if k <= srt.size:
         print(f"slowest {k:5d}-th wave: {srt[k - 1]:.3g} cycles")
+cb = (C.c_uint * (6 << 20))()
+lib.dpe_dbg_gn_counts(cb, 6 << 20)
+cnt = np.frombuffer(cb, dtype=np.uint32).reshape(-1, 6)[:m].astype(np.float64)
+names = ["radius steps", "probe Bresenham walks", "RANSAC tries", "RANSAC Bresenham walks",
+         "probe Bresenham clocks", "RANSAC Bresenham clocks"]
+nw = (m // 64) * 64
+for k, nm in enumerate(names):
+    v = cnt[:, k]
+    w = v[:nw].reshape(-1, 64)
+    util = w.sum() / max(1.0, 64 * w.max(1).sum())
+    print(f"{nm:24s} per pixel mean={v.mean():.1f}", q(v), f"| per wave max mean={w.max(1).mean():.1f} lane utilisation={util:.3f}")
 lib.dpe_destroy(ctx)
