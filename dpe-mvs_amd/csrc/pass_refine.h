@@ -104,8 +104,37 @@ DEV void taps36_at(const float* pw, int px, int py, f2v tmax, const uint8_t* bas
     }
     acc[0] = s_sr.x; acc[1] = s_ss; acc[2] = s_sr.y;
 }
-// Old NCC with the patch read from LDS (same arithmetic as ncc_old_patch36)
-template <int U8, bool FAST, bool IN = false>
+// row a of the generic (scalar) tap loop of lds_taps, added to the running sums in row order
+template <int U8, bool FAST>
+DEV void lds_taps_row(const float* pw, int px, int py, const PassConst& pc, const DevBufs& B, int v, const Homog& H, int a,
+                      float& s_src, float& s_ss, float& s_rs) {
+  const float x = (float)(px - 5 + 2 * a);
+  const float bx = __builtin_fmaf(H.h[0], x, H.h[2]) * kTexUnit;
+  const float by = __builtin_fmaf(H.h[3], x, H.h[5]) * kTexUnit;
+  const float bz = __builtin_fmaf(H.h[6], x, H.h[8]);
+  float r_src = 0, r_ss = 0, r_rs = 0;
+#pragma unroll
+  for (int b = 0; b < 6; ++b) {
+    const float y = (float)(py - 5 + 2 * b);
+    const float qx = __builtin_fmaf(H.h[1], y, bx);
+    const float qy = __builtin_fmaf(H.h[4], y, by);
+    const float iz = rcp_sel<FAST>(__builtin_fmaf(H.h[7], y, bz));
+    const float sp = sample_src<U8>(B, v, pc.W, pc.H, qx, qy, iz);
+    const float w = pw[2 * (a * 6 + b)], wr = pw[2 * (a * 6 + b) + 1];
+    r_src = __builtin_fmaf(w, sp, r_src);
+    const float ws = w * sp;
+    r_ss = __builtin_fmaf(ws, sp, r_ss);
+    r_rs = __builtin_fmaf(wr, sp, r_rs);
+  }
+  s_src += r_src; s_ss += r_ss; s_rs += r_rs;
+}
+#ifndef DPE_SLOW_ROWS
+#define DPE_SLOW_ROWS 0   // 1: every kernel's clamped / exact-reciprocal tap loop (rare) one patch row at a time
+#endif
+// Old NCC with the patch read from LDS (same arithmetic as ncc_old_patch36).  ROW1: the slow loop
+// (!FAST: a patch whose reciprocal range check failed) unrolled one row at a time, which lowers the
+// caller's register peak (same operations, same order)
+template <int U8, bool FAST, bool IN = false, bool ROW1 = false>
 DEV void lds_taps(const float* pw, int px, int py, const PassConst& pc, const DevBufs& B, int v, const Homog& H0,
                   float* acc) {
   const int W = pc.W, Hh = pc.H;
@@ -115,27 +144,12 @@ DEV void lds_taps(const float* pw, int px, int py, const PassConst& pc, const De
   } else {
     const Homog H = scale_cols(H0);
     float s_src = 0, s_ss = 0, s_rs = 0;
+    if constexpr (ROW1 || DPE_SLOW_ROWS) {
+#pragma unroll 1
+      for (int a = 0; a < 6; ++a) lds_taps_row<U8, FAST>(pw, px, py, pc, B, v, H, a, s_src, s_ss, s_rs);
+    } else {
 #pragma unroll
-    for (int a = 0; a < 6; ++a) {
-      const float x = (float)(px - 5 + 2 * a);
-      const float bx = __builtin_fmaf(H.h[0], x, H.h[2]) * kTexUnit;
-      const float by = __builtin_fmaf(H.h[3], x, H.h[5]) * kTexUnit;
-      const float bz = __builtin_fmaf(H.h[6], x, H.h[8]);
-      float r_src = 0, r_ss = 0, r_rs = 0;
-#pragma unroll
-      for (int b = 0; b < 6; ++b) {
-        const float y = (float)(py - 5 + 2 * b);
-        const float qx = __builtin_fmaf(H.h[1], y, bx);
-        const float qy = __builtin_fmaf(H.h[4], y, by);
-        const float iz = rcp_sel<FAST>(__builtin_fmaf(H.h[7], y, bz));
-        const float sp = sample_src<U8>(B, v, W, Hh, qx, qy, iz);
-        const float w = pw[2 * (a * 6 + b)], wr = pw[2 * (a * 6 + b) + 1];
-        r_src = __builtin_fmaf(w, sp, r_src);
-        const float ws = w * sp;
-        r_ss = __builtin_fmaf(ws, sp, r_ss);
-        r_rs = __builtin_fmaf(wr, sp, r_rs);
-      }
-      s_src += r_src; s_ss += r_ss; s_rs += r_rs;
+      for (int a = 0; a < 6; ++a) lds_taps_row<U8, FAST>(pw, px, py, pc, B, v, H, a, s_src, s_ss, s_rs);
     }
     acc[0] = s_src; acc[1] = s_ss; acc[2] = s_rs;
   }
@@ -211,13 +225,16 @@ DEV void lds_row(const float* pw, int px, int py, const PassConst& pc, const Dev
 #ifndef DPE_STRONG_ELIDE
 #define DPE_STRONG_ELIDE false
 #endif
+#ifndef DPE_D2W_ROW1
+#define DPE_D2W_ROW1 1   // DepthToWeak's slow tap loop one row at a time (lds_taps ROW1; A/B -0.3 ms)
+#endif
 #ifndef DPE_D2W_ELIDE
 #define DPE_D2W_ELIDE true
 #endif
 #ifndef DPE_LR_ELIDE
 #define DPE_LR_ELIDE false
 #endif
-template <int U8, bool ELIDE = false>
+template <int U8, bool ELIDE = false, bool ROW1 = false>
 DEV float ncc_old_lds(const float* pw, float s_ref, float s_rr, float s_w, int px, int py, const PassConst& pc,
                       const DevBufs& B, int v, const float4& pl) {
   const Homog H = make_homography(pc, v, pl);
@@ -250,16 +267,16 @@ DEV float ncc_old_lds(const float* pw, float s_ref, float s_rr, float s_w, int p
 #endif
       lds_taps<U8, true>(pw, px, py, pc, B, v, H, a);
   } else
-    lds_taps<U8, false>(pw, px, py, pc, B, v, H, a);
+    lds_taps<U8, false, false, ROW1>(pw, px, py, pc, B, v, H, a);
   return ncc_finalize_pre(s_ref, s_rr, s_w, a[0], a[1], a[2]);   // (inv, mref, var_ref) of patch_lds_pre
 }
 
 // ELIDE: try the clamp-free tap loop on patches that project inside the image (patch_inside); it
 // pays in DepthToWeak and the weak sweep, not in the strong sweep or LocalRefine (A/B).
-template <int U8, bool ELIDE = false>
+template <int U8, bool ELIDE = false, bool ROW1 = false>
 DEV float ncc_old_any(bool fast, const float* pw, float s_ref, float s_rr, float s_w, int px, int py,
                       const PassConst& pc, const DevBufs& B, int v, const float4& pl) {
-  if (fast) return ncc_old_lds<U8, ELIDE>(pw, s_ref, s_rr, s_w, px, py, pc, B, v, pl);
+  if (fast) return ncc_old_lds<U8, ELIDE, ROW1>(pw, s_ref, s_rr, s_w, px, py, pc, B, v, pl);
   return ncc_old_generic<U8>(pc, B, px, py, v, pl);
 }
 
@@ -411,7 +428,7 @@ __global__ void __launch_bounds__(64 * DPE_BW_D2W, DPE_D2W_WAVES) k_depth_to_wea
           GeomFetch gfe;
           if (pc.P.geom_consistency) gfe = geom_fetch(pc, B, si, fw);
 #endif
-          const float c = ncc_old_any<U8, DPE_D2W_ELIDE>(fast, pw, s_ref, s_rr, s_w, x, y, pc, B, si, tp);
+          const float c = ncc_old_any<U8, DPE_D2W_ELIDE, DPE_D2W_ROW1 != 0>(fast, pw, s_ref, s_rr, s_w, x, y, pc, B, si, tp);
           tcst += c;
           PHASE(1);
           if constexpr (LR) lr += (c * vw[vi]);                       // DPE.cu:2820

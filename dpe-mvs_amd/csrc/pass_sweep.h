@@ -731,6 +731,9 @@ struct WeakTab {
   float nbox[4];                          // x0, x1, y0, y1 of the union of the neighbour patches
 };
 
+#ifndef DPE_WEAK_ROWS
+#define DPE_WEAK_ROWS 8   // patch rows of tab_taps unrolled together (8: the whole patch)
+#endif
 // patch NCC with tabulated weights; the same tap order and arithmetic as patch_ncc_generic.
 // NN > 0: the patch side n is the compile-time NN, so the tap loop unrolls and the gathers of a
 // patch are in flight together (the weak sweep's patches are 3x3 and 4..6 square).
@@ -746,7 +749,7 @@ DEV void tab_taps(const PassConst& pc, const DevBufs& B, int v, const Homog& H0,
     const f2v tmax = tex_tmax2(W, Hh);
     f2v s_sr = f2s(0.0f);
     float s_ss = 0;
-#pragma unroll
+#pragma unroll DPE_WEAK_ROWS
     for (int a = 0; a < (NN > 0 ? NN : n); ++a) {
       const float xf = (float)(cx - rad + a * inc);
       const f2v bxy = fma2((f2v){H.h[0], H.h[3]}, f2s(xf), (f2v){H.h[2], H.h[5]}) * f2s(kTexUnit);
@@ -954,6 +957,19 @@ DEV float ncc_new_tab(const PassConst& pc, const DevBufs& B, const WeakTab& T, i
 // LDS floats per weak pixel (lds_layout.h WeakCarve: fixed part, then [8][nv] costs, [nv] sampling
 // probabilities, [nv] selected views, [7][nv] hypothesis values; multiple of 4).  At 9 source views a
 // pixel takes 636 floats, so four 4-wave workgroups (4 x 40.7 KB) fit a CU's LDS.
+#ifndef DPE_WEAK_OLD_ELIDE
+#define DPE_WEAK_OLD_ELIDE 1   // the final Old NCC with the clamp-free loop for patches inside the image
+                               // (its slow loop one row at a time, lds_taps ROW1: no scratch)
+#endif
+#ifndef DPE_WEAK_TBATCH
+#define DPE_WEAK_TBATCH 0   // patch weight tables filled 8 entries per lane at a time (loads batched)
+#endif
+#ifndef DPE_WEAK_SROWS
+#define DPE_WEAK_SROWS 0    // the centre patch's reference sums split by rows over lanes 0..5
+#endif
+#ifndef DPE_WEAK_GPOOL
+#define DPE_WEAK_GPOOL 0   // the final candidate costs' geometric terms as one wave pool (0: 8 lanes per pixel, serial)
+#endif
 #ifndef DPE_WEAK_PRE
 #define DPE_WEAK_PRE 1   // refinement draws on lanes 1..4 beside lane 0's acceptance (0: all on lane 0)
 #endif
@@ -1019,6 +1035,10 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
   T.n_n = T.rad_n >= 0 ? (2 * T.rad_n) / T.inc_n + 1 : 0;
   T.tab_c = T.n_c >= 1 && T.n_c <= 6;
   T.tab_n = T.n_n >= 1 && T.n_n <= 3;
+  // plain copies for the per-patch selects below: a select between two fields of T takes their
+  // addresses, which keeps T in scratch (24 B/lane) for the whole kernel
+  const int rad_c = T.rad_c, inc_c = T.inc_c, n_c = T.n_c, rad_n = T.rad_n, inc_n = T.inc_n, n_n = T.n_n;
+  const bool tab_c = T.tab_c, tab_n = T.tab_n;
   T.rc = active ? ref_texel(B.ref, W, Hh, x, y) : 0.0f;
   T.tc = tcp; T.tn = tnp; T.sums = sums; T.nbl = nbl; T.nsv = nsv;
   const short2* nbg = B.nb + (size_t)center * 9;
@@ -1051,12 +1071,40 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
       nbl[k] = np;
       nsv[k] = (np.x == -1 || np.y == -1) ? 0u : B.sel[np.x + np.y * W];
     }
-    const int ntc = T.tab_c ? T.n_c * T.n_c : 0, ntn = T.tab_n ? T.n_n * T.n_n : 0;
+    const int ntc = tab_c ? n_c * n_c : 0, ntn = tab_n ? n_n * n_n : 0;
     const float ss = pc.P.sigma_spatial, sc = pc.P.sigma_color;
+#if DPE_WEAK_TBATCH
+    // the same entries in batches of 8 per lane: neighbour pixels, then grey levels, then weights
+    // (two dependent loads per entry issued 8 at a time instead of one entry after another)
+    const int nt = ntc + 8 * ntn;
+    for (int t0 = c; t0 < nt; t0 += 8 * C) {
+      short2 npv[8]; int iv[8], jv[8], dv[8]; float rpv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int t = t0 + u * C;
+        int k = 0, tt = 0, n = 1, rad = 0, inc = 0;
+        if (t < ntc) { tt = t; n = n_c; rad = rad_c; inc = inc_c; }
+        else if (t < nt) { k = 1 + (t - ntc) / ntn; tt = (t - ntc) % ntn; n = n_n; rad = rad_n; inc = inc_n; }
+        iv[u] = -rad + (tt / n) * inc; jv[u] = -rad + (tt % n) * inc;
+        dv[u] = k == 0 ? 2 * tt : WC::TN - WC::TC + 2 * ((k - 1) * 9 + tt);   // float offset from tcp
+        npv[u] = t < nt ? nbg[k] : make_short2(-1, -1);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        rpv[u] = (npv[u].x == -1 || npv[u].y == -1) ? 0.0f : ref_texel(B.ref, W, Hh, npv[u].x + iv[u], npv[u].y + jv[u]);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (npv[u].x == -1 || npv[u].y == -1) continue;
+        const float w = bilateral_weight(iv[u], jv[u], rpv[u], T.rc, ss, sc);
+        float* dst = tcp + dv[u];
+        dst[0] = w; dst[1] = w * rpv[u];
+      }
+    }
+#else
     for (int t = c; t < ntc + 8 * ntn; t += C) {
       int k, tt, n, rad, inc;
-      if (t < ntc) { k = 0; tt = t; n = T.n_c; rad = T.rad_c; inc = T.inc_c; }
-      else { k = 1 + (t - ntc) / ntn; tt = (t - ntc) % ntn; n = T.n_n; rad = T.rad_n; inc = T.inc_n; }
+      if (t < ntc) { k = 0; tt = t; n = n_c; rad = rad_c; inc = inc_c; }
+      else { k = 1 + (t - ntc) / ntn; tt = (t - ntc) % ntn; n = n_n; rad = rad_n; inc = inc_n; }
       const short2 np = nbg[k];
       if (np.x == -1 || np.y == -1) continue;
       const int i = -rad + (tt / n) * inc, j = -rad + (tt % n) * inc;
@@ -1065,6 +1113,7 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
       float* dst = k == 0 ? tcp + 2 * tt : tnp + 2 * ((k - 1) * 9 + tt);
       dst[0] = w; dst[1] = w * rp;
     }
+#endif
     for (int i = c; i < 8; i += C) {
       const short2 np = nbg[i + 1];
       const bool fl = !(np.x == -1 || np.y == -1) && B.weak[np.x + np.y * W] == DPE_STRONG;
@@ -1091,16 +1140,37 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
     }
   }
   // ---- phase 1b: reference sums of every tabulated patch (tap order of patch_ncc_generic)
+  float cr_ref = 0.0f, cr_rr = 0.0f, cr_w = 0.0f;   // DPE_WEAK_SROWS: this lane's centre-patch row
+  (void)cr_ref; (void)cr_rr; (void)cr_w;
   if (active) {
     if (c == C - 2) {
       misc[WC::M_RADC] = T.rad_c; misc[WC::M_INCC] = T.inc_c; misc[WC::M_NC] = T.n_c; misc[WC::M_NB3] = T.nb3 ? 1 : 0;
       pb[WC::NBOX_A] = T.nbox[0]; pb[WC::NBOX_A + 1] = T.nbox[1]; pb[WC::NBOX_A + 2] = T.nbox[2]; pb[WC::NBOX_B] = T.nbox[3];
       pb[WC::RC] = T.rc;
     }
+#if DPE_WEAK_SROWS
+    // the centre patch's rows on lanes 0..5 (row sums combined in row order below), the 8 neighbour
+    // patches on lanes 6..13
+    if (c < 6) {
+      const short2 np = nbl[0];
+      if (!(np.x == -1 || np.y == -1) && tab_c && c < n_c) {
+        const int a = c;
+        for (int b = 0; b < n_c; ++b) {
+          const float rp = ref_texel(B.ref, W, Hh, np.x - rad_c + a * inc_c, np.y - rad_c + b * inc_c);
+          const float w = tcp[2 * (a * n_c + b)], wr = tcp[2 * (a * n_c + b) + 1];
+          cr_ref = cr_ref + wr;
+          cr_rr = __builtin_fmaf(wr, rp, cr_rr);
+          cr_w = cr_w + w;
+        }
+      }
+    }
+    for (int k = c - 5; k >= 1 && k < 9; k += C) {
+#else
     for (int k = c; k < 9; k += C) {
+#endif
       const short2 np = nbl[k];
-      if (np.x == -1 || np.y == -1 || !(k == 0 ? T.tab_c : T.tab_n)) continue;
-      const int n = k == 0 ? T.n_c : T.n_n, rad = k == 0 ? T.rad_c : T.rad_n, inc = k == 0 ? T.inc_c : T.inc_n;
+      if (np.x == -1 || np.y == -1 || !(k == 0 ? tab_c : tab_n)) continue;
+      const int n = k == 0 ? n_c : n_n, rad = k == 0 ? rad_c : rad_n, inc = k == 0 ? inc_c : inc_n;
       const float* tp = k == 0 ? tcp : tnp + (k - 1) * 18;
       float a_ref = 0, a_rr = 0, a_w = 0;
       for (int a = 0; a < n; ++a) {
@@ -1131,6 +1201,19 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
       alias[i] = a;
     }
   }
+#if DPE_WEAK_SROWS
+  {   // every lane: the pixel's centre rows 0..5 from lanes ps*C + a, added in row order on lane 0
+    float a_ref = 0, a_rr = 0, a_w = 0;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+      const int src = ps * C + a;
+      const float r0 = __shfl(cr_ref, src), r1 = __shfl(cr_rr, src), r2 = __shfl(cr_w, src);
+      if (a < n_c) { a_ref += r0; a_rr += r1; a_w += r2; }
+    }
+    if (active && c == 0 && tab_c && !(nbl[0].x == -1 || nbl[0].y == -1))
+      ncc_pre(a_ref, a_rr, a_w, sums[0], sums[1], sums[2]);
+  }
+#endif
   wave_sync();
   PHASE(1);
   // ---- phase 2: candidate cost vectors, jobs (unique flagged neighbour plane, view)
@@ -1145,7 +1228,7 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
     int Sj = 0;
 #pragma unroll
     for (int q = 0; q < P; ++q) {
-      pcnt[q] = wbase + q < nlist ? __builtin_popcount((uint32_t)((const int*)(pix(q) + 424))[5]) : 0;
+      pcnt[q] = wbase + q < nlist ? __builtin_popcount((uint32_t)((const int*)(pix(q) + WC::MISC))[WC::M_CMASK]) : 0;
       Sj += pcnt[q];
     }
     int q, r;
@@ -1237,9 +1320,9 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
     const float cn = ncc_new_tab<U8>(pc, B, tab_of(q), qx, qy, v, pl);
     return geom ? cn + gf * geom_cost(pc, B, qx, qy, v, pl) : cn;
   };
-  auto nsel_of = [&](int q) -> int { return wbase + q < nlist ? ((const int*)(pix(q) + 424))[0] : 0; };
+  auto nsel_of = [&](int q) -> int { return wbase + q < nlist ? ((const int*)(pix(q) + WC::MISC))[WC::M_NSEL] : 0; };
   auto fit_of = [&](int q) -> bool {
-    const float4 f = ((const float4*)(pix(q) + 388))[6];
+    const float4 f = ((const float4*)(pix(q) + WC::HYP))[6];
     return !(f.x == 0 && f.y == 0 && f.z == 0);
   };
   {
@@ -1254,6 +1337,30 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
       (qb + WC::hv(nv))[h * nv + k] = hyp_val_q(q, v, h ? ((const float4*)(qb + WC::HYP))[6] : B.planes[list[wbase + q]]);
     }
   }
+#if DPE_WEAK_GPOOL
+  // the final candidate costs' geometric terms, one pool of (pixel, candidate, selected view): each
+  // flagged candidate's cost[i][view] becomes cost + gf * geom in place (the same two roundings as
+  // the sum below would do), so the per-candidate sums only add
+  if (geom) {
+#pragma unroll
+    for (int q = 0; q < P; ++q) pcnt[q] = 8 * nsel_of(q);
+    int q, r;
+    for (int j = lane; job_decode<P>(pcnt, j, q, r); j += 64) {
+      float* qb = pix(q);
+      const int* qm = (const int*)(qb + WC::MISC);
+      const int ns = qm[WC::M_NSEL];
+      const int i = r / ns, k = r % ns;
+      if (!qm[WC::M_FLAGS + i]) continue;
+      const int vj = ((const int*)(qb + WC::sel(nv)))[k];
+      const int cq = list[wbase + q];
+      const int qx = cq % W, qy = cq / W;
+      float* cp = qb + WC::cost(nv) + i * nv + vj;
+      const float gterm = gf * geom_cost_at(pc, B, qx, qy, vj + 1, geom_point(pc, qx, qy, ((const float4*)(qb + WC::CPL))[i]));
+      *cp = *cp + gterm;
+    }
+  }
+  wave_sync();
+#endif
   if (active) {
 #else
   if (active) {
@@ -1265,13 +1372,20 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
 #endif
     for (int i = c; i < 8; i += C) {
       const bool fl = misc[WC::M_FLAGS + i] != 0;
-      const float3 fwi = (geom && fl) ? geom_point(pc, x, y, cpl[i]) : make_float3(0.0f, 0.0f, 0.0f);
+#if DPE_WEAK_POOL && DPE_WEAK_GPOOL
+      const bool gin = false;                            // geometric terms already in cost (pool above)
+      const float3 fwi = make_float3(0.0f, 0.0f, 0.0f);
+#else
+      const bool gin = geom && fl;
+      const float3 fwi = gin ? geom_point(pc, x, y, cpl[i]) : make_float3(0.0f, 0.0f, 0.0f);
+#endif
       float f = 0.0f;
       for (int j = 0; j < nv; ++j) {
         const int w = vwl[j];
         if (w > 0) {
           if (geom) {
-            if (fl) f += w * (cost[i * nv + j] + gf * geom_cost_at(pc, B, x, y, j + 1, fwi));
+            if (gin) f += w * (cost[i * nv + j] + gf * geom_cost_at(pc, B, x, y, j + 1, fwi));
+            else if (fl) f += w * cost[i * nv + j];
             else f += w * (cost[i * nv + j] + gf * 3.0f);
           } else {
             f += w * cost[i * nv + j];
@@ -1411,7 +1525,7 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
       float* qb = pix(q);
       const int cq = list[wbase + q];
       const int v = ((const int*)(qb + WC::sel(nv)))[r] + 1;
-      (qb + WC::hv(nv))[r] = ncc_old_any<U8, true>(fast_old, qb + WC::PW, qb[WC::OSUM], qb[WC::OSUM + 1], qb[WC::OSUM + 2], cq % W,
+      (qb + WC::hv(nv))[r] = ncc_old_any<U8, DPE_WEAK_OLD_ELIDE != 0, true>(fast_old, qb + WC::PW, qb[WC::OSUM], qb[WC::OSUM + 1], qb[WC::OSUM + 2], cq % W,
                                                    cq / W, pc, B, v, ((const float4*)(qb + WC::HYP))[5]);
     }
   }
@@ -1421,7 +1535,7 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
 #endif
     const float4 fin = hyp[5];
     for (int k = c; k < nsel; k += C)
-      hv[k] = ncc_old_any<U8, true>(fast_old, pw, osum[0], osum[1], osum[2], x, y, pc, B, sel_list[k] + 1, fin);
+      hv[k] = ncc_old_any<U8, DPE_WEAK_OLD_ELIDE != 0, true>(fast_old, pw, osum[0], osum[1], osum[2], x, y, pc, B, sel_list[k] + 1, fin);
   }
   wave_sync();
   PHASE(10);
