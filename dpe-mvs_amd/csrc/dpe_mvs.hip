@@ -367,6 +367,7 @@ static void compute_pass_constants(PassConst& pc) {
   // for all 2^32 x and d <= 8 by tools/check_gn_mod.c)
   pc.gn_shift_m = pc.gn_shift == 1 ? 0xFFFFFFFFu : (uint32_t)((1ull << 32) / (uint64_t)pc.gn_shift);
   pc.half_rows = std::min(pc.H, 2 * 16 * (((pc.H / 2) + 15) / 16));
+  pc.weak_nn = pc.P.weak_radius >= 0 && pc.P.weak_increment > 0 ? (2 * pc.P.weak_radius) / pc.P.weak_increment + 1 : 0;
 }
 
 // where a stage takes the initial state and the source depths from: host buffers (dpe_pm_stage) or

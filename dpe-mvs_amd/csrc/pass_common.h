@@ -30,6 +30,7 @@ struct PassConst {
   float gn_cos, gn_sin, gn_thr;
   int gn_shift;
   uint32_t gn_shift_m;       // floor(2^32 / gn_shift) (2^32 - 1 for 1): x % gn_shift as a multiply (gn_mod)
+  int weak_nn;               // side of the weak sweep's neighbour patches, (2 weak_radius) / weak_increment + 1 (0 if radius < 0)
   DpePatchMatchParams P;
   DpeCamera cams[DPE_MAX_IMAGES];
   ViewConst vc[DPE_MAX_IMAGES];

@@ -961,6 +961,12 @@ DEV float ncc_new_tab(const PassConst& pc, const DevBufs& B, const WeakTab& T, i
 #define DPE_WEAK_OLD_ELIDE 1   // the final Old NCC with the clamp-free loop for patches inside the image
                                // (its slow loop one row at a time, lds_taps ROW1: no scratch)
 #endif
+#ifndef DPE_WEAK_TPC
+#define DPE_WEAK_TPC 0      // pooled jobs read the neighbour-patch parameters from the pass constants
+#endif
+#ifndef DPE_WEAK_TCOPY
+#define DPE_WEAK_TCOPY 1    // plain copies of the patch parameters for the per-patch selects (no scratch for T)
+#endif
 #ifndef DPE_WEAK_TBATCH
 #define DPE_WEAK_TBATCH 0   // patch weight tables filled 8 entries per lane at a time (loads batched)
 #endif
@@ -1037,8 +1043,13 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
   T.tab_n = T.n_n >= 1 && T.n_n <= 3;
   // plain copies for the per-patch selects below: a select between two fields of T takes their
   // addresses, which keeps T in scratch (24 B/lane) for the whole kernel
+#if DPE_WEAK_TCOPY
   const int rad_c = T.rad_c, inc_c = T.inc_c, n_c = T.n_c, rad_n = T.rad_n, inc_n = T.inc_n, n_n = T.n_n;
   const bool tab_c = T.tab_c, tab_n = T.tab_n;
+#else   // references: the selects below take field addresses and keep T in scratch (the round-3 code)
+  const int &rad_c = T.rad_c, &inc_c = T.inc_c, &n_c = T.n_c, &rad_n = T.rad_n, &inc_n = T.inc_n, &n_n = T.n_n;
+  const bool &tab_c = T.tab_c, &tab_n = T.tab_n;
+#endif
   T.rc = active ? ref_texel(B.ref, W, Hh, x, y) : 0.0f;
   T.tc = tcp; T.tn = tnp; T.sums = sums; T.nbl = nbl; T.nsv = nsv;
   const short2* nbg = B.nb + (size_t)center * 9;
@@ -1051,7 +1062,13 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
     const int* h = (const int*)(qb + WC::MISC);
     WeakTab t;
     t.rad_c = h[WC::M_RADC]; t.inc_c = h[WC::M_INCC]; t.n_c = h[WC::M_NC]; t.nb3 = h[WC::M_NB3] != 0;
+#if DPE_WEAK_TPC
+    // the neighbour-patch parameters are pass constants: scalar loads here instead of registers
+    // held across the pools
+    t.rad_n = pc.P.weak_radius; t.inc_n = pc.P.weak_increment; t.n_n = pc.weak_nn; t.tab_n = t.n_n >= 1 && t.n_n <= 3;
+#else
     t.rad_n = T.rad_n; t.inc_n = T.inc_n; t.n_n = T.n_n; t.tab_n = T.tab_n;
+#endif
     t.tab_c = t.n_c >= 1 && t.n_c <= 6;
     t.rc = qb[WC::RC];
     t.nbox[0] = qb[WC::NBOX_A]; t.nbox[1] = qb[WC::NBOX_A + 1]; t.nbox[2] = qb[WC::NBOX_A + 2]; t.nbox[3] = qb[WC::NBOX_B];

@@ -13,7 +13,8 @@ for path in glob.glob(sys.argv[1] + "/g*/run_counter_collection.csv"):
         k = re.sub(r"\(.*", "", r["Kernel_Name"]).replace("dpe::", "").replace("void ", "")
         name = r["Counter_Name"]
         res[k][name if name != "GRBM_GUI_ACTIVE" else "GUI_" + g] += float(r["Counter_Value"])
-keys = ["k_strong_coop<3, true>", "k_strong_coop<2, true>", "k_depth_to_weak<2>", "k_depth_to_weak_cols<2>", "k_weak_coop<1, 16>", "k_local_refine_jobs<2>", "k_gen_neighbours",
+keys = ["k_strong_coop<3, true>", "k_strong_coop<2, true>", "k_depth_to_weak<2>", "k_depth_to_weak<2, true>", "k_depth_to_weak_cols<2>",
+        "k_weak_coop<1, 16>", "k_local_refine_jobs<2>", "k_gen_neighbours_lds<32>", "k_gen_neighbours",
         "k_random_init<2>", "k_ransac_fit", "k_gen_edge_inform"]
 for k in keys:
     d = res.get(k)
