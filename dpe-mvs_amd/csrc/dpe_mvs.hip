@@ -141,6 +141,7 @@ struct DpeContext {
   bool img8 = false;                 // all images are 8-bit grey levels -> u8 quad layout
   DevArr<float> depth[DPE_MAX_IMAGES];
   DevArr<uint8_t> edge, edge_low;
+  DevArr<uint64_t> edge_tiles;
   DevArr<int> label;
   // staged initial state
   DevArr<float4> planes0;
@@ -287,7 +288,7 @@ void dpe_destroy(DpeContext* c) {
   c->imgq8_all.release();
   c->imgq16_all.release();
   c->imgqp_all.release();
-  c->edge.release(); c->edge_low.release(); c->label.release();
+  c->edge.release(); c->edge_low.release(); c->edge_tiles.release(); c->label.release();
   c->planes0.release(); c->weak0.release(); c->sel0.release();
   c->planes.release(); c->planes_snap.release(); c->fit_plane.release();
   c->costs.release(); c->costs_snap.release(); c->complex_.release();
@@ -619,6 +620,15 @@ static int stage_impl(DpeContext* c, const DpePassInput* in, const StageSrc& src
     HIPC(hipMemcpyAsync(c->edge.p, in->edge, L, hipMemcpyHostToDevice, c->stream));
     HIPC(hipMemcpyAsync(c->edge_low.p, in->edge_low_res, (size_t)pc.LW * pc.LH, hipMemcpyHostToDevice, c->stream));
     B.edge = c->edge.p; B.edge_low = c->edge_low.p;
+#if DPE_BRES_TILE
+    {   // 8x8 bit tiles of the low-res map for the Bresenham walks (bresenham, DPE_BRES_TILE)
+      const int tw = (pc.LW + 7) / 8, th = (pc.LH + 7) / 8;
+      HIPC(c->edge_tiles.ensure((size_t)tw * th));
+      k_edge_tiles<<<(unsigned)((tw * th + 255) / 256), 256, 0, c->stream>>>(c->edge_low.p, pc.LW, pc.LH, c->edge_tiles.p);
+      HIPC(hipGetLastError());
+      B.edge_tiles = c->edge_tiles.p;
+    }
+#endif
     HIPC(hipMemcpyAsync(c->dc.p, &pc, sizeof(PassConst), hipMemcpyHostToDevice, c->stream));
   }
   if (P.use_label) {

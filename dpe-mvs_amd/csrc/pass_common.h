@@ -16,6 +16,7 @@
 //   nearest, edge_neigh[8], lab_bound[8] short2 per pixel; complex f32, radius i32, fit float4
 #pragma once
 #include "device_math.h"
+#include "bres_walk.h"
 #include "../../include/dpe_mvs.h"
 
 namespace dpe {
@@ -53,6 +54,7 @@ struct DevBufs {
   short2* nb; short2* nearest; short2* edge_neigh; short2* lab_bound;
   int* radius;
   const uint8_t* edge; const uint8_t* edge_low; const int* label;
+  const uint64_t* edge_tiles;   // low-res edge map as 8x8 bit tiles (DPE_BRES_TILE), bit (y & 7) * 8 + (x & 7)
   // algorithmic work counters of the launch class (nullptr unless counting):
   // [0] homographies (NCC set-ups), [1] bilinear taps, [2] geometric-consistency evaluations
   unsigned long long* cnt;
@@ -941,6 +943,12 @@ DEV uint8_t low_edge_at(const PassConst& pc, const DevBufs& B, int idx) {
 #ifndef DPE_BRES_BATCH
 #define DPE_BRES_BATCH 8
 #endif
+#ifndef DPE_BRES_TILE
+#define DPE_BRES_TILE 0     // walks tested against 8x8 bit tiles of the map (bres_walk.h walk_tiles)
+#endif
+#ifndef DPE_BRES_TILES
+#define DPE_BRES_TILES 4    // tiles loaded per round trip of walk_tiles
+#endif
 DEV bool bresenham(const PassConst& pc, const DevBufs& B, int Ax, int Ay, int Bx, int By) {
   const int W = pc.W;
   if (B.edge[Ax + Ay * W] || B.edge[Bx + By * W]) return false;
@@ -951,38 +959,16 @@ DEV bool bresenham(const PassConst& pc, const DevBufs& B, int Ax, int Ay, int Bx
   for (int pass = 0; pass < 2; ++pass) {
     const int fx = pass == 0 ? Bx : Ax, fy = pass == 0 ? By : Ay;
     const int tx = pass == 0 ? Ax : Bx, ty = pass == 0 ? Ay : By;
-    int x0 = (int)MINo(__builtin_roundf(fx * scale_x), (float)(width - 1));
-    int y0 = (int)MINo(__builtin_roundf(fy * scale_y), (float)(height - 1));
+    const int x0 = (int)MINo(__builtin_roundf(fx * scale_x), (float)(width - 1));
+    const int y0 = (int)MINo(__builtin_roundf(fy * scale_y), (float)(height - 1));
     const int x1 = (int)MINo(__builtin_roundf(tx * scale_x), (float)(width - 1));
     const int y1 = (int)MINo(__builtin_roundf(ty * scale_y), (float)(height - 1));
-    const int dx = abs(x1 - x0), sx = x0 < x1 ? 1 : -1;
-    const int dy = abs(y1 - y0), sy = y0 < y1 ? 1 : -1;
-    int erro = (dx > dy ? dx : dy) / 2;
-    int step = 0;
-    bool tagx = true, tagy = true, more = true;
-    while (more) {
-      int idx[DPE_BRES_BATCH];
-#pragma unroll
-      for (int k = 0; k < DPE_BRES_BATCH; ++k) {
-        idx[k] = -1;                                  // low_edge_at(-1) == 0
-        if (more && (tagx || tagy)) {
-          if (x0 == x1) tagx = false;
-          if (y0 == y1) tagy = false;
-          const int e2 = erro;
-          if (e2 > -dx) { erro -= dy; x0 += sx; }
-          if (e2 < dy) { erro += dx; y0 += sy; }
-          idx[k] = x0 + y0 * width;
-          step += 1;
-          if (step >= max_step) more = false;
-        } else {
-          more = false;
-        }
-      }
-      uint8_t hit = 0;
-#pragma unroll
-      for (int k = 0; k < DPE_BRES_BATCH; ++k) hit |= low_edge_at(pc, B, idx[k]);
-      if (hit) return true;
-    }
+    const bres::Walk w = bres::start(x0, y0, x1, y1, max_step);
+#if DPE_BRES_TILE
+    if (bres::walk_tiles<DPE_BRES_TILES>(w, B.edge_tiles, width, height)) return true;
+#else
+    if (bres::walk_bytes<DPE_BRES_BATCH>(w, B.edge_low, width, height)) return true;
+#endif
   }
   return false;
 }

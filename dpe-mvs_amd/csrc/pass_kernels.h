@@ -553,6 +553,15 @@ __global__ void __launch_bounds__(256, DPE_GN_WAVES) k_gen_neighbours(const Pass
 #ifndef DPE_GN_SHORT
 #define DPE_GN_SHORT 0   // 1: one-round-trip Bresenham walks for max_step <= 16 (more registers, slower)
 #endif
+// 8x8 bit tiles of the low-res edge map (bresenham with DPE_BRES_TILE): one thread per tile
+__global__ void k_edge_tiles(const uint8_t* __restrict__ e, int w, int h, uint64_t* __restrict__ tiles) {
+  const int tw = (w + 7) / 8, th = (h + 7) / 8;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= tw * th) return;
+  uint64_t m;
+  bres::build_tile(e, w, h, i, m);
+  tiles[i] = m;
+}
 // table of the normalised image coordinates: gtab[x] = (x - K[2]) / K[0], gtab[W + y] = (y - K[5]) / K[4]
 // + the direction walks' unit vectors (DPE.cu:2166-2190), pixel-independent: od of origin direction oi
 // after ri rotations at gtab[W + H + 2 (oi * 4 + ri)], and the attempt direction

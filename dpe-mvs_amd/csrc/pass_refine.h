@@ -149,7 +149,27 @@ DEV void lds_taps(const float* pw, int px, int py, const PassConst& pc, const De
       for (int a = 0; a < 6; ++a) lds_taps_row<U8, FAST>(pw, px, py, pc, B, v, H, a, s_src, s_ss, s_rs);
     } else {
 #pragma unroll
-      for (int a = 0; a < 6; ++a) lds_taps_row<U8, FAST>(pw, px, py, pc, B, v, H, a, s_src, s_ss, s_rs);
+      for (int a = 0; a < 6; ++a) {
+        const float x = (float)(px - 5 + 2 * a);
+        const float bx = __builtin_fmaf(H.h[0], x, H.h[2]) * kTexUnit;
+        const float by = __builtin_fmaf(H.h[3], x, H.h[5]) * kTexUnit;
+        const float bz = __builtin_fmaf(H.h[6], x, H.h[8]);
+        float r_src = 0, r_ss = 0, r_rs = 0;
+#pragma unroll
+        for (int b = 0; b < 6; ++b) {
+          const float y = (float)(py - 5 + 2 * b);
+          const float qx = __builtin_fmaf(H.h[1], y, bx);
+          const float qy = __builtin_fmaf(H.h[4], y, by);
+          const float iz = rcp_sel<FAST>(__builtin_fmaf(H.h[7], y, bz));
+          const float sp = sample_src<U8>(B, v, W, Hh, qx, qy, iz);
+          const float w = pw[2 * (a * 6 + b)], wr = pw[2 * (a * 6 + b) + 1];
+          r_src = __builtin_fmaf(w, sp, r_src);
+          const float ws = w * sp;
+          r_ss = __builtin_fmaf(ws, sp, r_ss);
+          r_rs = __builtin_fmaf(wr, sp, r_rs);
+        }
+        s_src += r_src; s_ss += r_ss; s_rs += r_rs;
+      }
     }
     acc[0] = s_src; acc[1] = s_ss; acc[2] = s_rs;
   }

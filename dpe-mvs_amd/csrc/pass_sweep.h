@@ -731,9 +731,6 @@ struct WeakTab {
   float nbox[4];                          // x0, x1, y0, y1 of the union of the neighbour patches
 };
 
-#ifndef DPE_WEAK_ROWS
-#define DPE_WEAK_ROWS 8   // patch rows of tab_taps unrolled together (8: the whole patch)
-#endif
 // patch NCC with tabulated weights; the same tap order and arithmetic as patch_ncc_generic.
 // NN > 0: the patch side n is the compile-time NN, so the tap loop unrolls and the gathers of a
 // patch are in flight together (the weak sweep's patches are 3x3 and 4..6 square).
@@ -749,7 +746,7 @@ DEV void tab_taps(const PassConst& pc, const DevBufs& B, int v, const Homog& H0,
     const f2v tmax = tex_tmax2(W, Hh);
     f2v s_sr = f2s(0.0f);
     float s_ss = 0;
-#pragma unroll DPE_WEAK_ROWS
+#pragma unroll
     for (int a = 0; a < (NN > 0 ? NN : n); ++a) {
       const float xf = (float)(cx - rad + a * inc);
       const f2v bxy = fma2((f2v){H.h[0], H.h[3]}, f2s(xf), (f2v){H.h[2], H.h[5]}) * f2s(kTexUnit);
@@ -961,11 +958,14 @@ DEV float ncc_new_tab(const PassConst& pc, const DevBufs& B, const WeakTab& T, i
 #define DPE_WEAK_OLD_ELIDE 1   // the final Old NCC with the clamp-free loop for patches inside the image
                                // (its slow loop one row at a time, lds_taps ROW1: no scratch)
 #endif
+#ifndef DPE_WEAK_ROW1
+#define DPE_WEAK_ROW1 0     // the final Old NCC's slow tap loop one row at a time (lds_taps ROW1)
+#endif
 #ifndef DPE_WEAK_TPC
 #define DPE_WEAK_TPC 0      // pooled jobs read the neighbour-patch parameters from the pass constants
 #endif
 #ifndef DPE_WEAK_TCOPY
-#define DPE_WEAK_TCOPY 1    // plain copies of the patch parameters for the per-patch selects (no scratch for T)
+#define DPE_WEAK_TCOPY 0    // plain copies of the patch parameters for the per-patch selects (no scratch for T)
 #endif
 #ifndef DPE_WEAK_TBATCH
 #define DPE_WEAK_TBATCH 0   // patch weight tables filled 8 entries per lane at a time (loads batched)
@@ -1390,20 +1390,23 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
     for (int i = c; i < 8; i += C) {
       const bool fl = misc[WC::M_FLAGS + i] != 0;
 #if DPE_WEAK_POOL && DPE_WEAK_GPOOL
-      const bool gin = false;                            // geometric terms already in cost (pool above)
-      const float3 fwi = make_float3(0.0f, 0.0f, 0.0f);
+      float f = 0.0f;                                    // geometric terms already in cost (pool above)
+      for (int j = 0; j < nv; ++j) {
+        const int w = vwl[j];
+        if (w > 0) {
+          if (geom) {
+            if (fl) f += w * cost[i * nv + j];
+            else f += w * (cost[i * nv + j] + gf * 3.0f);
 #else
-      const bool gin = geom && fl;
-      const float3 fwi = gin ? geom_point(pc, x, y, cpl[i]) : make_float3(0.0f, 0.0f, 0.0f);
-#endif
+      const float3 fwi = (geom && fl) ? geom_point(pc, x, y, cpl[i]) : make_float3(0.0f, 0.0f, 0.0f);
       float f = 0.0f;
       for (int j = 0; j < nv; ++j) {
         const int w = vwl[j];
         if (w > 0) {
           if (geom) {
-            if (gin) f += w * (cost[i * nv + j] + gf * geom_cost_at(pc, B, x, y, j + 1, fwi));
-            else if (fl) f += w * cost[i * nv + j];
+            if (fl) f += w * (cost[i * nv + j] + gf * geom_cost_at(pc, B, x, y, j + 1, fwi));
             else f += w * (cost[i * nv + j] + gf * 3.0f);
+#endif
           } else {
             f += w * cost[i * nv + j];
           }
@@ -1542,7 +1545,7 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
       float* qb = pix(q);
       const int cq = list[wbase + q];
       const int v = ((const int*)(qb + WC::sel(nv)))[r] + 1;
-      (qb + WC::hv(nv))[r] = ncc_old_any<U8, DPE_WEAK_OLD_ELIDE != 0, true>(fast_old, qb + WC::PW, qb[WC::OSUM], qb[WC::OSUM + 1], qb[WC::OSUM + 2], cq % W,
+      (qb + WC::hv(nv))[r] = ncc_old_any<U8, DPE_WEAK_OLD_ELIDE != 0, DPE_WEAK_ROW1 != 0>(fast_old, qb + WC::PW, qb[WC::OSUM], qb[WC::OSUM + 1], qb[WC::OSUM + 2], cq % W,
                                                    cq / W, pc, B, v, ((const float4*)(qb + WC::HYP))[5]);
     }
   }
@@ -1552,7 +1555,7 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
 #endif
     const float4 fin = hyp[5];
     for (int k = c; k < nsel; k += C)
-      hv[k] = ncc_old_any<U8, DPE_WEAK_OLD_ELIDE != 0, true>(fast_old, pw, osum[0], osum[1], osum[2], x, y, pc, B, sel_list[k] + 1, fin);
+      hv[k] = ncc_old_any<U8, DPE_WEAK_OLD_ELIDE != 0, DPE_WEAK_ROW1 != 0>(fast_old, pw, osum[0], osum[1], osum[2], x, y, pc, B, sel_list[k] + 1, fin);
   }
   wave_sync();
   PHASE(10);
