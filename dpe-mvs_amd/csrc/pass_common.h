@@ -963,11 +963,10 @@ DEV bool bresenham(const PassConst& pc, const DevBufs& B, int Ax, int Ay, int Bx
     const int y0 = (int)MINo(__builtin_roundf(fy * scale_y), (float)(height - 1));
     const int x1 = (int)MINo(__builtin_roundf(tx * scale_x), (float)(width - 1));
     const int y1 = (int)MINo(__builtin_roundf(ty * scale_y), (float)(height - 1));
-    const bres::Walk w = bres::start(x0, y0, x1, y1, max_step);
 #if DPE_BRES_TILE
-    if (bres::walk_tiles<DPE_BRES_TILES>(w, B.edge_tiles, width, height)) return true;
+    if (bres::walk_tiles<DPE_BRES_TILES>(bres::start(x0, y0, x1, y1, max_step), B.edge_tiles, width, height)) return true;
 #else
-    if (bres::walk_bytes<DPE_BRES_BATCH>(w, B.edge_low, width, height)) return true;
+    if (bres::walk_bytes_flat<DPE_BRES_BATCH>(x0, y0, x1, y1, max_step, B.edge_low, width, height)) return true;
 #endif
   }
   return false;

@@ -675,6 +675,66 @@ DEV bool bresenham_short(const PassConst& pc, const DevBufs& B, int Ax, int Ay, 
 // Per-pixel durations of the scratch-free GenNeighbours (build with -DDPE_GN_TIMES=1;
 // tools/gn_times.py): shader clocks from the start to the end of the probes and to the pixel's end,
 // at the pixel's list index (one wave = 64 consecutive indices).  Off in the product.
+// GenNeighbours' probe walks shared by the wave (DPE_GN_COOP): every lane of the wave calls this
+// with the same control flow; the lanes with `want` set each get BresenhamLine(A, B) (bresenham()'s
+// result).  With at most DPE_GN_COOP_MAX lines pending, each line is walked by all active lanes
+// together, consecutive steps from the closed form (bres::walk_pos), one byte load each per round
+// and a ballot; with more, every lane walks its own line.
+#ifndef DPE_GN_COOP
+#define DPE_GN_COOP 0
+#endif
+// The probe's walk pair in the other order: BresenhamLine(A, B) is "an edge on the walk B -> A or
+// on the walk A -> B", whichever is walked first; with the pixel as B the first walk starts at the
+// pixel, where the edge that blocks a direction usually is, and stops there
+#ifndef DPE_GN_PIXFIRST
+#define DPE_GN_PIXFIRST 1
+#endif
+#ifndef DPE_GN_COOP_MAX
+#define DPE_GN_COOP_MAX 8
+#endif
+DEV bool crosses_coop(const PassConst& pc, const DevBufs& B, bool want, int ax, int ay, int bx, int by, int max_step) {
+  const uint64_t act = __ballot(1);
+  uint64_t todo = __ballot(want);
+  if (todo == 0) return false;
+  if (__popcll(todo) > DPE_GN_COOP_MAX) return want ? bresenham(pc, B, ax, ay, bx, by) : false;
+  const int lane = (int)(threadIdx.x & 63);
+  const int rank = __popcll(act & ((1ull << lane) - 1ull)), nact = __popcll(act);
+  const int W = pc.W, width = pc.LW, height = pc.LH;
+  const float scale_x = 1.0f * pc.LW / (float)pc.W;
+  const float scale_y = 1.0f * pc.LH / (float)pc.H;
+  bool res = false;
+  while (todo) {
+    const int L = __builtin_ctzll(todo);
+    todo &= todo - 1;
+    const int Ax = __shfl(ax, L), Ay = __shfl(ay, L), Bx = __shfl(bx, L), By = __shfl(by, L);
+    bool hit = false;
+    if (!(B.edge[Ax + Ay * W] || B.edge[Bx + By * W])) {
+      for (int pass = 0; pass < 2 && !hit; ++pass) {
+        const int fx = pass == 0 ? Bx : Ax, fy = pass == 0 ? By : Ay;
+        const int tx = pass == 0 ? Ax : Bx, ty = pass == 0 ? Ay : By;
+        const int x0 = (int)MINo(__builtin_roundf(fx * scale_x), (float)(width - 1));
+        const int y0 = (int)MINo(__builtin_roundf(fy * scale_y), (float)(height - 1));
+        const int x1 = (int)MINo(__builtin_roundf(tx * scale_x), (float)(width - 1));
+        const int y1 = (int)MINo(__builtin_roundf(ty * scale_y), (float)(height - 1));
+        const bres::Walk w = bres::start(x0, y0, x1, y1, max_step);
+        const int K = bres::walk_steps(w);
+        for (int k0 = 0; k0 < K && !hit; k0 += nact) {
+          const int k = k0 + rank + 1;
+          uint8_t v = 0;
+          if (k <= K) {
+            int px, py;
+            bres::walk_pos(w, k, px, py);
+            const int idx = px + py * width;
+            if (idx >= 0 && idx < width * height) v = B.edge_low[idx];
+          }
+          hit = __ballot(v != 0) != 0;
+        }
+      }
+    }
+    if (lane == L) res = hit;
+  }
+  return res;
+}
 #ifndef DPE_GN_TIMES
 #define DPE_GN_TIMES 0
 #endif
@@ -769,6 +829,82 @@ __global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(c
       normalize2(od);
       return od;
     };
+#if DPE_GN_COOP
+    // the same walks with the loop kept wave-uniform (a lane whose 8 x rotate_time walks are done
+    // idles through it), so the probes' Bresenham walks can be shared: a wave with few walks pending
+    // walks each line with all its lanes (crosses_coop), 64 steps per load round
+    static_assert(DPE_GNL_SPEC == 4, "one attempt batch per radius");
+    int oi = 0, ri = 0, radius = 2;
+    float2 od = origin_od(0);
+    while (__any(oi < 8)) {
+      const bool alive = oi < 8;
+      bool next = alive && radius > 4096;
+      if (alive) GN_C(0, 1);
+      if (alive && !next) {
+        const float tpx = (float)x + od.x * radius, tpy = (float)y + od.y * radius;
+        if (tpx < 0 || tpy < 0 || tpx >= W || tpy >= H) next = true;
+      }
+      const bool probe = alive && !next;
+      bool dir_found = false;
+      short2 cand[4], nnv[4];
+      uint8_t wkv[4];
+      bool inm[4];
+      uint32_t pos0 = 0;
+      if (probe) {
+        pos0 = rs.idx == 4 ? rs.ctr * 4u : (rs.ctr - 1u) * 4u + (uint32_t)rs.idx;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t r1 = rng_u32(rs); const uint32_t r2 = rng_u32(rs);
+          const uint32_t r3 = rng_u32(rs); const uint32_t r4 = rng_u32(rs);
+          const int rxs = (int)(((r1 % 2 == 0) ? 1u : 0xFFFFFFFFu) * r2 % (uint32_t)shift_range);
+          const int rys = (int)(((r3 % 2 == 0) ? 1u : 0xFFFFFFFFu) * r4 % (uint32_t)shift_range);
+          float2 dir = make_float2(od.x * 20 + (float)rxs, od.y * 20 + (float)rys);
+          normalize2(dir);
+          const short2 np = make_short2((short)f2i((float)x + dir.x * radius), (short)f2i((float)y + dir.y * radius));
+          inm[q] = !(np.x < min_margin || np.y < min_margin || np.x >= W - min_margin || np.y >= H - min_margin);
+          const int npc = inm[q] ? np.x + np.y * W : center;
+          wkv[q] = B.weak[npc];
+          nnv[q] = B.nearest[npc];
+          cand[q] = np;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        bool want = false;
+        short2 np = make_short2(0, 0);
+        if (probe && !dir_found && inm[q]) {
+          np = cand[q];
+          if (wkv[q] != DPE_STRONG) np = nnv[q];
+          if (!(np.x == -1 || np.y == -1)) want = gn_angle_ok((float)(np.x - x), (float)(np.y - y), od, threshhold);
+        }
+        if (want && edge_limit) GN_C(1, 1);
+        const uint64_t gn_b0_ = GN_CLK(); (void)gn_b0_;
+        const bool cr = DPE_GN_PIXFIRST ? crosses_coop(pc, B, want && edge_limit, np.x, np.y, x, y, max_step)
+                                        : crosses_coop(pc, B, want && edge_limit, x, y, np.x, np.y, max_step);
+        if (want && edge_limit) GN_C(4, (uint32_t)(GN_CLK() - gn_b0_));
+        if (want && (!edge_limit || !cr)) {
+          push(np);
+          dir_found = true;
+          rng_seek(rs, pos0 + 4u * (uint32_t)(q + 1));
+        }
+      }
+      if (probe) {
+        if (dir_found) next = true;
+        else radius = MINo(radius * 2, radius + 25);
+      }
+      if (alive && next) {
+        radius = 2;
+        if (++ri < rotate_time) {
+          float2 rd = make_float2(od.x * cos_angle - od.y * sin_angle, od.x * sin_angle + od.y * cos_angle);
+          normalize2(rd);
+          od = rd;
+        } else {
+          ri = 0;
+          if (++oi < 8) od = origin_od(oi);
+        }
+      }
+    }
+#else
     int oi = 0, ri = 0, radius = 2;
     float2 od = origin_od(0);
     while (oi < 8) {
@@ -860,7 +996,7 @@ __global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(c
             const bool ang = gn_angle_ok((float)(np.x - x), (float)(np.y - y), od, threshhold);
             if (ang && edge_limit) GN_C(1, 1);
             const uint64_t gn_b0_ = GN_CLK(); (void)gn_b0_;
-            const bool pass_ = ang && (!edge_limit || !crosses(x, y, np.x, np.y));
+            const bool pass_ = ang && (!edge_limit || !(DPE_GN_PIXFIRST ? crosses(np.x, np.y, x, y) : crosses(x, y, np.x, np.y)));
             GN_C(4, (uint32_t)(GN_CLK() - gn_b0_));
             if (pass_) {
               push(np);
@@ -884,6 +1020,7 @@ __global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(c
         }
       }
     }
+#endif
   }
   PHASE(0);
   if (pc.P.use_label && B.label[center] > 0) {

@@ -959,7 +959,7 @@ DEV float ncc_new_tab(const PassConst& pc, const DevBufs& B, const WeakTab& T, i
                                // (its slow loop one row at a time, lds_taps ROW1: no scratch)
 #endif
 #ifndef DPE_WEAK_ROW1
-#define DPE_WEAK_ROW1 0     // the final Old NCC's slow tap loop one row at a time (lds_taps ROW1)
+#define DPE_WEAK_ROW1 1     // the final Old NCC's slow tap loop one row at a time (lds_taps ROW1)
 #endif
 #ifndef DPE_WEAK_TPC
 #define DPE_WEAK_TPC 0      // pooled jobs read the neighbour-patch parameters from the pass constants

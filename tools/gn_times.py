@@ -62,4 +62,12 @@ for k, nm in enumerate(names):
     w = v[:nw].reshape(-1, 64)
     util = w.sum() / max(1.0, 64 * w.max(1).sum())
     print(f"{nm:24s} per pixel mean={v.mean():.1f}", q(v), f"| per wave max mean={w.max(1).mean():.1f} lane utilisation={util:.3f}")
+# the slowest waves: their slowest lane's time and work counts (what the kernel's tail is made of)
+order = np.argsort(wmax)[::-1][:20]
+print("slowest waves (a lane's time is its wave's: lanes wait for each other at every reconvergence):")
+print("  wave: cycles | probe cycles | max over lanes of: radius steps, probe walks, RANSAC tries, RANSAC walks, probe walk clocks, RANSAC walk clocks")
+for wi in order:
+    lanes = np.arange(wi * 64, wi * 64 + 64)
+    mx = cnt[lanes].max(axis=0)
+    print(f"  wave {wi:5d}: {wmax[wi]:.3g} | {probe[lanes].max():.3g} | " + " ".join(f"{mx[k]:.0f}" for k in range(6)))
 lib.dpe_destroy(ctx)
