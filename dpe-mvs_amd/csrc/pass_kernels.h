@@ -686,6 +686,10 @@ DEV bool bresenham_short(const PassConst& pc, const DevBufs& B, int Ax, int Ay, 
 // The probe's walk pair in the other order: BresenhamLine(A, B) is "an edge on the walk B -> A or
 // on the walk A -> B", whichever is walked first; with the pixel as B the first walk starts at the
 // pixel, where the edge that blocks a direction usually is, and stops there
+// RANSACToGetFitPlane's three edge walks of a try stopped at the first that crosses an edge
+#ifndef DPE_GN_RSC
+#define DPE_GN_RSC 0
+#endif
 #ifndef DPE_GN_PIXFIRST
 #define DPE_GN_PIXFIRST 1
 #endif
@@ -1115,10 +1119,18 @@ __global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(c
           if (vca) eca = vca == 2; else { eca = crosses(pcc.x, pcc.y, pa.x, pa.y); *sca = eca ? 2 : 1; }
         } else {
           const uint64_t gn_b1_ = GN_CLK(); (void)gn_b1_;
+#if DPE_GN_RSC
+          // only their OR is used: the later walks are skipped once one crosses an edge
+          eab = crosses(pa.x, pa.y, pb.x, pb.y);
+          ebc = !eab && crosses(pb.x, pb.y, pcc.x, pcc.y);
+          eca = !eab && !ebc && crosses(pcc.x, pcc.y, pa.x, pa.y);
+          GN_C(3, 1 + (eab ? 0 : 1) + (eab || ebc ? 0 : 1));
+#else
           eab = crosses(pa.x, pa.y, pb.x, pb.y);
           ebc = crosses(pb.x, pb.y, pcc.x, pcc.y);
           eca = crosses(pcc.x, pcc.y, pa.x, pa.y);
           GN_C(3, 3);
+#endif
           GN_C(5, (uint32_t)(GN_CLK() - gn_b1_));
         }
         if (eab || ebc || eca) continue;
