@@ -218,6 +218,9 @@ const char* dpe_last_error(void) { return g_err.c_str(); }
 #ifndef DPE_FORK_AFTER_INIT
 #define DPE_FORK_AFTER_INIT 1
 #endif
+#ifndef DPE_GN_AFTER_RI
+#define DPE_GN_AFTER_RI 0
+#endif
 DpeContext* dpe_create(int device) {
   g_err.clear();
   int n = 0;
@@ -885,7 +888,12 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
     }
     return 0;
   };
-  const bool gn_after_init = overlap && !early && DPE_FORK_AFTER_INIT;
+  // early fork + DPE_GN_AFTER_RI: GenNeighbours still follows the setup chain on the aux stream, but
+  // also waits for RandomInitialization, which otherwise gets CU slots only as GenNeighbours' long
+  // waves leave (0.83 ms alone, ~5 ms beside it in the overlapped timeline), delaying the first
+  // strong half-sweep; ev_fork is recorded again after it (a wait binds the record made before it)
+  const bool gn_after_ri = early && DPE_GN_AFTER_RI;
+  const bool gn_after_init = (overlap && !early && DPE_FORK_AFTER_INIT) || gn_after_ri;
   if (!gn_after_init) { const int r = launch_gn(); if (r) return r; }
   if (!overlap) {
     // per-colour pixel lists of the sweeps (weak_info is fixed from here until DepthToWeak)
@@ -897,6 +905,10 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   Bc = begin(DPE_CLASS_INIT);
   if (c->img8) k_random_init<kTexInit><<<fg, fb, 0, s>>>(dpc, Bc); else k_random_init<TEX_F32><<<fg, fb, 0, s>>>(dpc, Bc);
   end();
+  if (gn_after_ri) {
+    HIPC(hipEventRecord(c->ev_fork, s));
+    HIPC(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
+  }
   if (gn_after_init) { const int r = launch_gn(); if (r) return r; }
   if (early) HIPC(hipStreamWaitEvent(s, c->ev_ei, 0));   // the strong sweeps read GenEdgeInform's rays
   HIPC(hipGetLastError());
