@@ -130,7 +130,7 @@ struct Rng {
 };
 
 #ifndef DPE_PHILOX64
-#define DPE_PHILOX64 0   // 1: each round's two 32x32 products as one 64-bit product (v_mad_u64_u32) each
+#define DPE_PHILOX64 1   // 1: each round's two 32x32 products as one 64-bit product (v_mad_u64_u32) each
 #endif
 DEV void philox10(uint32_t& c0, uint32_t& c1, uint32_t& c2, uint32_t& c3, uint32_t k0, uint32_t k1) {
 #pragma unroll
