@@ -218,6 +218,9 @@ const char* dpe_last_error(void) { return g_err.c_str(); }
 #ifndef DPE_FORK_AFTER_INIT
 #define DPE_FORK_AFTER_INIT 1
 #endif
+#ifndef DPE_GN_LDS_PAD
+#define DPE_GN_LDS_PAD 0   // unused dynamic LDS per GenNeighbours workgroup: caps its resident waves (A/B)
+#endif
 #ifndef DPE_GN_AFTER_RI
 #define DPE_GN_AFTER_RI 0
 #endif
@@ -844,7 +847,7 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
         k_gen_neighbours_lds<8><<<gg, DPE_GN_BT, 0, a>>>(dpc, Bgn, lst, cnt, c->gn_tab.p, c->gn_ovf.p, c->list_totals.p + 6,
                                                          nullptr, 0);
       else if (pc.P.rotate_time <= 2 && c->gn_slots != 64)   // at most 16 x rotate_time support points
-        k_gen_neighbours_lds<32><<<gg, DPE_GN_BT, 0, a>>>(dpc, Bgn, lst, cnt, c->gn_tab.p, c->gn_ovf.p, c->list_totals.p + 6,
+        k_gen_neighbours_lds<32><<<gg, DPE_GN_BT, DPE_GN_LDS_PAD, a>>>(dpc, Bgn, lst, cnt, c->gn_tab.p, c->gn_ovf.p, c->list_totals.p + 6,
                                                           ec, (long)L + 64);
       else
         k_gen_neighbours_lds<64><<<gg, DPE_GN_BT, 0, a>>>(dpc, Bgn, lst, cnt, c->gn_tab.p, c->gn_ovf.p, c->list_totals.p + 6,
