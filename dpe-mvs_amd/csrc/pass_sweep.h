@@ -731,6 +731,9 @@ struct WeakTab {
   float nbox[4];                          // x0, x1, y0, y1 of the union of the neighbour patches
 };
 
+#ifndef DPE_WEAK_NBMAX
+#define DPE_WEAK_NBMAX 0   // the neighbour loop's patch_ncc_tab without the side-4..6 cases (tab_n implies side <= 3)
+#endif
 // patch NCC with tabulated weights; the same tap order and arithmetic as patch_ncc_generic.
 // NN > 0: the patch side n is the compile-time NN, so the tap loop unrolls and the gathers of a
 // patch are in flight together (the weak sweep's patches are 3x3 and 4..6 square).
@@ -829,7 +832,8 @@ DEV void tab_taps_masked(const PassConst& pc, const DevBufs& B, int v, const Hom
   acc[0] = s_sr.x; acc[1] = s_ss; acc[2] = s_sr.y;
 }
 
-template <int U8>
+// NMAX: the largest side the caller can pass (the neighbour patches are tabulated only up to 3)
+template <int U8, int NMAX = 6>
 DEV float patch_ncc_tab(const PassConst& pc, const DevBufs& B, int v, const Homog& H, int cx, int cy, int rad, int inc,
                         int n, const float* __restrict__ tw, const float* sm) {
   float a[3];
@@ -841,6 +845,13 @@ DEV float patch_ncc_tab(const PassConst& pc, const DevBufs& B, int v, const Homo
         return ncc_finalize_pre(sm[0], sm[1], sm[2], a[0], a[1], a[2]);
       }
     }
+#if DPE_WEAK_NBMAX
+    if (n == 3) tab_taps<U8, true, 3>(pc, B, v, H, cx, cy, rad, inc, n, tw, a);
+    else if (NMAX >= 4 && n == 4) tab_taps<U8, true, (NMAX >= 4 ? 4 : 1)>(pc, B, v, H, cx, cy, rad, inc, n, tw, a);
+    else if (NMAX >= 5 && n == 5) tab_taps<U8, true, (NMAX >= 5 ? 5 : 1)>(pc, B, v, H, cx, cy, rad, inc, n, tw, a);
+    else if (NMAX >= 6 && n == 6) tab_taps<U8, true, (NMAX >= 6 ? 6 : 1)>(pc, B, v, H, cx, cy, rad, inc, n, tw, a);
+    else tab_taps<U8, true>(pc, B, v, H, cx, cy, rad, inc, n, tw, a);
+#else
     switch (n) {
       case 3: tab_taps<U8, true, 3>(pc, B, v, H, cx, cy, rad, inc, n, tw, a); break;
       case 4: tab_taps<U8, true, 4>(pc, B, v, H, cx, cy, rad, inc, n, tw, a); break;
@@ -848,6 +859,7 @@ DEV float patch_ncc_tab(const PassConst& pc, const DevBufs& B, int v, const Homo
       case 6: tab_taps<U8, true, 6>(pc, B, v, H, cx, cy, rad, inc, n, tw, a); break;
       default: tab_taps<U8, true>(pc, B, v, H, cx, cy, rad, inc, n, tw, a); break;
     }
+#endif
   } else {
     tab_taps<U8, false>(pc, B, v, H, cx, cy, rad, inc, n, tw, a);
   }
@@ -933,7 +945,7 @@ DEV float ncc_new_tab(const PassConst& pc, const DevBufs& B, const WeakTab& T, i
       const float* sm = T.sums + 3 * k;
       tc = ncc_finalize_pre(sm[0], sm[1], sm[2], a[0], a[1], a[2]);
     } else {
-      tc = T.tab_n ? patch_ncc_tab<U8>(pc, B, v, H, np.x, np.y, T.rad_n, T.inc_n, T.n_n, T.tn + (k - 1) * 18,
+      tc = T.tab_n ? patch_ncc_tab<U8, DPE_WEAK_NBMAX ? 3 : 6>(pc, B, v, H, np.x, np.y, T.rad_n, T.inc_n, T.n_n, T.tn + (k - 1) * 18,
                                        T.sums + 3 * k)
                    : patch_ncc_generic<U8>(pc, B, v, H, np.x, np.y, T.rc, T.rad_n, T.inc_n);
     }
