@@ -218,6 +218,9 @@ const char* dpe_last_error(void) { return g_err.c_str(); }
 #ifndef DPE_FORK_AFTER_INIT
 #define DPE_FORK_AFTER_INIT 1
 #endif
+#ifndef DPE_RANSAC_LIST
+#define DPE_RANSAC_LIST 1   // RANSACToGetFitPlane over the WEAK list instead of the whole image
+#endif
 #ifndef DPE_GN_LDS_PAD
 #define DPE_GN_LDS_PAD 0   // unused dynamic LDS per GenNeighbours workgroup: caps its resident waves (A/B)
 #endif
@@ -947,7 +950,11 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
     }
     HIPC(hipGetLastError());
     Bc = begin(DPE_CLASS_RANSAC);
-    k_ransac_fit<<<rg, rb, 0, s>>>(dpc, Bc, it);
+    if (DPE_RANSAC_LIST && !split)   // the WEAK list of slot 4 (built before GenNeighbours, kept to the end)
+      k_ransac_fit<true><<<(unsigned)((L + kRansacThreads - 1) / kRansacThreads), kRansacThreads, 0, s>>>(dpc, Bc, it, weak_list,
+                                                                                                         c->list_totals.p + 4);
+    else
+      k_ransac_fit<false><<<rg, rb, 0, s>>>(dpc, Bc, it, nullptr, nullptr);
     end();
     for (int colour = 0; colour < 2; ++colour) {
       Bc = begin(DPE_CLASS_WEAK);

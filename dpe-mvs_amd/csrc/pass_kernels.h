@@ -1333,9 +1333,26 @@ __global__ void __launch_bounds__(256) k_random_init(const PassConst* __restrict
 
 // ------------------------------------------------------------------------------ RANSACToGetFitPlane
 constexpr int kRansacThreads = 128;   // 16 x 8 workgroups: 28 KB of LDS each
-__global__ void __launch_bounds__(kRansacThreads) k_ransac_fit(const PassConst* __restrict__ pcp, DevBufs B, int iter) {   // DPE.cu:2891-3124
+// LISTED: one thread per entry of the WEAK list built before GenNeighbours (1-D workgroups; pixels
+// that NeigbourUpdate made UNKNOWN are skipped by the weak_info test), instead of one thread per
+// pixel of the image with ~80 % of them returning at once
+template <bool LISTED>
+__global__ void __launch_bounds__(kRansacThreads) k_ransac_fit(const PassConst* __restrict__ pcp, DevBufs B, int iter,
+                                                               const int* __restrict__ list, const int* __restrict__ nlist_p) {   // DPE.cu:2891-3124
   const PassConst& pc = *pcp;
-  PIX2D_FULL();
+  int x, y, center;
+  if constexpr (LISTED) {
+    const int gi = xcd_remap(blockIdx.x, gridDim.x, B.xcd_rows * 16) * kRansacThreads + (int)threadIdx.x;
+    if (gi >= *nlist_p) return;
+    center = list[gi];
+    x = center % pc.W; y = center / pc.W;
+  } else {
+    const int lb_ = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y, B.xcd_rows * gridDim.x);
+    x = (lb_ % gridDim.x) * blockDim.x + threadIdx.x;
+    y = (lb_ / gridDim.x) * blockDim.y + threadIdx.y;
+    if (x >= pc.W || y >= pc.H) return;
+    center = x + y * pc.W;
+  }
   const int W = pc.W;
   if (B.weak[center] != DPE_WEAK) return;
   Rng rs; rng_init(rs, (uint32_t)center, pc.seed32, STREAM_ITER_BASE + 4 * iter + 1, pc.salt);
