@@ -218,6 +218,12 @@ const char* dpe_last_error(void) { return g_err.c_str(); }
 #ifndef DPE_FORK_AFTER_INIT
 #define DPE_FORK_AFTER_INIT 1
 #endif
+#ifndef DPE_WEAK_PAR
+#define DPE_WEAK_PAR 1   // the two colours' weak sweeps on two streams (they are independent)
+#endif
+#ifndef DPE_RANSAC_SPLIT
+#define DPE_RANSAC_SPLIT 0   // with DPE_WEAK_PAR: each colour's RANSAC fit on its own stream before its weak sweep
+#endif
 #ifndef DPE_RANSAC_LIST
 #define DPE_RANSAC_LIST 1   // RANSACToGetFitPlane over the WEAK list instead of the whole image
 #endif
@@ -949,26 +955,50 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
       end();
     }
     HIPC(hipGetLastError());
+    // DPE_RANSAC_SPLIT (with the two-stream weak sweeps): each colour's RANSACToGetFitPlane over that
+    // colour's weak list, on that colour's stream, just before its weak sweep (a fit reads STRONG
+    // pixels and writes its own pixel's fit plane, which only its own weak update reads)
+    const bool ransac_split = overlap && DPE_WEAK_PAR && DPE_RANSAC_SPLIT && !split;
+    const unsigned rl_grid = (unsigned)((L / 2 + 1 + kRansacThreads - 1) / kRansacThreads);
     Bc = begin(DPE_CLASS_RANSAC);
-    if (DPE_RANSAC_LIST && !split)   // the WEAK list of slot 4 (built before GenNeighbours, kept to the end)
+    if (ransac_split) {   // fork first: the colour-1 fit must not wait for the colour-0 one
+      HIPC(hipEventRecord(c->ev_fork, s));
+      HIPC(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
+      k_ransac_fit<true><<<rl_grid, kRansacThreads, 0, c->aux>>>(dpc, Bc, it, c->lists.p + 3 * list_stride, c->list_totals.p + 3);
+      k_ransac_fit<true><<<rl_grid, kRansacThreads, 0, s>>>(dpc, Bc, it, c->lists.p + 1 * list_stride, c->list_totals.p + 1);
+    } else if (DPE_RANSAC_LIST && !split)   // the WEAK list of slot 4 (built before GenNeighbours, kept to the end)
       k_ransac_fit<true><<<(unsigned)((L + kRansacThreads - 1) / kRansacThreads), kRansacThreads, 0, s>>>(dpc, Bc, it, weak_list,
                                                                                                          c->list_totals.p + 4);
     else
       k_ransac_fit<false><<<rg, rb, 0, s>>>(dpc, Bc, it, nullptr, nullptr);
     end();
+    // The two colours' weak sweeps read only STRONG pixels' state besides their own pixel (planes and
+    // selected views of the GenNeighbours support points, DPE.cu:1690-1725; the NCC-New patches come
+    // from the images), and write only their own pixel, so they are independent: with DPE_WEAK_PAR the
+    // colour-1 sweep runs on the aux stream beside the colour-0 one (the launch tails overlap)
+    const bool weak_par = overlap && DPE_WEAK_PAR;
+    if (weak_par && !ransac_split) {
+      HIPC(hipEventRecord(c->ev_fork, s));
+      HIPC(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
+    }
     for (int colour = 0; colour < 2; ++colour) {
       Bc = begin(DPE_CLASS_WEAK);
       {
+        const hipStream_t sw = weak_par && colour == 1 ? c->aux : s;
         const int* lst = c->lists.p + (colour * 2 + 1) * list_stride;
         const int* cnt = c->list_totals.p + colour * 2 + 1;
         constexpr int C = kWeakLanes, P = 64 / C;
         const size_t per_wave = (size_t)P * weak_lds_per_pixel(nv) * sizeof(float);
         const int wpb = per_wave * 4 <= 64 * 1024 ? 4 : (per_wave * 2 <= 64 * 1024 ? 2 : 1);
         const unsigned grid = (unsigned)((L / 2 + 1 + wpb * P - 1) / (wpb * P));
-        if (c->img8) k_weak_coop<kTexWeak, C><<<grid, 64 * wpb, per_wave * wpb, s>>>(dpc, Bc, it, lst, cnt);
-        else k_weak_coop<TEX_F32, C><<<grid, 64 * wpb, per_wave * wpb, s>>>(dpc, Bc, it, lst, cnt);
+        if (c->img8) k_weak_coop<kTexWeak, C><<<grid, 64 * wpb, per_wave * wpb, sw>>>(dpc, Bc, it, lst, cnt);
+        else k_weak_coop<TEX_F32, C><<<grid, 64 * wpb, per_wave * wpb, sw>>>(dpc, Bc, it, lst, cnt);
       }
       end();
+    }
+    if (weak_par) {
+      HIPC(hipEventRecord(c->ev_join, c->aux));
+      HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
     }
     HIPC(hipGetLastError());
   }
