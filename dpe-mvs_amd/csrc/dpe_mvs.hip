@@ -222,7 +222,7 @@ const char* dpe_last_error(void) { return g_err.c_str(); }
 #define DPE_WEAK_PAR 1   // the two colours' weak sweeps on two streams (they are independent)
 #endif
 #ifndef DPE_RANSAC_SPLIT
-#define DPE_RANSAC_SPLIT 0   // with DPE_WEAK_PAR: each colour's RANSAC fit on its own stream before its weak sweep
+#define DPE_RANSAC_SPLIT 1   // with DPE_WEAK_PAR: each colour's RANSAC fit on its own stream before its weak sweep
 #endif
 #ifndef DPE_RANSAC_LIST
 #define DPE_RANSAC_LIST 1   // RANSACToGetFitPlane over the WEAK list instead of the whole image
