@@ -32,6 +32,9 @@ namespace dpe {
 // LDS (bit 0 edge, bit 1 label 0, bit 2 inside the image) for r <= kEiTileR; the counts are
 // integers, so the tile changes nothing but the number of global loads (r^2 per pixel -> ~1.6).
 constexpr int kEiTileR = 8, kEiTile = 16 + 2 * kEiTileR;
+#ifndef DPE_EI_SEP
+#define DPE_EI_SEP 0   // the window counts as a row pass and a column pass over the tile (exact integer sums)
+#endif
 // GenEdgeInform's 8 edge rays (DPE.cu:2497-2530: the first edge pixel along each direction, to the
 // image border) as line scans: every pixel lies on one row, one column, one diagonal (x - y const)
 // and one anti-diagonal (x + y const); along a line the ray in one direction is the nearest edge
@@ -97,6 +100,9 @@ __global__ void __launch_bounds__(64) k_edge_rays(const PassConst* __restrict__ 
 __global__ void __launch_bounds__(256) k_gen_edge_inform(const PassConst* __restrict__ pcp, DevBufs B) {   // DPE.cu:2483-2591
   const PassConst& pc = *pcp;
   __shared__ uint8_t s_tile[kEiTile * kEiTile];
+#if DPE_EI_SEP
+  __shared__ uint32_t s_hsum[kEiTile][16];
+#endif
   const int radius = pc.P.strong_radius;
   const bool tiled = pc.P.use_edge && radius >= 0 && radius <= kEiTileR;
   if (tiled) {   // block-uniform; every thread of the block helps before any returns
@@ -113,6 +119,21 @@ __global__ void __launch_bounds__(256) k_gen_edge_inform(const PassConst* __rest
       s_tile[t] = v;
     }
     __syncthreads();
+#if DPE_EI_SEP
+    // separable window counts: each tile row's (2r+1)-wide sums for the block's 16 columns, the three
+    // counts packed 10 bits apart (at most 17 x 17 = 289 each), then 2r+1 of them down each column
+    for (int t = threadIdx.y * blockDim.x + threadIdx.x; t < th * 16; t += blockDim.x * blockDim.y) {
+      const int r = t / 16, cc = t % 16;
+      const uint8_t* row = s_tile + r * tw + cc;
+      uint32_t acc = 0;
+      for (int i = 0; i <= 2 * radius; i++) {
+        const uint32_t v = row[i];
+        acc += (v & 1u) | (((v >> 1) & 1u) << 10) | ((v >> 2) << 20);
+      }
+      s_hsum[r][cc] = acc;
+    }
+    __syncthreads();
+#endif
   }
   PIX2D_FULL();
   const int W = pc.W, H = pc.H;
@@ -138,7 +159,11 @@ __global__ void __launch_bounds__(256) k_gen_edge_inform(const PassConst* __rest
       en[i] = r;
     }
     int edge_pix = 0, tot_pix = 0, bound_pix = 0;
-    if (tiled) {
+    if (tiled && DPE_EI_SEP) {
+      uint32_t acc = 0;
+      for (int j = 0; j <= 2 * radius; j++) acc += s_hsum[threadIdx.y + j][threadIdx.x];
+      edge_pix = (int)(acc & 1023u); bound_pix = (int)((acc >> 10) & 1023u); tot_pix = (int)(acc >> 20);
+    } else if (tiled) {
       const int tw = blockDim.x + 2 * radius;
       for (int j = 0; j <= 2 * radius; j++) {
         const uint8_t* row = s_tile + (threadIdx.y + j) * tw + threadIdx.x;
