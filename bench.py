@@ -267,8 +267,14 @@ def main():
     ts = time.perf_counter()
     ctx.stage(inp, st)            # second staging: the steady-state host->HBM cost of one pass (images cached)
     stage_ms = (time.perf_counter() - ts) * 1e3
-    stream = torch.cuda.current_stream()
+    # a dedicated (non-default) stream, made current: the pass, export_depth, the all-gather and the
+    # step events are then ordered on one stream.  torch's default stream is the null stream (handle
+    # 0), which the library would read as "use my own stream", leaving the collective and the events
+    # unordered with the pass
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
+    assert sp, "bench stream handle must be non-null"
     depth_local = torch.empty((Hd, Wd), dtype=torch.float32, device="cuda")
     gathered = [torch.empty_like(depth_local) for _ in range(world)] if world > 1 else None
 

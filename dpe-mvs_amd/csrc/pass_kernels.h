@@ -159,11 +159,14 @@ __global__ void __launch_bounds__(256) k_gen_edge_inform(const PassConst* __rest
       en[i] = r;
     }
     int edge_pix = 0, tot_pix = 0, bound_pix = 0;
-    if (tiled && DPE_EI_SEP) {
+#if DPE_EI_SEP
+    if (tiled) {
       uint32_t acc = 0;
       for (int j = 0; j <= 2 * radius; j++) acc += s_hsum[threadIdx.y + j][threadIdx.x];
       edge_pix = (int)(acc & 1023u); bound_pix = (int)((acc >> 10) & 1023u); tot_pix = (int)(acc >> 20);
-    } else if (tiled) {
+    } else
+#endif
+    if (tiled) {
       const int tw = blockDim.x + 2 * radius;
       for (int j = 0; j <= 2 * radius; j++) {
         const uint8_t* row = s_tile + (threadIdx.y + j) * tw + threadIdx.x;
