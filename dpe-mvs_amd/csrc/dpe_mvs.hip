@@ -367,6 +367,13 @@ static void compute_pass_constants(PassConst& pc) {
     pc.vc[v].b[1] = (float)(sK4 * trel[1] + sK5 * trel[2]);
     pc.vc[v].b[2] = (float)(sK8 * trel[2]);
   }
+  pc.cam_ik_ok = 0;
+  for (int v = 0; v < pc.N; ++v) {   // exact_div.h: reciprocals of the focal lengths, float RN
+    const float k0 = pc.cams[v].K[0], k4 = pc.cams[v].K[4];
+    pc.cam_ik[v][0] = 1.0f / k0;
+    pc.cam_ik[v][1] = 1.0f / k4;
+    if (xdiv::div_in_range(k0) && xdiv::div_in_range(k4)) pc.cam_ik_ok |= 1u << v;
+  }
   pc.kinv0 = (float)(1.0 / rK0);
   pc.kinv4 = (float)(1.0 / rK4);
   pc.kc2 = (float)(rK2 / rK0);

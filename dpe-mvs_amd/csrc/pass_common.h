@@ -17,6 +17,7 @@
 #pragma once
 #include "device_math.h"
 #include "bres_walk.h"
+#include "exact_div.h"
 #include "../../include/dpe_mvs.h"
 
 namespace dpe {
@@ -35,6 +36,8 @@ struct PassConst {
   DpePatchMatchParams P;
   DpeCamera cams[DPE_MAX_IMAGES];
   ViewConst vc[DPE_MAX_IMAGES];
+  float cam_ik[DPE_MAX_IMAGES][2];   // RN(1 / K[0]), RN(1 / K[4]) of each camera (exact_div.h)
+  uint32_t cam_ik_ok;                // bit v: camera v's K[0], K[4] in div_in_range (else IEEE division)
 };
 
 struct DevBufs {
@@ -172,6 +175,38 @@ DEV float2 project_cam(const float3& X, const DpeCamera& c) {                 //
   const float tz = c.R[6] * X.x + c.R[7] * X.y + c.R[8] * X.z + c.t[2];
   const float d = c.K[6] * tx + c.K[7] * ty + c.K[8] * tz;
   return make_float2((c.K[0] * tx + c.K[1] * ty + c.K[2] * tz) / d, (c.K[3] * tx + c.K[4] * ty + c.K[5] * tz) / d);
+}
+
+// The geometric-consistency term's divisions as exact_div.h quotients (same operations before each
+// division, the IEEE quotient bit for bit).  The fast form runs straight through and only collects
+// whether every operand was in div_in_range; a lane with one that was not recomputes the term with
+// the IEEE divisions (geom_cost_at's caller-visible result is the same either way).
+// DPE_GEOM_MDIV 0: world_point / project_cam as written.
+#ifndef DPE_GEOM_MDIV
+#define DPE_GEOM_MDIV 0   // A/B: +0.4 ms DepthToWeak (profiles/r04_ab_geom_mdiv.log), not adopted
+#endif
+DEV float3 world_point_m(const DpeCamera& c, float ik0, float ik4, float x, float y, float depth, bool& ok) {
+  const float ax = depth * (x - c.K[2]), ay = depth * (y - c.K[5]);
+  ok = ok && xdiv::div_in_range(ax) && xdiv::div_in_range(ay);
+  float3 X;
+  X.x = xdiv::div_markstein(ax, c.K[0], ik0);
+  X.y = xdiv::div_markstein(ay, c.K[4], ik4);
+  X.z = depth;
+  float3 T;
+  T.x = c.R[0] * X.x + c.R[3] * X.y + c.R[6] * X.z;
+  T.y = c.R[1] * X.x + c.R[4] * X.y + c.R[7] * X.z;
+  T.z = c.R[2] * X.x + c.R[5] * X.y + c.R[8] * X.z;
+  return make_float3(T.x + c.c[0], T.y + c.c[1], T.z + c.c[2]);
+}
+DEV float2 project_cam_m(const float3& X, const DpeCamera& c, bool& ok) {
+  const float tx = c.R[0] * X.x + c.R[1] * X.y + c.R[2] * X.z + c.t[0];
+  const float ty = c.R[3] * X.x + c.R[4] * X.y + c.R[5] * X.z + c.t[1];
+  const float tz = c.R[6] * X.x + c.R[7] * X.y + c.R[8] * X.z + c.t[2];
+  const float d = c.K[6] * tx + c.K[7] * ty + c.K[8] * tz;
+  const float nx = c.K[0] * tx + c.K[1] * ty + c.K[2] * tz, ny = c.K[3] * tx + c.K[4] * ty + c.K[5] * tz;
+  ok = ok && xdiv::div_in_range(d) && xdiv::div_in_range(nx) && xdiv::div_in_range(ny);
+  const float yd = d_rcp_fast(d);   // RN(1/d) while d's biased exponent is in [67, 187]
+  return make_float2(xdiv::div_markstein(nx, d, yd), xdiv::div_markstein(ny, d, yd));
 }
 
 // GenerateRandomNormal (DPE.cu:361-387)
@@ -896,8 +931,7 @@ DEV float3 geom_point(const PassConst& pc, int px, int py, const float4& pl) {
   const float depth = depth_from_plane(rc, pl, px, py);
   return world_point((float)px, (float)py, depth, rc);
 }
-DEV float geom_cost_at(const PassConst& pc, const DevBufs& B, int px, int py, int v, const float3& fw) {
-  if (B.cnt) atomicAdd(B.cnt + 2, 1ull);
+DEV float geom_cost_ieee(const PassConst& pc, const DevBufs& B, int px, int py, int v, const float3& fw) {
   const DpeCamera& rc = pc.cams[0];
   const DpeCamera& sc = pc.cams[v];
   const float2 sp = project_cam(fw, sc);
@@ -908,6 +942,24 @@ DEV float geom_cost_at(const PassConst& pc, const DevBufs& B, int px, int py, in
   const float dc = (float)px - bp.x, dr = (float)py - bp.y;
   const float cc = __builtin_sqrtf(dc * dc + dr * dr);
   return __builtin_fminf(3.0f, cc);
+}
+DEV float geom_cost_at(const PassConst& pc, const DevBufs& B, int px, int py, int v, const float3& fw) {
+  if (B.cnt) atomicAdd(B.cnt + 2, 1ull);
+  if (!DPE_GEOM_MDIV) return geom_cost_ieee(pc, B, px, py, v, fw);
+  const DpeCamera& rc = pc.cams[0];
+  const DpeCamera& sc = pc.cams[v];
+  bool ok1 = true, ok2 = (pc.cam_ik_ok >> v) & 1u;
+  const float2 sp = project_cam_m(fw, sc, ok1);
+  const float src_depth = depth_texel(B.depth[v], pc.W, pc.H, sp.x, sp.y);
+  const float3 s3 = world_point_m(sc, pc.cam_ik[v][0], pc.cam_ik[v][1], sp.x, sp.y, src_depth, ok2);
+  const float2 bp = project_cam_m(s3, rc, ok2);
+  const float dc = (float)px - bp.x, dr = (float)py - bp.y;
+  const float cc = __builtin_sqrtf(dc * dc + dr * dr);
+  const bool miss = src_depth == 0.0f;
+  float g = miss ? 3.0f : __builtin_fminf(3.0f, cc);
+  // a missing source depth needs only the first projection's range (the rest is not used)
+  if (__builtin_expect(!ok1 || (!miss && !ok2), 0)) g = geom_cost_ieee(pc, B, px, py, v, fw);
+  return g;
 }
 // geom_cost_at in two halves, so that a caller can issue the source-depth gather before other work
 // (same operations, same result): geom_fetch projects and loads, geom_finish completes
