@@ -270,7 +270,9 @@ def main():
     # a dedicated (non-default) stream, made current: the pass, export_depth, the all-gather and the
     # step events are then ordered on one stream.  torch's default stream is the null stream (handle
     # 0), which the library would read as "use my own stream", leaving the collective and the events
-    # unordered with the pass
+    # unordered with the pass.  torch is imported before DPE_MVS, so the library's libamdhip64.so.7
+    # resolves to torch's already-loaded copy (same SONAME): one HIP runtime, and torch's stream
+    # handle is valid in the library
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
