@@ -186,18 +186,34 @@ def pipeline_config4(dist, rank: int, world: int, local_rank: int, n: int = 16, 
     pipeline.run_dpe_pipeline(folder, gpu_index=local_rank, verbose=False, dist=dist if world > 1 else None)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    import ctypes
+    ph = (ctypes.c_double * 7)()
+    pipeline.lib().dpe_pipeline_last_timings(ph, 7)
+    # per rank: wall, pass work, depth exchanges (status + export + all-gather + import), EdgeSegment
+    mine = [dt, ph[6], ph[5], ph[2]]
+    per_rank = [mine]
     if dist:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+        t = torch.tensor(mine, dtype=torch.float64, device="cuda" if dist.get_backend() == "nccl" else "cpu")
+        allr = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(allr, t)
+        per_rank = [[float(v) for v in a.tolist()] for a in allr]
         dist.barrier()
+    dt = max(p[0] for p in per_rank)
     if rank == 0:
         shutil.rmtree(folder, ignore_errors=True)
+    passes = [round(p[1], 3) for p in per_rank]
     return {"config": "BASELINE configs[3]: ETH3D-size 2688x1792, 16 reference images, 9 source views each, "
                       "full 3-round schedule, images sharded over the ranks (synthetic scene)",
-            "images": n, "width": W, "height": H, "ranks": world, "wall_s": round(dt, 3),
-            "mpix_s": round(n * W * H / dt / 1e6, 4),
-            "note": "pipeline wall incl. JPEG decode, EdgeSegment, 12 passes per image, depth all-gathers, .npy outputs"}
+            "images": n, "width": W, "height": H, "ranks": world, "ranks_in_group": world,
+            "images_per_rank": [((r + 1) * n) // world - (r * n) // world for r in range(world)],
+            "wall_s": round(dt, 3), "mpix_s": round(n * W * H / dt / 1e6, 4),
+            "passes_s": max(passes), "passes_s_per_rank": passes,
+            "exchange_s": round(max(p[2] for p in per_rank), 3),
+            "edge_segment_s": round(max(p[3] for p in per_rank), 3),
+            "note": "pipeline wall incl. JPEG decode, EdgeSegment, 12 passes per image, depth all-gathers, .npy outputs; "
+                    "passes_s / exchange_s: max over ranks of the pass work and of the depth exchanges "
+                    "(dpe_pipeline_last_timings [6] / [5]); passes_s_per_rank shows the load balance" +
+                    ("" if world > 1 else "; one rank: no exchange")}
 
 
 def parity_on_sample(native, local_rank: int, sample) -> dict:

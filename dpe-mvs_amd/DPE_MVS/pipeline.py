@@ -44,6 +44,7 @@ class DpePipelineOptions(C.Structure):
         ("fusion_runner", C.c_void_p), ("fusion_user", C.c_void_p),
         ("max_iterations", C.c_int), ("photometric_only", C.c_bool),
         ("allgather_device", C.c_void_p), ("allgather_device_user", C.c_void_p),
+        ("abort_collectives", C.c_void_p), ("abort_user", C.c_void_p),
     ]
 
 

@@ -129,20 +129,13 @@ struct Rng {
   int idx;
 };
 
-#ifndef DPE_PHILOX64
-#define DPE_PHILOX64 1   // 1: each round's two 32x32 products as one 64-bit product (v_mad_u64_u32) each
-#endif
 DEV void philox10(uint32_t& c0, uint32_t& c1, uint32_t& c2, uint32_t& c3, uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-#if DPE_PHILOX64
+    // each round's two 32x32 products as one 64-bit product (v_mad_u64_u32) each
     const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
     const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
     const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
-#else
-    const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
-    const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
-#endif
     const uint32_t n0 = hi1 ^ c1 ^ k0;
     const uint32_t n2 = hi0 ^ c3 ^ k1;
     c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;

@@ -28,10 +28,7 @@
 using namespace dpe;
 
 static const int kDefaultXcdRows = 1;
-#ifndef DPE_WEAK_LANES
-#define DPE_WEAK_LANES 16
-#endif
-static constexpr int kWeakLanes = DPE_WEAK_LANES;   // lanes per weak pixel in k_weak_coop (16 or 32)
+static constexpr int kWeakLanes = 16;   // lanes per weak pixel in k_weak_coop
 
 namespace {
 
@@ -116,7 +113,7 @@ struct DpeContext {
   uint64_t icache_clock = 0;
   hipStream_t stream = nullptr;
   hipStream_t aux = nullptr;         // GenNeighbours beside the first strong half-sweep
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_ei = nullptr, ev_gn0 = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_ei = nullptr;
   hipEvent_t ev_done = nullptr;      // end of the last dpe_pm_execute's work on its stream
   bool pending = false;              // ev_done recorded and not yet waited for
   bool staged = false;
@@ -141,7 +138,6 @@ struct DpeContext {
   bool img8 = false;                 // all images are 8-bit grey levels -> u8 quad layout
   DevArr<float> depth[DPE_MAX_IMAGES];
   DevArr<uint8_t> edge, edge_low;
-  DevArr<uint64_t> edge_tiles;
   DevArr<int> label;
   // staged initial state
   DevArr<float4> planes0;
@@ -157,7 +153,6 @@ struct DpeContext {
   DevArr<int> tab_right, tab_down;   // FindNearestStrongPoint tables
   DevArr<int> gn_ovf;                // GenNeighbours pixels left to the scratch kernel (k_gen_neighbours_lds)
   DevArr<float> gn_tab;              // normalised image coordinates per column / row (k_gn_tables)
-  DevArr<uint8_t> gn_ecache;         // GenNeighbours' edge-test cache, 496 pair bytes per WEAK pixel
   DevArr<int> lists, row_counts, list_totals;   // per-colour pixel lists for the sweeps
   DevBufs bufs;
   // fusion (dpe_fusion_stage / dpe_fusion_candidates)
@@ -203,36 +198,6 @@ void dpe_params_default(DpePatchMatchParams* p) {   // main.h:78-106
 
 const char* dpe_last_error(void) { return g_err.c_str(); }
 
-#ifndef DPE_GN_LDS
-#define DPE_GN_LDS 1   // scratch-free GenNeighbours (pass_kernels.h k_gen_neighbours_lds)
-#endif
-#ifndef DPE_TABLE_SCAN
-#define DPE_TABLE_SCAN 1   // FindNearestStrongPoint's tables by wave line scans (pass_refine.h)
-#endif
-#ifndef DPE_GN_SPLIT
-#define DPE_GN_SPLIT 0   // 1: GenNeighbours of the colour-0 grid pixels first (early fork only; measured slower)
-#endif
-#ifndef DPE_EARLY_FORK
-#define DPE_EARLY_FORK 1
-#endif
-#ifndef DPE_FORK_AFTER_INIT
-#define DPE_FORK_AFTER_INIT 1
-#endif
-#ifndef DPE_WEAK_PAR
-#define DPE_WEAK_PAR 1   // the two colours' weak sweeps on two streams (they are independent)
-#endif
-#ifndef DPE_RANSAC_SPLIT
-#define DPE_RANSAC_SPLIT 1   // with DPE_WEAK_PAR: each colour's RANSAC fit on its own stream before its weak sweep
-#endif
-#ifndef DPE_RANSAC_LIST
-#define DPE_RANSAC_LIST 1   // RANSACToGetFitPlane over the WEAK list instead of the whole image
-#endif
-#ifndef DPE_GN_LDS_PAD
-#define DPE_GN_LDS_PAD 0   // unused dynamic LDS per GenNeighbours workgroup: caps its resident waves (A/B)
-#endif
-#ifndef DPE_GN_AFTER_RI
-#define DPE_GN_AFTER_RI 0
-#endif
 DpeContext* dpe_create(int device) {
   g_err.clear();
   int n = 0;
@@ -249,7 +214,6 @@ DpeContext* dpe_create(int device) {
   if (hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_gn0, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_ei, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming) != hipSuccess ||
       hipEventCreate(&c->ev_start) != hipSuccess) {
@@ -257,7 +221,6 @@ DpeContext* dpe_create(int device) {
     if (c->ev_start) (void)hipEventDestroy(c->ev_start);
     if (c->ev_done) (void)hipEventDestroy(c->ev_done);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
-    if (c->ev_gn0) (void)hipEventDestroy(c->ev_gn0);
     if (c->ev_ei) (void)hipEventDestroy(c->ev_ei);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->aux) (void)hipStreamDestroy(c->aux);
@@ -303,7 +266,7 @@ void dpe_destroy(DpeContext* c) {
   c->imgq8_all.release();
   c->imgq16_all.release();
   c->imgqp_all.release();
-  c->edge.release(); c->edge_low.release(); c->edge_tiles.release(); c->label.release();
+  c->edge.release(); c->edge_low.release(); c->label.release();
   c->planes0.release(); c->weak0.release(); c->sel0.release();
   c->planes.release(); c->planes_snap.release(); c->fit_plane.release();
   c->costs.release(); c->costs_snap.release(); c->complex_.release();
@@ -318,11 +281,10 @@ void dpe_destroy(DpeContext* c) {
   c->e_rows.release(); c->e_mag.release(); c->e_itab.release(); c->e_dx.release(); c->e_dy.release();
   c->e_ftab.release(); c->e_stab.release();
   c->cnt.release();
-  c->tab_right.release(); c->tab_down.release(); c->gn_ovf.release(); c->gn_tab.release(); c->gn_ecache.release();
+  c->tab_right.release(); c->tab_down.release(); c->gn_ovf.release(); c->gn_tab.release();
   c->lists.release(); c->row_counts.release(); c->list_totals.release();
   (void)hipStreamSynchronize(c->aux);
   (void)hipEventDestroy(c->ev_fork); (void)hipEventDestroy(c->ev_join); (void)hipEventDestroy(c->ev_ei);
-  (void)hipEventDestroy(c->ev_gn0);
   (void)hipStreamDestroy(c->aux);
   (void)hipStreamDestroy(c->stream);
   delete c;
@@ -367,13 +329,6 @@ static void compute_pass_constants(PassConst& pc) {
     pc.vc[v].b[1] = (float)(sK4 * trel[1] + sK5 * trel[2]);
     pc.vc[v].b[2] = (float)(sK8 * trel[2]);
   }
-  pc.cam_ik_ok = 0;
-  for (int v = 0; v < pc.N; ++v) {   // exact_div.h: reciprocals of the focal lengths, float RN
-    const float k0 = pc.cams[v].K[0], k4 = pc.cams[v].K[4];
-    pc.cam_ik[v][0] = 1.0f / k0;
-    pc.cam_ik[v][1] = 1.0f / k4;
-    if (xdiv::div_in_range(k0) && xdiv::div_in_range(k4)) pc.cam_ik_ok |= 1u << v;
-  }
   pc.kinv0 = (float)(1.0 / rK0);
   pc.kinv4 = (float)(1.0 / rK4);
   pc.kc2 = (float)(rK2 / rK0);
@@ -385,10 +340,6 @@ static void compute_pass_constants(PassConst& pc) {
   const double sr = tan((double)(angle / 2.0f) * M_PI / 180.0f) * 20;
   const int sri = (sr != sr) ? 0 : (int)sr;
   pc.gn_shift = sri < 1 ? 1 : sri;
-  // mul_hi(x, m) undershoots x / d by less than 1 for every 32-bit x (x (2^32 / d - m) / 2^32 < 1),
-  // so x - d mul_hi(x, m) lies in [0, 2d) and one conditional subtract gives x % d (gn_mod; checked
-  // for all 2^32 x and d <= 8 by tools/check_gn_mod.c)
-  pc.gn_shift_m = pc.gn_shift == 1 ? 0xFFFFFFFFu : (uint32_t)((1ull << 32) / (uint64_t)pc.gn_shift);
   pc.half_rows = std::min(pc.H, 2 * 16 * (((pc.H / 2) + 15) / 16));
   pc.weak_nn = pc.P.weak_radius >= 0 && pc.P.weak_increment > 0 ? (2 * pc.P.weak_radius) / pc.P.weak_increment + 1 : 0;
 }
@@ -642,15 +593,6 @@ static int stage_impl(DpeContext* c, const DpePassInput* in, const StageSrc& src
     HIPC(hipMemcpyAsync(c->edge.p, in->edge, L, hipMemcpyHostToDevice, c->stream));
     HIPC(hipMemcpyAsync(c->edge_low.p, in->edge_low_res, (size_t)pc.LW * pc.LH, hipMemcpyHostToDevice, c->stream));
     B.edge = c->edge.p; B.edge_low = c->edge_low.p;
-#if DPE_BRES_TILE
-    {   // 8x8 bit tiles of the low-res map for the Bresenham walks (bresenham, DPE_BRES_TILE)
-      const int tw = (pc.LW + 7) / 8, th = (pc.LH + 7) / 8;
-      HIPC(c->edge_tiles.ensure((size_t)tw * th));
-      k_edge_tiles<<<(unsigned)((tw * th + 255) / 256), 256, 0, c->stream>>>(c->edge_low.p, pc.LW, pc.LH, c->edge_tiles.p);
-      HIPC(hipGetLastError());
-      B.edge_tiles = c->edge_tiles.p;
-    }
-#endif
     HIPC(hipMemcpyAsync(c->dc.p, &pc, sizeof(PassConst), hipMemcpyHostToDevice, c->stream));
   }
   if (P.use_label) {
@@ -684,7 +626,7 @@ static int stage_impl(DpeContext* c, const DpePassInput* in, const StageSrc& src
   HIPC(c->nb.ensure(L * 9)); HIPC(c->nearest.ensure(L)); HIPC(c->edge_neigh.ensure(L * 8)); HIPC(c->lab_bound.ensure(L * 8));
   HIPC(c->radius.ensure(L));
   HIPC(c->tab_right.ensure(L)); HIPC(c->tab_down.ensure(L));
-  HIPC(c->gn_ovf.ensure(L + 64)); HIPC(c->gn_tab.ensure((size_t)W + H + kGnTabExtra));
+  HIPC(c->gn_ovf.ensure(L + 64)); HIPC(c->gn_tab.ensure((size_t)W + H));
   HIPC(c->lists.ensure(6 * (L / 2 + 64) + 3 * (L + 64))); HIPC(c->row_counts.ensure(4 * (size_t)H + 4)); HIPC(c->list_totals.ensure(16));
   B.planes = c->planes.p; B.planes_snap = c->planes_snap.p; B.fit_plane = c->fit_plane.p;
   B.planes0 = c->planes0.p;
@@ -778,164 +720,83 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   DevBufs Bc;
 
   // RunPatchMatch launch sequence (DPE.cu:3150-3226)
-  // DPE_OVERLAP=0 keeps one stream (profiling runs whose per-kernel durations must not overlap)
+  // DPE_OVERLAP=0 keeps one stream (profiling runs whose per-kernel durations must not overlap);
+  // timed / counting executes keep one stream too (per-class events)
   static const bool overlap_env = [] { const char* e = getenv("DPE_OVERLAP"); return !(e && atoi(e) == 0); }();
   // (the join into `s` sits in the first strong half-sweep, so a pass without iterations keeps one stream)
   const bool overlap = overlap_env && !timing && !c->counting && pc.P.max_iterations >= 1;
   const long list_stride = (long)(L / 2 + 64);
-  // early fork: the whole setup chain (GenEdgeInform .. GenNeighbours) on the aux stream, beside
-  // RandomInitialization; the first strong half-sweep waits for GenEdgeInform's edge rays only
-  const bool early = overlap && DPE_EARLY_FORK;
-  const hipStream_t se = early ? c->aux : s;
-  Bc = begin(DPE_CLASS_SETUP);
-  if (early) {   // pre-GenNeighbours sweep lists (the colour-0 strong list is the one used)
-    k_list_count<0><<<(pc.half_rows + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p);
-    k_list_scan<0><<<1, 256, 0, s>>>(dpc, c->row_counts.p, c->list_totals.p);
-    k_list_fill<0><<<(pc.half_rows + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p, c->lists.p, list_stride);
-    HIPC(hipEventRecord(c->ev_fork, s));
-    HIPC(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
-  }
-  k_gen_edge_inform<<<fg, fb, 0, se>>>(dpc, Bc);
-  if (DPE_EDGE_SCAN && pc.P.use_edge) k_edge_rays<<<(unsigned)(3 * (W + H) - 2), 64, 0, se>>>(dpc, Bc);
-  if (early) HIPC(hipEventRecord(c->ev_ei, se));
-  if (DPE_TABLE_SCAN) {
-    k_strong_tables_scan<<<(unsigned)(W + H), 64, 0, se>>>(dpc, Bc, c->tab_right.p, c->tab_down.p);
-  } else {
-    k_strong_tables_rows<<<(H + 63) / 64, 64, 0, se>>>(dpc, Bc, c->tab_right.p);
-    k_strong_tables_cols<<<(W + 63) / 64, 64, 0, se>>>(dpc, Bc, c->tab_down.p);
-  }
-  k_find_nearest_strong<<<fg, fb, 0, se>>>(dpc, Bc, c->tab_right.p, c->tab_down.p);
-  // list of all WEAK pixels (list slot 4), then GenNeighbours one thread per WEAK pixel.  With
-  // DPE_GN_SPLIT (early fork) the WEAK pixels come as two lists instead (MODE 3: colour 0 of the
-  // sweep grid, slot 9; the rest, slot 10), GenNeighbours runs over the first, the colour-0 failed
-  // list is built (slot 5) and signalled (ev_gn0), then GenNeighbours over the second, NeigbourUpdate
-  // and the colour-1 failed list (slot 8).  list_totals: 0..3 sweep lists, 4 WEAK, 5 / 8 failed
-  // colour 0 / 1, 6 GenNeighbours overflow, 9 / 10 split WEAK lists.
-  const bool split = early && DPE_GN_SPLIT;
-  int* weak_list = c->lists.p + 4 * list_stride;
-  int* failed_list = weak_list + L + 64;             // MODE 2 list (slot 5 of list_totals)
-  int* split_lists = failed_list + list_stride;      // MODE 3 lists, stride L + 64
-  int* failed_list1 = split_lists + 2 * (L + 64);    // MODE 4 list (slot 8)
-  if (split) {
-    k_list_count<3><<<(H + 3) / 4, 256, 0, se>>>(dpc, Bc, c->row_counts.p + 2 * (size_t)H + 2);
-    k_list_scan<3><<<1, 128, 0, se>>>(dpc, c->row_counts.p + 2 * (size_t)H + 2, c->list_totals.p + 9);
-    k_list_fill<3><<<(H + 3) / 4, 256, 0, se>>>(dpc, Bc, c->row_counts.p + 2 * (size_t)H + 2, split_lists, (long)L + 64);
-  } else {
-    k_list_count<1><<<(H + 3) / 4, 256, 0, se>>>(dpc, Bc, c->row_counts.p + 2 * (size_t)H + 2);
-    k_list_scan<1><<<1, 64, 0, se>>>(dpc, c->row_counts.p + 2 * (size_t)H + 2, c->list_totals.p + 4);
-    k_list_fill<1><<<(H + 3) / 4, 256, 0, se>>>(dpc, Bc, c->row_counts.p + 2 * (size_t)H + 2, weak_list, (long)L);
-  }
+  int* weak_list = c->lists.p + 4 * list_stride;     // all WEAK pixels (list_totals slot 4)
+  int* failed_list = weak_list + L + 64;             // colour-0 pixels whose GenNeighbours failed (slot 5)
+  // The whole setup chain (GenEdgeInform, FindNearestStrongPoint's tables, the WEAK list,
+  // GenNeighbours, NeigbourUpdate) runs on the aux stream `a`, forked at the start of the pass beside
+  // RandomInitialization; the first strong half-sweep waits for GenEdgeInform's edge rays only.
   // GenNeighbours + NeigbourUpdate only decide which WEAK pixels join the strong lists; nothing the
-  // first strong half-sweep (iteration 0, colour 0) or RandomInitialization reads is written by
-  // them, and GenNeighbours reads the staged planes, not the ones those two rewrite.  So they run
-  // on the aux stream beside RandomInitialization + that half-sweep over the pixels that were not
-  // WEAK; the colour-0 pixels whose GenNeighbours failed (NeigbourUpdate makes them UNKNOWN) get the
-  // same half-sweep (same snapshot) once the streams join.  Pixels of one half-sweep are
-  // independent, so this is the reference's order of results.  Timed / counting executes keep
-  // one stream (per-class events).
-  hipStream_t a = overlap ? c->aux : s;
-  if (overlap && !early) {   // pre-GenNeighbours sweep lists (the colour-0 strong list is the one used)
-    k_list_count<0><<<(pc.half_rows + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p);
+  // first strong half-sweep (iteration 0, colour 0) or RandomInitialization reads is written by them,
+  // and GenNeighbours reads the staged planes, not the ones those two rewrite.  So that half-sweep
+  // runs over the pre-GenNeighbours colour-0 strong list, and the colour-0 pixels whose GenNeighbours
+  // failed (NeigbourUpdate makes them UNKNOWN) get the same half-sweep (same snapshot) once the
+  // streams join.  Pixels of one half-sweep are independent, so this is the reference's order of
+  // results (GPU test test_overlapped_and_sequential_schedules_agree).
+  const hipStream_t a = overlap ? c->aux : s;
+  auto sweep_lists = [&](const DevBufs& Bl) {   // per-colour strong / weak lists of the sweeps
+    k_list_count<0><<<(pc.half_rows + 3) / 4, 256, 0, s>>>(dpc, Bl, c->row_counts.p);
     k_list_scan<0><<<1, 256, 0, s>>>(dpc, c->row_counts.p, c->list_totals.p);
-    k_list_fill<0><<<(pc.half_rows + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p, c->lists.p, list_stride);
+    k_list_fill<0><<<(pc.half_rows + 3) / 4, 256, 0, s>>>(dpc, Bl, c->row_counts.p, c->lists.p, list_stride);
+  };
+  Bc = begin(DPE_CLASS_SETUP);
+  if (overlap) {   // pre-GenNeighbours sweep lists (the colour-0 strong list is the one used)
+    sweep_lists(Bc);
+    HIPC(hipEventRecord(c->ev_fork, s));
+    HIPC(hipStreamWaitEvent(a, c->ev_fork, 0));
   }
-  // GenNeighbours + NeigbourUpdate (+ the failed-pixel list on the aux stream).  With the early fork
-  // they follow GenEdgeInform and the nearest-strong tables on the aux stream; otherwise they are
-  // forked after RandomInitialization: launched beside it, GenNeighbours' ~4.7 K long waves (all
-  // resident at once) starved it of registers (0.86 -> 8.5 ms in a kernel trace of the overlapped pass)
-  const DevBufs Bgn = Bc;
-  // GenNeighbours over one list: the scratch-free kernel plus the scratch kernel for its overflow
-  // pixels, or the scratch kernel alone (rotate_time > 4)
-  bool gn_tables = false;
-  auto gn_over = [&](const int* lst, const int* cnt) -> int {
-#if DPE_GN_LDS
-    if (pc.P.rotate_time <= 4) {   // probe slots in the reference's compaction order (dir_index < 32)
-      if (!gn_tables) { k_gn_tables<<<(unsigned)((W + H + 8 + 255) / 256), 256, 0, a>>>(dpc, c->gn_tab.p); gn_tables = true; }
-      HIPC(hipMemsetAsync(c->list_totals.p + 6, 0, sizeof(int), a));
-      const unsigned gg = (unsigned)((L + DPE_GN_BT - 1) / DPE_GN_BT);
-      uint8_t* ec = nullptr;
-      if (DPE_GN_ECACHE && pc.P.use_limit && pc.P.rotate_time <= 2) {   // 32 points: 496 pairs
-        HIPC(c->gn_ecache.ensure((size_t)496 * (L + 64)));
-        HIPC(hipMemsetAsync(c->gn_ecache.p, 0, (size_t)496 * (L + 64), a));
-        ec = c->gn_ecache.p;
-      }
-      if (c->gn_slots == 8)   // test setting: most pixels overflow into the scratch kernel
-        k_gen_neighbours_lds<8><<<gg, DPE_GN_BT, 0, a>>>(dpc, Bgn, lst, cnt, c->gn_tab.p, c->gn_ovf.p, c->list_totals.p + 6,
-                                                         nullptr, 0);
-      else if (pc.P.rotate_time <= 2 && c->gn_slots != 64)   // at most 16 x rotate_time support points
-        k_gen_neighbours_lds<32><<<gg, DPE_GN_BT, DPE_GN_LDS_PAD, a>>>(dpc, Bgn, lst, cnt, c->gn_tab.p, c->gn_ovf.p, c->list_totals.p + 6,
-                                                          ec, (long)L + 64);
-      else
-        k_gen_neighbours_lds<64><<<gg, DPE_GN_BT, 0, a>>>(dpc, Bgn, lst, cnt, c->gn_tab.p, c->gn_ovf.p, c->list_totals.p + 6,
-                                                          nullptr, 0);
-      k_gen_neighbours<<<(unsigned)((L + 255) / 256), 256, 0, a>>>(dpc, Bgn, c->gn_ovf.p, c->list_totals.p + 6);
-      return 0;
-    }
-#endif
-    k_gen_neighbours<<<(unsigned)((L + 255) / 256), 256, 0, a>>>(dpc, Bgn, lst, cnt);
-    return 0;
-  };
-  auto launch_gn = [&]() -> int {
-    if (overlap && !early) {
-      HIPC(hipEventRecord(c->ev_fork, s));
-      HIPC(hipStreamWaitEvent(a, c->ev_fork, 0));
-    }
-    if (split) {
-      if (gn_over(split_lists, c->list_totals.p + 9)) return 1;
-      k_list_count<2><<<(pc.half_rows + 3) / 4, 256, 0, a>>>(dpc, Bgn, c->row_counts.p);
-      k_list_scan<2><<<1, 64, 0, a>>>(dpc, c->row_counts.p, c->list_totals.p + 5);
-      k_list_fill<2><<<(pc.half_rows + 3) / 4, 256, 0, a>>>(dpc, Bgn, c->row_counts.p, failed_list, list_stride);
-      HIPC(hipEventRecord(c->ev_gn0, a));
-      if (gn_over(split_lists + L + 64, c->list_totals.p + 10)) return 1;
-      k_neighbour_update<<<fg, fb, 0, a>>>(dpc, Bgn);
-      k_list_count<4><<<(pc.half_rows + 3) / 4, 256, 0, a>>>(dpc, Bgn, c->row_counts.p);
-      k_list_scan<4><<<1, 64, 0, a>>>(dpc, c->row_counts.p, c->list_totals.p + 8);
-      k_list_fill<4><<<(pc.half_rows + 3) / 4, 256, 0, a>>>(dpc, Bgn, c->row_counts.p, failed_list1, list_stride);
-      HIPC(hipEventRecord(c->ev_join, a));
-      return 0;
-    }
-    if (gn_over(weak_list, c->list_totals.p + 4)) return 1;
-#ifdef DPE_GN_TWICE   // timing-only sensitivity probe (not the reference's results)
-    k_gen_neighbours<<<(unsigned)((L + 255) / 256), 256, 0, a>>>(dpc, Bgn, weak_list, c->list_totals.p + 4);
-#endif
-    k_neighbour_update<<<fg, fb, 0, a>>>(dpc, Bgn);
-    if (overlap) {
-      k_list_count<2><<<(pc.half_rows + 3) / 4, 256, 0, a>>>(dpc, Bgn, c->row_counts.p);
-      k_list_scan<2><<<1, 64, 0, a>>>(dpc, c->row_counts.p, c->list_totals.p + 5);
-      k_list_fill<2><<<(pc.half_rows + 3) / 4, 256, 0, a>>>(dpc, Bgn, c->row_counts.p, failed_list, list_stride);
-      HIPC(hipEventRecord(c->ev_join, a));
-    }
-    return 0;
-  };
-  // early fork + DPE_GN_AFTER_RI: GenNeighbours still follows the setup chain on the aux stream, but
-  // also waits for RandomInitialization, which otherwise gets CU slots only as GenNeighbours' long
-  // waves leave (0.83 ms alone, ~5 ms beside it in the overlapped timeline), delaying the first
-  // strong half-sweep; ev_fork is recorded again after it (a wait binds the record made before it)
-  const bool gn_after_ri = early && DPE_GN_AFTER_RI;
-  const bool gn_after_init = (overlap && !early && DPE_FORK_AFTER_INIT) || gn_after_ri;
-  if (!gn_after_init) { const int r = launch_gn(); if (r) return r; }
-  if (!overlap) {
-    // per-colour pixel lists of the sweeps (weak_info is fixed from here until DepthToWeak)
-    k_list_count<0><<<(pc.half_rows + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p);
-    k_list_scan<0><<<1, 256, 0, s>>>(dpc, c->row_counts.p, c->list_totals.p);
-    k_list_fill<0><<<(pc.half_rows + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p, c->lists.p, list_stride);
+  k_gen_edge_inform<<<fg, fb, 0, a>>>(dpc, Bc);
+  if (pc.P.use_edge) k_edge_rays<<<(unsigned)(3 * (W + H) - 2), 64, 0, a>>>(dpc, Bc);
+  if (overlap) HIPC(hipEventRecord(c->ev_ei, a));
+  k_strong_tables_scan<<<(unsigned)(W + H), 64, 0, a>>>(dpc, Bc, c->tab_right.p, c->tab_down.p);
+  k_find_nearest_strong<<<fg, fb, 0, a>>>(dpc, Bc, c->tab_right.p, c->tab_down.p);
+  // list of all WEAK pixels, then GenNeighbours one thread per WEAK pixel
+  k_list_count<1><<<(H + 3) / 4, 256, 0, a>>>(dpc, Bc, c->row_counts.p + 2 * (size_t)H + 2);
+  k_list_scan<1><<<1, 64, 0, a>>>(dpc, c->row_counts.p + 2 * (size_t)H + 2, c->list_totals.p + 4);
+  k_list_fill<1><<<(H + 3) / 4, 256, 0, a>>>(dpc, Bc, c->row_counts.p + 2 * (size_t)H + 2, weak_list, (long)L);
+  if (pc.P.rotate_time <= 4) {
+    // the scratch-free kernel; pixels with more support points than its LDS slots (none at the
+    // BASELINE workloads) or a NaN go to the scratch kernel, a small persistent grid that loops over
+    // that overflow list (list_totals slot 6)
+    k_gn_tables<<<(unsigned)((W + H + 255) / 256), 256, 0, a>>>(dpc, c->gn_tab.p);
+    HIPC(hipMemsetAsync(c->list_totals.p + 6, 0, sizeof(int), a));
+    const unsigned gg = (unsigned)((L + kGnBT - 1) / kGnBT);
+    const int* cnt = c->list_totals.p + 4;
+    if (c->gn_slots == 8)   // test setting: most pixels overflow into the scratch kernel
+      k_gen_neighbours_lds<8><<<gg, kGnBT, 0, a>>>(dpc, Bc, weak_list, cnt, c->gn_tab.p, c->gn_ovf.p, c->list_totals.p + 6);
+    else if (pc.P.rotate_time <= 2 && c->gn_slots != 64)   // at most 16 x rotate_time support points
+      k_gen_neighbours_lds<32><<<gg, kGnBT, 0, a>>>(dpc, Bc, weak_list, cnt, c->gn_tab.p, c->gn_ovf.p, c->list_totals.p + 6);
+    else
+      k_gen_neighbours_lds<64><<<gg, kGnBT, 0, a>>>(dpc, Bc, weak_list, cnt, c->gn_tab.p, c->gn_ovf.p, c->list_totals.p + 6);
+    k_gen_neighbours<<<kGnOvfBlocks, 256, 0, a>>>(dpc, Bc, c->gn_ovf.p, c->list_totals.p + 6);
+  } else {
+    k_gen_neighbours<<<kGnOvfBlocks, 256, 0, a>>>(dpc, Bc, weak_list, c->list_totals.p + 4);
+  }
+  k_neighbour_update<<<fg, fb, 0, a>>>(dpc, Bc);
+  if (overlap) {
+    k_list_count<2><<<(pc.half_rows + 3) / 4, 256, 0, a>>>(dpc, Bc, c->row_counts.p);
+    k_list_scan<2><<<1, 64, 0, a>>>(dpc, c->row_counts.p, c->list_totals.p + 5);
+    k_list_fill<2><<<(pc.half_rows + 3) / 4, 256, 0, a>>>(dpc, Bc, c->row_counts.p, failed_list, list_stride);
+    HIPC(hipEventRecord(c->ev_join, a));
+  } else {
+    sweep_lists(Bc);   // weak_info is fixed from here until DepthToWeak
   }
   end();
   Bc = begin(DPE_CLASS_INIT);
   if (c->img8) k_random_init<kTexInit><<<fg, fb, 0, s>>>(dpc, Bc); else k_random_init<TEX_F32><<<fg, fb, 0, s>>>(dpc, Bc);
   end();
-  if (gn_after_ri) {
-    HIPC(hipEventRecord(c->ev_fork, s));
-    HIPC(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
-  }
-  if (gn_after_init) { const int r = launch_gn(); if (r) return r; }
-  if (early) HIPC(hipStreamWaitEvent(s, c->ev_ei, 0));   // the strong sweeps read GenEdgeInform's rays
+  if (overlap) HIPC(hipStreamWaitEvent(s, c->ev_ei, 0));   // the strong sweeps read GenEdgeInform's rays
   HIPC(hipGetLastError());
   auto strong_sweep = [&](const DevBufs& Bs, int it, const int* lst, const int* cnt) {
     const bool edge = pc.P.use_edge;
     const int P = edge ? 4 : 8, C = edge ? 16 : 8;
-    const size_t lds = (size_t)DPE_BW_STRONG * strong_lds_per_wave(P, C, nv) * sizeof(float);
-    const unsigned grid = (unsigned)((L / 2 + 1 + DPE_BW_STRONG * P - 1) / (DPE_BW_STRONG * P));
+    const size_t lds = (size_t)kBwStrong * strong_lds_per_wave(P, C, nv) * sizeof(float);
+    const unsigned grid = (unsigned)((L / 2 + 1 + kBwStrong * P - 1) / (kBwStrong * P));
     launch_strong(edge, c->img8, grid, lds, s, dpc, Bs, it, lst, cnt);
   };
   for (int it = 0; it < pc.P.max_iterations; ++it) {
@@ -945,53 +806,38 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
       HIPC(hipMemcpyAsync(B.sel_snap, B.sel, L * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
       Bc = begin(DPE_CLASS_STRONG);
       strong_sweep(Bc, it, c->lists.p + (colour * 2 + 0) * list_stride, c->list_totals.p + colour * 2 + 0);
-      if (overlap && it == 0 && (colour == 0 || split)) {
-        // this colour's pixels whose GenNeighbours failed (UNKNOWN after NeigbourUpdate), same snapshot;
-        // split: colour 0 once GenNeighbours has finished the colour-0 grid pixels, colour 1 (whose
-        // pre-GenNeighbours list ran above) at the join
-        const bool last = !split || colour == 1;
-        HIPC(hipStreamWaitEvent(s, last ? c->ev_join : c->ev_gn0, 0));
-        strong_sweep(Bc, it, colour == 0 ? failed_list : failed_list1, c->list_totals.p + (colour == 0 ? 5 : 8));
-        if (last) {
-          // the sweep lists after NeigbourUpdate (weak_info is fixed from here until DepthToWeak)
-          k_list_count<0><<<(pc.half_rows + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p);
-          k_list_scan<0><<<1, 256, 0, s>>>(dpc, c->row_counts.p, c->list_totals.p);
-          k_list_fill<0><<<(pc.half_rows + 3) / 4, 256, 0, s>>>(dpc, Bc, c->row_counts.p, c->lists.p, list_stride);
-        }
+      if (overlap && it == 0 && colour == 0) {
+        // the colour-0 pixels whose GenNeighbours failed (UNKNOWN after NeigbourUpdate), same snapshot
+        HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
+        strong_sweep(Bc, it, failed_list, c->list_totals.p + 5);
+        sweep_lists(Bc);   // the sweep lists after NeigbourUpdate (weak_info is fixed until DepthToWeak)
       }
       end();
     }
     HIPC(hipGetLastError());
-    // DPE_RANSAC_SPLIT (with the two-stream weak sweeps): each colour's RANSACToGetFitPlane over that
-    // colour's weak list, on that colour's stream, just before its weak sweep (a fit reads STRONG
-    // pixels and writes its own pixel's fit plane, which only its own weak update reads)
-    const bool ransac_split = overlap && DPE_WEAK_PAR && DPE_RANSAC_SPLIT && !split;
-    const unsigned rl_grid = (unsigned)((L / 2 + 1 + kRansacThreads - 1) / kRansacThreads);
-    Bc = begin(DPE_CLASS_RANSAC);
-    if (ransac_split) {   // fork first: the colour-1 fit must not wait for the colour-0 one
-      HIPC(hipEventRecord(c->ev_fork, s));
-      HIPC(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
-      k_ransac_fit<true><<<rl_grid, kRansacThreads, 0, c->aux>>>(dpc, Bc, it, c->lists.p + 3 * list_stride, c->list_totals.p + 3);
-      k_ransac_fit<true><<<rl_grid, kRansacThreads, 0, s>>>(dpc, Bc, it, c->lists.p + 1 * list_stride, c->list_totals.p + 1);
-    } else if (DPE_RANSAC_LIST && !split)   // the WEAK list of slot 4 (built before GenNeighbours, kept to the end)
-      k_ransac_fit<true><<<(unsigned)((L + kRansacThreads - 1) / kRansacThreads), kRansacThreads, 0, s>>>(dpc, Bc, it, weak_list,
-                                                                                                         c->list_totals.p + 4);
-    else
-      k_ransac_fit<false><<<rg, rb, 0, s>>>(dpc, Bc, it, nullptr, nullptr);
-    end();
     // The two colours' weak sweeps read only STRONG pixels' state besides their own pixel (planes and
     // selected views of the GenNeighbours support points, DPE.cu:1690-1725; the NCC-New patches come
-    // from the images), and write only their own pixel, so they are independent: with DPE_WEAK_PAR the
-    // colour-1 sweep runs on the aux stream beside the colour-0 one (the launch tails overlap)
-    const bool weak_par = overlap && DPE_WEAK_PAR;
-    if (weak_par && !ransac_split) {
+    // from the images), and write only their own pixel, so they are independent: the colour-1 sweep
+    // runs on the aux stream beside the colour-0 one (the launch tails overlap).  Each colour's
+    // RANSACToGetFitPlane over that colour's weak list runs on that colour's stream just before its
+    // sweep (a fit reads STRONG pixels and writes its own pixel's fit plane, which only its own weak
+    // update reads).
+    const unsigned rl_grid = (unsigned)((L / 2 + 1 + kRansacThreads - 1) / kRansacThreads);
+    if (overlap) {   // fork first: the colour-1 fit must not wait for the colour-0 one
       HIPC(hipEventRecord(c->ev_fork, s));
       HIPC(hipStreamWaitEvent(c->aux, c->ev_fork, 0));
     }
+    Bc = begin(DPE_CLASS_RANSAC);
+    for (int colour = 1; colour >= 0; --colour) {
+      const hipStream_t sr = colour == 1 ? a : s;
+      k_ransac_fit<<<rl_grid, kRansacThreads, 0, sr>>>(dpc, Bc, it, c->lists.p + (colour * 2 + 1) * list_stride,
+                                                        c->list_totals.p + colour * 2 + 1);
+    }
+    end();
     for (int colour = 0; colour < 2; ++colour) {
       Bc = begin(DPE_CLASS_WEAK);
       {
-        const hipStream_t sw = weak_par && colour == 1 ? c->aux : s;
+        const hipStream_t sw = colour == 1 ? a : s;
         const int* lst = c->lists.p + (colour * 2 + 1) * list_stride;
         const int* cnt = c->list_totals.p + colour * 2 + 1;
         constexpr int C = kWeakLanes, P = 64 / C;
@@ -1003,7 +849,7 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
       }
       end();
     }
-    if (weak_par) {
+    if (overlap) {
       HIPC(hipEventRecord(c->ev_join, c->aux));
       HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
     }
@@ -1507,9 +1353,10 @@ extern "C" int dpe_set_option(DpeContext* c, int option, int value) {
 
 extern "C" long long dpe_pm_last_stat(DpeContext* c, int stat) {
   if (!c || !c->staged || stat != DPE_STAT_GN_DEFERRED || !c->list_totals.p) return -1;
-  int v = 0;
-  if (hipSetDevice(c->device) != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
-      hipMemcpy(&v, c->list_totals.p + 6, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+  int v = 0;   // waits for this context's pass only (not the whole device)
+  if (hipSetDevice(c->device) != hipSuccess || wait_pending(c) != hipSuccess || hipStreamSynchronize(c->aux) != hipSuccess ||
+      hipMemcpyAsync(&v, c->list_totals.p + 6, sizeof(int), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+      hipStreamSynchronize(c->stream) != hipSuccess)
     return -1;
   return v;
 }

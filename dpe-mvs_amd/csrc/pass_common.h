@@ -17,7 +17,6 @@
 #pragma once
 #include "device_math.h"
 #include "bres_walk.h"
-#include "exact_div.h"
 #include "../../include/dpe_mvs.h"
 
 namespace dpe {
@@ -36,8 +35,6 @@ struct PassConst {
   DpePatchMatchParams P;
   DpeCamera cams[DPE_MAX_IMAGES];
   ViewConst vc[DPE_MAX_IMAGES];
-  float cam_ik[DPE_MAX_IMAGES][2];   // RN(1 / K[0]), RN(1 / K[4]) of each camera (exact_div.h)
-  uint32_t cam_ik_ok;                // bit v: camera v's K[0], K[4] in div_in_range (else IEEE division)
 };
 
 struct DevBufs {
@@ -57,7 +54,6 @@ struct DevBufs {
   short2* nb; short2* nearest; short2* edge_neigh; short2* lab_bound;
   int* radius;
   const uint8_t* edge; const uint8_t* edge_low; const int* label;
-  const uint64_t* edge_tiles;   // low-res edge map as 8x8 bit tiles (DPE_BRES_TILE), bit (y & 7) * 8 + (x & 7)
   // algorithmic work counters of the launch class (nullptr unless counting):
   // [0] homographies (NCC set-ups), [1] bilinear taps, [2] geometric-consistency evaluations
   unsigned long long* cnt;
@@ -65,11 +61,20 @@ struct DevBufs {
   int xcd_rows;   // block rows per XCD chunk (0 = dispatcher order)
 };
 
-// Phase profiling (build with -DDPE_PHASE_PROF=1; tools/phase_prof.sh): shader-clock cycles of
-// each phase of a cooperative kernel, summed over waves into B.phase[k].
-#ifndef DPE_PHASE_PROF
-#define DPE_PHASE_PROF 0
+// Diagnostic builds, -DDPE_DIAG=<bits> (none of them changes a result; the product is DPE_DIAG=0):
+//   1  phase cycle sums of the cooperative kernels (tools/phase_prof.py)
+//   2  gather-line statistics of the fast tap loops (tools/line_stats.py)
+//   4  weak-sweep path statistics (tools/weak_stats.py)
+//   8  GenNeighbours per-pixel clocks and counts (tools/gn_times.py)
+#ifndef DPE_DIAG
+#define DPE_DIAG 0
 #endif
+#define DPE_PHASE_PROF ((DPE_DIAG) & 1)
+#define DPE_LINE_STATS (((DPE_DIAG) >> 1) & 1)
+#define DPE_WEAK_STATS (((DPE_DIAG) >> 2) & 1)
+#define DPE_GN_TIMES (((DPE_DIAG) >> 3) & 1)
+// Phase profiling (DPE_DIAG & 1): shader-clock cycles of each phase of a cooperative kernel,
+// summed over waves into B.phase[k].
 #if DPE_PHASE_PROF
 #define PHASE_BEGIN() uint64_t ph_t_ = __builtin_readcyclecounter(), ph_acc_[16] = {}
 #define PHASE(k)                                                                    \
@@ -175,38 +180,6 @@ DEV float2 project_cam(const float3& X, const DpeCamera& c) {                 //
   const float tz = c.R[6] * X.x + c.R[7] * X.y + c.R[8] * X.z + c.t[2];
   const float d = c.K[6] * tx + c.K[7] * ty + c.K[8] * tz;
   return make_float2((c.K[0] * tx + c.K[1] * ty + c.K[2] * tz) / d, (c.K[3] * tx + c.K[4] * ty + c.K[5] * tz) / d);
-}
-
-// The geometric-consistency term's divisions as exact_div.h quotients (same operations before each
-// division, the IEEE quotient bit for bit).  The fast form runs straight through and only collects
-// whether every operand was in div_in_range; a lane with one that was not recomputes the term with
-// the IEEE divisions (geom_cost_at's caller-visible result is the same either way).
-// DPE_GEOM_MDIV 0: world_point / project_cam as written.
-#ifndef DPE_GEOM_MDIV
-#define DPE_GEOM_MDIV 0   // A/B: +0.4 ms DepthToWeak (profiles/r04_ab_geom_mdiv.log), not adopted
-#endif
-DEV float3 world_point_m(const DpeCamera& c, float ik0, float ik4, float x, float y, float depth, bool& ok) {
-  const float ax = depth * (x - c.K[2]), ay = depth * (y - c.K[5]);
-  ok = ok && xdiv::div_in_range(ax) && xdiv::div_in_range(ay);
-  float3 X;
-  X.x = xdiv::div_markstein(ax, c.K[0], ik0);
-  X.y = xdiv::div_markstein(ay, c.K[4], ik4);
-  X.z = depth;
-  float3 T;
-  T.x = c.R[0] * X.x + c.R[3] * X.y + c.R[6] * X.z;
-  T.y = c.R[1] * X.x + c.R[4] * X.y + c.R[7] * X.z;
-  T.z = c.R[2] * X.x + c.R[5] * X.y + c.R[8] * X.z;
-  return make_float3(T.x + c.c[0], T.y + c.c[1], T.z + c.c[2]);
-}
-DEV float2 project_cam_m(const float3& X, const DpeCamera& c, bool& ok) {
-  const float tx = c.R[0] * X.x + c.R[1] * X.y + c.R[2] * X.z + c.t[0];
-  const float ty = c.R[3] * X.x + c.R[4] * X.y + c.R[5] * X.z + c.t[1];
-  const float tz = c.R[6] * X.x + c.R[7] * X.y + c.R[8] * X.z + c.t[2];
-  const float d = c.K[6] * tx + c.K[7] * ty + c.K[8] * tz;
-  const float nx = c.K[0] * tx + c.K[1] * ty + c.K[2] * tz, ny = c.K[3] * tx + c.K[4] * ty + c.K[5] * tz;
-  ok = ok && xdiv::div_in_range(d) && xdiv::div_in_range(nx) && xdiv::div_in_range(ny);
-  const float yd = d_rcp_fast(d);   // RN(1/d) while d's biased exponent is in [67, 187]
-  return make_float2(xdiv::div_markstein(nx, d, yd), xdiv::div_markstein(ny, d, yd));
 }
 
 // GenerateRandomNormal (DPE.cu:361-387)
@@ -350,31 +323,6 @@ DEV bool rcp_range_ok(const Homog& H, float x0, float x1, float y0, float y1) {
          amax < 1.2676506002282294e+30f;
 }
 
-// True when every tap of the rectangle projects into [0, W - 1] x [0, H - 1], so the clamp of the
-// fixed-point coordinate (tex_t_fast) is the identity for all of them.  Call only after
-// rcp_range_ok on the same rectangle (qz of one sign, exact reciprocal).  The corners are computed
-// with the taps' own operations; with qz of one sign the exact projective map of the rectangle lies
-// within its corner values, and the computed taps differ from the exact map by < 1e-3 px for any
-// corner value below W, so the one-pixel margin covers the rounding.  NaN -> false.
-DEV bool patch_inside(const Homog& H, float x0, float x1, float y0, float y1, int W, int Hh) {
-  const float lx = (float)(W - 1), ly = (float)(Hh - 1);
-  bool ok = true;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const float x = i ? x1 : x0;
-    const float bx = __builtin_fmaf(H.h[0], x, H.h[2]), by = __builtin_fmaf(H.h[3], x, H.h[5]);
-    const float bz = __builtin_fmaf(H.h[6], x, H.h[8]);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const float y = j ? y1 : y0;
-      const float iz = d_rcp_fast(__builtin_fmaf(H.h[7], y, bz));
-      const float sx = __builtin_fmaf(H.h[1], y, bx) * iz, sy = __builtin_fmaf(H.h[4], y, by) * iz;
-      ok = ok && sx <= lx && sy <= ly && sx >= 0.0f && sy >= 0.0f;   // NaN -> false
-    }
-  }
-  return ok;
-}
-
 // ------------------------------------------------------------------------------ sampling
 DEV float ref_texel(const float* ref, int W, int H, int x, int y) {
   x = x < 0 ? 0 : (x > W - 1 ? W - 1 : x);
@@ -393,25 +341,15 @@ DEV float ref_texel(const float* ref, int W, int H, int x, int y) {
 // trunc(fma(q·iz, 256, 256.5)): a multiply, an FMA, a clamp and a half-rate conversion).  The clamp
 // is taken on t (monotone; NaN -> the low end), and the bound |256 s + 256| < 2^22 for unclamped taps
 // holds for images narrower than 16383 px (dpe_pm_stage checks).
-// DPE_TEX_FRACT=1 (round 3): the same U on the 1/256-unit grid of [2^15, 2^16) instead of the unit grid
+// Round 3: the same U on the 1/256-unit grid of [2^15, 2^16) instead of the unit grid
 // of [2^23, 2^24): t' = fma(q, iz, 1.5·2^15 + 1) = t / 256 exactly (scaling by a power of two commutes
 // with the FMA's one rounding, and the row terms are no longer scaled), its encoding still differs
 // from that of 1.5·2^15 by U, and the tap's weight (U & 255) / 256 is v_fract_f32(t') straight from
 // the float (one full-rate op in place of v_cvt_f32_ubyte0 + a multiply per axis).
-#ifndef DPE_TEX_FRACT
-#define DPE_TEX_FRACT 1
-#endif
-#if DPE_TEX_FRACT
 constexpr float kTexMagic = 49152.0f;             // 1.5 * 2^15
 constexpr uint32_t kTexMagicBits = 0x47400000u;   // its encoding
 constexpr uint32_t kTexMagicHi = 0x474000u;       // encoding >> 8: texel index bias of t >> 8
 constexpr float kTexUnit = 1.0f;                  // one texel in t units
-#else
-constexpr float kTexMagic = 12582912.0f;          // 1.5 * 2^23
-constexpr uint32_t kTexMagicBits = 0x4B400000u;   // its encoding
-constexpr uint32_t kTexMagicHi = 0x4B4000u;       // encoding >> 8: texel index bias of t >> 8
-constexpr float kTexUnit = 256.0f;
-#endif
 DEV float tex_tmax(int lim) { return kTexMagic + kTexUnit * (float)(lim + 1); }   // t of U = 256 lim + 256
 // clamped t of a tap with scaled row value Q (generic path: NaN -> kTexMagic)
 DEV float tex_t(float Q, float iz, float tmax) {
@@ -420,13 +358,8 @@ DEV float tex_t(float Q, float iz, float tmax) {
 }
 // bilinear weight (U & 255) / 256 of a clamped t whose encoding is `bits`
 DEV float tex_frac(float t, uint32_t bits) {
-#if DPE_TEX_FRACT
   (void)bits;
   return __builtin_amdgcn_fractf(t);
-#else
-  (void)t;
-  return (float)(bits & 255u) * 0.00390625f;
-#endif
 }
 // The taps' numerators Q = 256 q: the column coefficients h1, h4 scaled by 256 here, the row terms
 // (h0 x + h2, h3 x + h5) scaled after their FMA (the oracle's OracleSampleQ caller does the same).
@@ -475,20 +408,10 @@ template <int T> DEV uint32_t tex_view(const DevBufs& B) {
 template <int T> constexpr uint32_t tex_bytes() { return T == TEX_F16 ? 8u : 4u; }
 template <int T> DEV uint32_t tex_stride(int W) { return (uint32_t)(W + (T == TEX_P16 ? 3 : 2)); }
 // the two row interpolations (r0 at y0, r1 at y1) of the texel at `p` for the x weight ax = fx / 256
-// DPE_FAKE_GATHER=1: timing-only diagnostic (wrong results): the P16 / F16 texel comes from its
-// address bits instead of memory, so the tap loops keep their VALU work without the gathers
-#ifndef DPE_FAKE_GATHER
-#define DPE_FAKE_GATHER 0
-#endif
 template <int T>
 DEV void texel_rows(const uint8_t* p, float ax, float& r0, float& r1) {
   if constexpr (T == TEX_P16) {
-#if DPE_FAKE_GATHER
-    const uint32_t lo = (uint32_t)(uintptr_t)p;
-    const uint2 t = make_uint2((lo & 0x00FF00FFu) | 0x58005800u, (lo & 0x00FF00FFu) | 0x58005900u);
-#else
     const uint2 t = *(const uint2_a4*)p;                 // (a, c), (b, d)
-#endif
     const h2v df = __builtin_bit_cast(h2v, t.y) - __builtin_bit_cast(h2v, t.x);
     const uint32_t d = __builtin_bit_cast(uint32_t, df);
     asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(r0) : "v"(ax), "v"(d), "v"(t.x));
@@ -496,12 +419,7 @@ DEV void texel_rows(const uint8_t* p, float ax, float& r0, float& r1) {
   } else if constexpr (T == TEX_F16) {
     // v_fma_mix_f32 is fma(ax, (float)half, (float)half) with one rounding; the compiler only forms
     // it under f32 denormal flushing, which cannot matter here (|ax*d| >= 2^-8 or 0, a integer)
-#if DPE_FAKE_GATHER
-    const uint32_t lo = (uint32_t)(uintptr_t)p;
-    const uint2 t = make_uint2((lo & 0x00FF00FFu) | 0x58005800u, (lo & 0x00FF00FFu) | 0x58005900u);
-#else
     const uint2 t = *(const uint2*)p;
-#endif
     asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(r0) : "v"(ax), "v"(t.y), "v"(t.x));
     asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[0,1,1] op_sel_hi:[0,1,1]" : "=v"(r1) : "v"(ax), "v"(t.y), "v"(t.x));
   } else {
@@ -524,33 +442,19 @@ DEV float sample_quad8(const uint8_t* __restrict__ q, int W, int H, float Qx, fl
   return __builtin_fmaf(ay, r1 - r0, r0);
 }
 // The default 36-tap patch (strong radius 5, increment 2) that the tabulated fast paths serve.
-#ifndef DPE_FAST_PATCH
-#define DPE_FAST_PATCH(pc) ((pc).P.strong_radius == 5 && (pc).P.strong_increment == 2)
-#endif
+// (a macro, not a function: the short-circuit keeps the second load behind a branch, as in round 4)
+#define FAST_PATCH(pc) ((pc).P.strong_radius == 5 && (pc).P.strong_increment == 2)
 // Minimum waves per SIMD the tap-heavy kernels are compiled for (register cap 512 / waves).
-#ifndef DPE_TAP_WAVES
-#define DPE_TAP_WAVES 4
-#endif
-// 1: unroll the 6 rows of the 36-tap patch loop (more ILP, more registers)
-#ifndef DPE_UNROLL_ROWS
-#define DPE_UNROLL_ROWS 1
-#endif
-// 1: the u8 fast tap uses packed FP32 / med3 / one-base 32-bit offsets (tap_u8_fast)
-#ifndef DPE_PACKED_TAP
-#define DPE_PACKED_TAP 1
-#endif
+constexpr int kTapWaves = 4;
 
 typedef float f2v __attribute__((ext_vector_type(2)));
 DEV f2v f2s(float a) { return (f2v){a, a}; }
 DEV f2v fma2(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
 
-// Gather-locality diagnostic (build with -DDPE_LINE_STATS=1; tools/line_stats.py): for every wave
+// Gather-locality diagnostic (DPE_DIAG & 2; tools/line_stats.py): for every wave
 // gather of a fast-path tap, the number of distinct 128-B lines and 64-B sectors its active lanes
 // touch, summed per texel layout T in a per-translation-unit device array (read back with
 // dpe_dbg_line_stats).  Off in the product.
-#ifndef DPE_LINE_STATS
-#define DPE_LINE_STATS 0
-#endif
 #if DPE_LINE_STATS
 static __device__ unsigned long long g_lstat[4][4];   // [T][loads, lines, quad lines, active lanes]
 DEV void line_stat(int T, const void* p) {
@@ -595,24 +499,20 @@ DEV f2v tex_tmax2(int W, int H) { return (f2v){tex_tmax(W), tex_tmax(H)}; }
 template <int T> DEV uint32_t tex_vadj(uint32_t vofs, uint32_t stride) {
   return vofs - kTexMagicHi * (stride + 1u) * tex_bytes<T>();
 }
-// clamped t of the fast path (no NaN there: rcp_range_ok), or unclamped when IN (patch_inside)
-template <bool IN>
-DEV float tex_t_fast(float t, float tmax) {
-  if constexpr (IN) return t;
-  else return __builtin_amdgcn_fmed3f(t, kTexMagic, tmax);
-}
+// clamped t of the fast path (no NaN there: rcp_range_ok)
+DEV float tex_t_fast(float t, float tmax) { return __builtin_amdgcn_fmed3f(t, kTexMagic, tmax); }
 
 // One bilinear tap of the 8-bit quad image (layout T) at the view offset `vadj` (tex_vadj), from
 // the homography h with scaled column coefficients (scale_cols) and its row terms
 // bxy = 256 (h0 x + h2, h3 x + h5), bz = h6 x + h8; column yf.  Bit-identical to sample_quad8
 // when the tap's qz is in d_rcp_fast's exact range (rcp_range_ok).
-template <int T, bool IN = false>
+template <int T>
 DEV float tap_u8_fast(const DevBufs& B, uint32_t vadj, uint32_t stride, f2v tmax, const float* h, f2v bxy, float bz,
                       float yf) {
   const f2v q = fma2((f2v){h[1], h[4]}, f2s(yf), bxy);
   const float iz = d_rcp_fast(__builtin_fmaf(h[7], yf, bz));
   const f2v t = fma2(q, f2s(iz), f2s(kTexMagic + kTexUnit));
-  const float ctx = tex_t_fast<IN>(t.x, tmax.x), cty = tex_t_fast<IN>(t.y, tmax.y);
+  const float ctx = tex_t_fast(t.x, tmax.x), cty = tex_t_fast(t.y, tmax.y);
   const uint32_t ux = __float_as_uint(ctx), uy = __float_as_uint(cty);
   const uint8_t* p = tex_base<T>(B) + (vadj + (__umul24(uy >> 8, stride) + (ux >> 8)) * tex_bytes<T>());
   LINE_STAT(T, p);
@@ -634,27 +534,17 @@ DEV float tap_u8_fast(const DevBufs& B, uint32_t vadj, uint32_t stride, f2v tmax
 // Two taps of one patch row (columns yf.x, yf.y) with the projection, reciprocal refinement and
 // the coordinate FMAs packed across the two taps; per element the same operations as tap_u8_fast,
 // so each result is bit-identical to it.
-#ifndef DPE_EXP_CHEAP
-#define DPE_EXP_CHEAP 0
-#endif
-#ifndef DPE_TAP_PAIR
-#define DPE_TAP_PAIR 1
-#endif
 // `base` is the texel array the byte offsets index (tex_base of the layout; vadj selects the view).
-template <int T, bool IN = false>
+template <int T>
 DEV f2v tap2_at(const uint8_t* base, uint32_t vadj, uint32_t stride, f2v tmax, const float* h, f2v bxy, float bz, f2v yf) {
   const f2v qx = fma2(f2s(h[1]), yf, f2s(bxy.x));
   const f2v qy = fma2(f2s(h[4]), yf, f2s(bxy.y));
   const f2v qz = fma2(f2s(h[7]), yf, f2s(bz));
   const f2v r = (f2v){__builtin_amdgcn_rcpf(qz.x), __builtin_amdgcn_rcpf(qz.y)};
-#if DPE_EXP_CHEAP   // timing experiment only (not bit-exact): no Newton step
-  const f2v iz = r;
-#else
   const f2v iz = fma2(fma2(-qz, r, f2s(1.0f)), r, r);
-#endif
   const f2v tx = fma2(qx, iz, f2s(kTexMagic + kTexUnit)), ty = fma2(qy, iz, f2s(kTexMagic + kTexUnit));
-  const float cx0 = tex_t_fast<IN>(tx.x, tmax.x), cx1 = tex_t_fast<IN>(tx.y, tmax.x);
-  const float cy0 = tex_t_fast<IN>(ty.x, tmax.y), cy1 = tex_t_fast<IN>(ty.y, tmax.y);
+  const float cx0 = tex_t_fast(tx.x, tmax.x), cx1 = tex_t_fast(tx.y, tmax.x);
+  const float cy0 = tex_t_fast(ty.x, tmax.y), cy1 = tex_t_fast(ty.y, tmax.y);
   const uint32_t ux0 = __float_as_uint(cx0), ux1 = __float_as_uint(cx1);
   const uint32_t uy0 = __float_as_uint(cy0), uy1 = __float_as_uint(cy1);
   const uint8_t* p0 = base + (vadj + (__umul24(uy0 >> 8, stride) + (ux0 >> 8)) * tex_bytes<T>());
@@ -668,9 +558,9 @@ DEV f2v tap2_at(const uint8_t* base, uint32_t vadj, uint32_t stride, f2v tmax, c
   const f2v r0 = (f2v){a0, b0}, r1 = (f2v){a1, b1};
   return fma2(ay, r1 - r0, r0);
 }
-template <int T, bool IN = false>
+template <int T>
 DEV f2v tap2_fast(const DevBufs& B, uint32_t vadj, uint32_t stride, f2v tmax, const float* h, f2v bxy, float bz, f2v yf) {
-  return tap2_at<T, IN>(tex_base<T>(B), vadj, stride, tmax, h, bxy, bz, yf);
+  return tap2_at<T>(tex_base<T>(B), vadj, stride, tmax, h, bxy, bz, yf);
 }
 
 // Sample of view v at the tap with scaled numerators (Qx, Qy) and reciprocal denominator iz.
@@ -931,7 +821,8 @@ DEV float3 geom_point(const PassConst& pc, int px, int py, const float4& pl) {
   const float depth = depth_from_plane(rc, pl, px, py);
   return world_point((float)px, (float)py, depth, rc);
 }
-DEV float geom_cost_ieee(const PassConst& pc, const DevBufs& B, int px, int py, int v, const float3& fw) {
+DEV float geom_cost_at(const PassConst& pc, const DevBufs& B, int px, int py, int v, const float3& fw) {
+  if (B.cnt) atomicAdd(B.cnt + 2, 1ull);
   const DpeCamera& rc = pc.cams[0];
   const DpeCamera& sc = pc.cams[v];
   const float2 sp = project_cam(fw, sc);
@@ -939,42 +830,6 @@ DEV float geom_cost_ieee(const PassConst& pc, const DevBufs& B, int px, int py, 
   if (src_depth == 0.0f) return 3.0f;
   const float3 s3 = world_point(sp.x, sp.y, src_depth, sc);
   const float2 bp = project_cam(s3, rc);
-  const float dc = (float)px - bp.x, dr = (float)py - bp.y;
-  const float cc = __builtin_sqrtf(dc * dc + dr * dr);
-  return __builtin_fminf(3.0f, cc);
-}
-DEV float geom_cost_at(const PassConst& pc, const DevBufs& B, int px, int py, int v, const float3& fw) {
-  if (B.cnt) atomicAdd(B.cnt + 2, 1ull);
-  if (!DPE_GEOM_MDIV) return geom_cost_ieee(pc, B, px, py, v, fw);
-  const DpeCamera& rc = pc.cams[0];
-  const DpeCamera& sc = pc.cams[v];
-  bool ok1 = true, ok2 = (pc.cam_ik_ok >> v) & 1u;
-  const float2 sp = project_cam_m(fw, sc, ok1);
-  const float src_depth = depth_texel(B.depth[v], pc.W, pc.H, sp.x, sp.y);
-  const float3 s3 = world_point_m(sc, pc.cam_ik[v][0], pc.cam_ik[v][1], sp.x, sp.y, src_depth, ok2);
-  const float2 bp = project_cam_m(s3, rc, ok2);
-  const float dc = (float)px - bp.x, dr = (float)py - bp.y;
-  const float cc = __builtin_sqrtf(dc * dc + dr * dr);
-  const bool miss = src_depth == 0.0f;
-  float g = miss ? 3.0f : __builtin_fminf(3.0f, cc);
-  // a missing source depth needs only the first projection's range (the rest is not used)
-  if (__builtin_expect(!ok1 || (!miss && !ok2), 0)) g = geom_cost_ieee(pc, B, px, py, v, fw);
-  return g;
-}
-// geom_cost_at in two halves, so that a caller can issue the source-depth gather before other work
-// (same operations, same result): geom_fetch projects and loads, geom_finish completes
-struct GeomFetch { float2 sp; float depth; };
-DEV GeomFetch geom_fetch(const PassConst& pc, const DevBufs& B, int v, const float3& fw) {
-  GeomFetch g;
-  g.sp = project_cam(fw, pc.cams[v]);
-  g.depth = depth_texel(B.depth[v], pc.W, pc.H, g.sp.x, g.sp.y);
-  return g;
-}
-DEV float geom_finish(const PassConst& pc, const DevBufs& B, int px, int py, int v, const GeomFetch& g) {
-  if (B.cnt) atomicAdd(B.cnt + 2, 1ull);
-  if (g.depth == 0.0f) return 3.0f;
-  const float3 s3 = world_point(g.sp.x, g.sp.y, g.depth, pc.cams[v]);
-  const float2 bp = project_cam(s3, pc.cams[0]);
   const float dc = (float)px - bp.x, dr = (float)py - bp.y;
   const float cc = __builtin_sqrtf(dc * dc + dr * dr);
   return __builtin_fminf(3.0f, cc);
@@ -992,15 +847,7 @@ DEV uint8_t low_edge_at(const PassConst& pc, const DevBufs& B, int idx) {
 // reference returns at the first edge pixel it meets, so the result is "any edge pixel among the
 // positions the walk visits before it stops".  Positions are generated in batches of 8 and their
 // loads issued together: one memory latency per batch instead of one per step.
-#ifndef DPE_BRES_BATCH
-#define DPE_BRES_BATCH 8
-#endif
-#ifndef DPE_BRES_TILE
-#define DPE_BRES_TILE 0     // walks tested against 8x8 bit tiles of the map (bres_walk.h walk_tiles)
-#endif
-#ifndef DPE_BRES_TILES
-#define DPE_BRES_TILES 4    // tiles loaded per round trip of walk_tiles
-#endif
+constexpr int kBresBatch = 8;
 DEV bool bresenham(const PassConst& pc, const DevBufs& B, int Ax, int Ay, int Bx, int By) {
   const int W = pc.W;
   if (B.edge[Ax + Ay * W] || B.edge[Bx + By * W]) return false;
@@ -1015,11 +862,7 @@ DEV bool bresenham(const PassConst& pc, const DevBufs& B, int Ax, int Ay, int Bx
     const int y0 = (int)MINo(__builtin_roundf(fy * scale_y), (float)(height - 1));
     const int x1 = (int)MINo(__builtin_roundf(tx * scale_x), (float)(width - 1));
     const int y1 = (int)MINo(__builtin_roundf(ty * scale_y), (float)(height - 1));
-#if DPE_BRES_TILE
-    if (bres::walk_tiles<DPE_BRES_TILES>(bres::start(x0, y0, x1, y1, max_step), B.edge_tiles, width, height)) return true;
-#else
-    if (bres::walk_bytes_flat<DPE_BRES_BATCH>(x0, y0, x1, y1, max_step, B.edge_low, width, height)) return true;
-#endif
+    if (bres::walk_bytes_flat<kBresBatch>(x0, y0, x1, y1, max_step, B.edge_low, width, height)) return true;
   }
   return false;
 }

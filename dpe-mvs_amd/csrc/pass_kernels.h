@@ -32,9 +32,6 @@ namespace dpe {
 // LDS (bit 0 edge, bit 1 label 0, bit 2 inside the image) for r <= kEiTileR; the counts are
 // integers, so the tile changes nothing but the number of global loads (r^2 per pixel -> ~1.6).
 constexpr int kEiTileR = 8, kEiTile = 16 + 2 * kEiTileR;
-#ifndef DPE_EI_SEP
-#define DPE_EI_SEP 0   // the window counts as a row pass and a column pass over the tile (exact integer sums)
-#endif
 // GenEdgeInform's 8 edge rays (DPE.cu:2497-2530: the first edge pixel along each direction, to the
 // image border) as line scans: every pixel lies on one row, one column, one diagonal (x - y const)
 // and one anti-diagonal (x + y const); along a line the ray in one direction is the nearest edge
@@ -42,9 +39,6 @@ constexpr int kEiTileR = 8, kEiTile = 16 + 2 * kEiTileR;
 // positions per step: the edge bits of a step by ballot, the nearest set bit above / below each lane
 // by bit arithmetic, the nearest edge beyond the step carried from the steps already done (the
 // lines are walked once from each end).  Same positions as the per-pixel walks, O(L) loads in all.
-#ifndef DPE_EDGE_SCAN
-#define DPE_EDGE_SCAN 1
-#endif
 __global__ void __launch_bounds__(64) k_edge_rays(const PassConst* __restrict__ pcp, DevBufs B) {
   const PassConst& pc = *pcp;
   const int W = pc.W, H = pc.H;
@@ -100,9 +94,6 @@ __global__ void __launch_bounds__(64) k_edge_rays(const PassConst* __restrict__ 
 __global__ void __launch_bounds__(256) k_gen_edge_inform(const PassConst* __restrict__ pcp, DevBufs B) {   // DPE.cu:2483-2591
   const PassConst& pc = *pcp;
   __shared__ uint8_t s_tile[kEiTile * kEiTile];
-#if DPE_EI_SEP
-  __shared__ uint32_t s_hsum[kEiTile][16];
-#endif
   const int radius = pc.P.strong_radius;
   const bool tiled = pc.P.use_edge && radius >= 0 && radius <= kEiTileR;
   if (tiled) {   // block-uniform; every thread of the block helps before any returns
@@ -119,53 +110,11 @@ __global__ void __launch_bounds__(256) k_gen_edge_inform(const PassConst* __rest
       s_tile[t] = v;
     }
     __syncthreads();
-#if DPE_EI_SEP
-    // separable window counts: each tile row's (2r+1)-wide sums for the block's 16 columns, the three
-    // counts packed 10 bits apart (at most 17 x 17 = 289 each), then 2r+1 of them down each column
-    for (int t = threadIdx.y * blockDim.x + threadIdx.x; t < th * 16; t += blockDim.x * blockDim.y) {
-      const int r = t / 16, cc = t % 16;
-      const uint8_t* row = s_tile + r * tw + cc;
-      uint32_t acc = 0;
-      for (int i = 0; i <= 2 * radius; i++) {
-        const uint32_t v = row[i];
-        acc += (v & 1u) | (((v >> 1) & 1u) << 10) | ((v >> 2) << 20);
-      }
-      s_hsum[r][cc] = acc;
-    }
-    __syncthreads();
-#endif
   }
   PIX2D_FULL();
   const int W = pc.W, H = pc.H;
-  if (pc.P.use_edge) {
-    short2* en = B.edge_neigh + (size_t)center * 8;
-    for (int i = 0; i < 8 && !DPE_EDGE_SCAN; i++) {   // DPE_EDGE_SCAN: k_edge_rays writes them
-      // first edge pixel along the ray; loads in batches of 8 (one latency per batch)
-      short2 r = make_short2(-1, -1);
-      const int dx = kDir[i][0], dy = kDir[i][1];
-      // steps until the ray leaves the image
-      const int sx = dx > 0 ? W - 1 - x : (dx < 0 ? x : 1 << 30);
-      const int sy = dy > 0 ? H - 1 - y : (dy < 0 ? y : 1 << 30);
-      const int n = MINo(sx, sy);
-      for (int k0 = 1; k0 <= n; k0 += 8) {
-        uint8_t e[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) e[k] = (k0 + k <= n) ? B.edge[(x + (k0 + k) * dx) + (y + (k0 + k) * dy) * W] : 0;
-        int hit = -1;
-#pragma unroll
-        for (int k = 7; k >= 0; --k) if (e[k]) hit = k;
-        if (hit >= 0) { r = make_short2((short)(x + (k0 + hit) * dx), (short)(y + (k0 + hit) * dy)); break; }
-      }
-      en[i] = r;
-    }
+  if (pc.P.use_edge) {   // the 8 edge rays come from k_edge_rays
     int edge_pix = 0, tot_pix = 0, bound_pix = 0;
-#if DPE_EI_SEP
-    if (tiled) {
-      uint32_t acc = 0;
-      for (int j = 0; j <= 2 * radius; j++) acc += s_hsum[threadIdx.y + j][threadIdx.x];
-      edge_pix = (int)(acc & 1023u); bound_pix = (int)((acc >> 10) & 1023u); tot_pix = (int)(acc >> 20);
-    } else
-#endif
     if (tiled) {
       const int tw = blockDim.x + 2 * radius;
       for (int j = 0; j <= 2 * radius; j++) {
@@ -220,20 +169,12 @@ __global__ void __launch_bounds__(256) k_gen_edge_inform(const PassConst* __rest
 }
 
 // ------------------------------------------------------------------------------ GenNeighbours
-// One thread per WEAK pixel of `list` (the reference's full-grid launch with most threads idle).
-#ifndef DPE_GN_WAVES
-#define DPE_GN_WAVES 1
-#endif
-#ifndef DPE_GN_SPEC
-#define DPE_GN_SPEC 4
-#endif
-__global__ void __launch_bounds__(256, DPE_GN_WAVES) k_gen_neighbours(const PassConst* __restrict__ pcp, DevBufs B,
-                                                        const int* __restrict__ list, const int* __restrict__ nlist_p) {   // DPE.cu:2103-2463
-  const PassConst& pc = *pcp;
-  const int gi = xcd_remap(blockIdx.x, gridDim.x, B.xcd_rows * 16) * blockDim.x + threadIdx.x;
-  if (gi >= *nlist_p) return;
+// One WEAK pixel of GenNeighbours with per-thread arrays (2.3 KB/lane of scratch): the fallback for
+// the pixels k_gen_neighbours_lds defers (more support points than its LDS slots, or a NaN where its
+// selections need an order), and for rotate_time > 4.
+constexpr int kGnSpec = 4;   // probe attempts drawn and loaded together
+DEV void gen_neighbours_px(const PassConst& pc, const DevBufs& B, int center) {   // DPE.cu:2103-2463
   const int W = pc.W, H = pc.H;
-  const int center = list[gi];
   PHASE_BEGIN();
   const int x = center % W, y = center / W;
   const int min_margin = 6;
@@ -271,19 +212,18 @@ __global__ void __launch_bounds__(256, DPE_GN_WAVES) k_gen_neighbours(const Pass
         for (int radius = 2; radius <= 4096; radius = MINo(radius * 2, radius + 25)) {
           const float tpx = (float)x + od.x * radius, tpy = (float)y + od.y * radius;
           if (tpx < 0 || tpy < 0 || tpx >= W || tpy >= H) break;
-#if DPE_GN_SPEC > 1
-          // DPE_GN_SPEC attempts at a time: their draws, targets and weak[] / nearest[] loads are all
+          // kGnSpec attempts at a time: their draws, targets and weak[] / nearest[] loads are all
           // issued first, then the attempts are tested in order; the stream is put back to just
           // after the attempt that succeeded, so the draws consumed are the serial loop's.
           bool found = false;
-          for (int radius_iter = 0; radius_iter < 4 && !found; radius_iter += DPE_GN_SPEC) {
-            short2 cand[DPE_GN_SPEC], nnv[DPE_GN_SPEC];
-            uint8_t wkv[DPE_GN_SPEC];
-            bool inm[DPE_GN_SPEC];
-            uint32_t rb[DPE_GN_SPEC][4], rc[DPE_GN_SPEC];
-            int ri[DPE_GN_SPEC];
+          for (int radius_iter = 0; radius_iter < 4 && !found; radius_iter += kGnSpec) {
+            short2 cand[kGnSpec], nnv[kGnSpec];
+            uint8_t wkv[kGnSpec];
+            bool inm[kGnSpec];
+            uint32_t rb[kGnSpec][4], rc[kGnSpec];
+            int ri[kGnSpec];
 #pragma unroll
-            for (int q = 0; q < DPE_GN_SPEC; ++q) {
+            for (int q = 0; q < kGnSpec; ++q) {
               const uint32_t r1 = rng_u32(rs); const uint32_t r2 = rng_u32(rs);
               const int rxs = (int)(((r1 % 2 == 0) ? 1u : 0xFFFFFFFFu) * r2 % (uint32_t)shift_range);
               const uint32_t r3 = rng_u32(rs); const uint32_t r4 = rng_u32(rs);
@@ -299,7 +239,7 @@ __global__ void __launch_bounds__(256, DPE_GN_WAVES) k_gen_neighbours(const Pass
               cand[q] = np;
             }
 #pragma unroll
-            for (int q = 0; q < DPE_GN_SPEC; ++q) {
+            for (int q = 0; q < kGnSpec; ++q) {
               if (found || !inm[q]) continue;
               short2 np = cand[q];
               if (wkv[q] != DPE_STRONG) {
@@ -318,35 +258,6 @@ __global__ void __launch_bounds__(256, DPE_GN_WAVES) k_gen_neighbours(const Pass
               }
             }
           }
-#else
-          for (int radius_iter = 0; radius_iter < 4; ++radius_iter) {
-            const uint32_t r1 = rng_u32(rs); const uint32_t r2 = rng_u32(rs);
-            const int rxs = (int)(((r1 % 2 == 0) ? 1u : 0xFFFFFFFFu) * r2 % (uint32_t)shift_range);
-            const uint32_t r3 = rng_u32(rs); const uint32_t r4 = rng_u32(rs);
-            const int rys = (int)(((r3 % 2 == 0) ? 1u : 0xFFFFFFFFu) * r4 % (uint32_t)shift_range);
-            float2 dir = make_float2(od.x * 20 + (float)rxs, od.y * 20 + (float)rys);
-            normalize2(dir);
-            short2 np = make_short2((short)f2i((float)x + dir.x * radius), (short)f2i((float)y + dir.y * radius));
-            if (np.x < min_margin || np.y < min_margin || np.x >= W - min_margin || np.y >= H - min_margin) continue;
-            int npc = np.x + np.y * W;
-            const uint8_t wk = B.weak[npc];
-            const short2 nn = B.nearest[npc];        // issued with weak[]: one latency, not two
-            if (wk != DPE_STRONG) {
-              np = nn;
-              if (np.x == -1 || np.y == -1) continue;
-              npc = np.x + np.y * W;
-            }
-            float2 td = make_float2((float)(np.x - x), (float)(np.y - y));
-            normalize2(td);
-            const float ca = td.x * od.x + td.y * od.y;
-            if (ca > threshhold && (!edge_limit || !bresenham(pc, B, x, y, np.x, np.y))) {
-              strong_points[dir_index] = np;
-              dir_valid |= (1ull << dir_index);
-              strong_point_size++;
-              break;
-            }
-          }
-#endif
           if ((dir_valid >> dir_index) & 1ull) break;
         }
         float2 rd = make_float2(od.x * cos_angle - od.y * sin_angle, od.x * sin_angle + od.y * cos_angle);
@@ -555,6 +466,17 @@ __global__ void __launch_bounds__(256, DPE_GN_WAVES) k_gen_neighbours(const Pass
   PHASE(4);
   PHASE_END_ALL(2);
 }
+// over `list`: a small persistent grid (kGnOvfBlocks x 256 threads) striding through the list, so
+// that the usual empty overflow list costs one short launch (the round-4 full-grid launch took the
+// aux stream for 0.7 ms)
+constexpr int kGnOvfBlocks = 64;
+__global__ void __launch_bounds__(256) k_gen_neighbours(const PassConst* __restrict__ pcp, DevBufs B,
+                                                        const int* __restrict__ list, const int* __restrict__ nlist_p) {
+  const PassConst& pc = *pcp;
+  const int n = *nlist_p;
+  for (int gi = blockIdx.x * blockDim.x + threadIdx.x; gi < n; gi += gridDim.x * blockDim.x)
+    gen_neighbours_px(pc, B, list[gi]);
+}
 
 // ------------------------------------------------------------------------------ GenNeighbours, scratch-free
 // The same GenNeighbours with no per-thread arrays (k_gen_neighbours keeps 2.3 KB/lane of them in
@@ -572,211 +494,24 @@ __global__ void __launch_bounds__(256, DPE_GN_WAVES) k_gen_neighbours(const Pass
 // or weight is NaN.  A pixel with more than K support points, or a NaN where a sort needs the
 // order, writes nothing and is appended to `ovf` for k_gen_neighbours (its Philox stream is
 // addressed by the pixel, so the rerun draws the same numbers).  96 VGPRs, 5 waves per SIMD.
-#ifndef DPE_GN_BT
-#define DPE_GN_BT 64
-#endif
-#ifndef DPE_GN_DP
-#define DPE_GN_DP 0      // 1: support-point depths in LDS too (0: re-read from planes0, half the LDS)
-#endif
-#ifndef DPE_GN_SHORT
-#define DPE_GN_SHORT 0   // 1: one-round-trip Bresenham walks for max_step <= 16 (more registers, slower)
-#endif
-// 8x8 bit tiles of the low-res edge map (bresenham with DPE_BRES_TILE): one thread per tile
-__global__ void k_edge_tiles(const uint8_t* __restrict__ e, int w, int h, uint64_t* __restrict__ tiles) {
-  const int tw = (w + 7) / 8, th = (h + 7) / 8;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= tw * th) return;
-  uint64_t m;
-  bres::build_tile(e, w, h, i, m);
-  tiles[i] = m;
-}
+constexpr int kGnBT = 64;   // threads per workgroup
 // table of the normalised image coordinates: gtab[x] = (x - K[2]) / K[0], gtab[W + y] = (y - K[5]) / K[4]
-// + the direction walks' unit vectors (DPE.cu:2166-2190), pixel-independent: od of origin direction oi
-// after ri rotations at gtab[W + H + 2 (oi * 4 + ri)], and the attempt direction
-// normalize(20 od + (a, b)) for the shift residues a, b < gn_shift at
-// gtab[W + H + 64 + 2 (((oi * 4 + ri) * 8 + a) * 8 + b)]: the same operations as the per-attempt code
-constexpr int kGnDirOfs = 64, kGnTabExtra = 64 + 2 * 32 * 64;
 __global__ void k_gn_tables(const PassConst* __restrict__ pcp, float* __restrict__ gtab) {
   const PassConst& pc = *pcp;
   const DpeCamera& camera = pc.cams[0];
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < pc.W) gtab[i] = ((float)i - camera.K[2]) / camera.K[0];
   else if (i < pc.W + pc.H) gtab[i] = ((float)(i - pc.W) - camera.K[5]) / camera.K[4];
-  else if (i < pc.W + pc.H + 8 && pc.P.rotate_time <= 4) {
-    const int oi = i - pc.W - pc.H;
-    float* t = gtab + pc.W + pc.H;
-    const int k = oi < 4 ? oi : oi + 1;          // odx -1..1 outer, ody -1..1 inner, (0, 0) skipped
-    float2 od = make_float2((float)(k / 3 - 1), (float)(k % 3 - 1));
-    normalize2(od);
-    for (int ri = 0; ri < pc.P.rotate_time; ++ri) {
-      if (ri > 0) {
-        float2 rd = make_float2(od.x * pc.gn_cos - od.y * pc.gn_sin, od.x * pc.gn_sin + od.y * pc.gn_cos);
-        normalize2(rd);
-        od = rd;
-      }
-      t[2 * (oi * 4 + ri)] = od.x; t[2 * (oi * 4 + ri) + 1] = od.y;
-      for (int a = 0; a < pc.gn_shift && a < 8; ++a)
-        for (int b = 0; b < pc.gn_shift && b < 8; ++b) {
-          float2 dir = make_float2(od.x * 20 + (float)a, od.y * 20 + (float)b);
-          normalize2(dir);
-          float* d = t + kGnDirOfs + 2 * (((oi * 4 + ri) * 8 + a) * 8 + b);
-          d[0] = dir.x; d[1] = dir.y;
-        }
-    }
-  }
 }
-// x % gn_shift (DPE.cu:2182's `% shift`) as a multiply by the per-pass constant gn_shift_m
-DEV uint32_t gn_mod(const PassConst& pc, uint32_t x) {
-  const uint32_t d = (uint32_t)pc.gn_shift;
-  const uint32_t r = x - __umulhi(x, pc.gn_shift_m) * d;
-  return r >= d ? r - d : r;
-}
-// the angle test of a probe, td = normalize(np - p), td . od > thr (DPE.cu:2196-2199): decided from
-// an approximate reciprocal square root unless the approximate dot product lies within 1e-5 of thr
-// (its error is below 1e-6: |td|, |od| <= 1, v_rsq_f32 within 1 ulp), else from the exact one
+// the angle test of a probe, td = normalize(np - p), td . od > thr (DPE.cu:2196-2199)
 DEV bool gn_angle_ok(float dxf, float dyf, float2 od, float thr) {
-#if DPE_GN_FASTANGLE
-  const float n2 = dxf * dxf + dyf * dyf;
-  const float ia = __builtin_amdgcn_rsqf(n2);
-  const float caa = (dxf * ia) * od.x + (dyf * ia) * od.y;
-  if (__builtin_fabsf(caa - thr) > 1e-5f) return caa > thr;
-#endif
   float2 td = make_float2(dxf, dyf);
   normalize2(td);
   return td.x * od.x + td.y * od.y > thr;
 }
-// BresenhamLine for walks of at most 16 steps per direction (high-resolution images: max_step =
-// round(max(LH, LW) / 60)): all positions of both directions generated first and their low-res edge
-// bytes loaded together, one memory round trip; the result is the OR over the visited positions.
-DEV bool bresenham_short(const PassConst& pc, const DevBufs& B, int Ax, int Ay, int Bx, int By, int max_step) {
-  const int W = pc.W;
-  const uint8_t ea = B.edge[Ax + Ay * W], eb = B.edge[Bx + By * W];
-  const float scale_x = 1.0f * pc.LW / (float)pc.W;
-  const float scale_y = 1.0f * pc.LH / (float)pc.H;
-  const int height = pc.LH, width = pc.LW;
-  int idx[2][16];
-#pragma unroll
-  for (int pass = 0; pass < 2; ++pass) {
-    const int fx = pass == 0 ? Bx : Ax, fy = pass == 0 ? By : Ay;
-    const int tx = pass == 0 ? Ax : Bx, ty = pass == 0 ? Ay : By;
-    int x0 = (int)MINo(__builtin_roundf(fx * scale_x), (float)(width - 1));
-    int y0 = (int)MINo(__builtin_roundf(fy * scale_y), (float)(height - 1));
-    const int x1 = (int)MINo(__builtin_roundf(tx * scale_x), (float)(width - 1));
-    const int y1 = (int)MINo(__builtin_roundf(ty * scale_y), (float)(height - 1));
-    const int dx = abs(x1 - x0), sx = x0 < x1 ? 1 : -1;
-    const int dy = abs(y1 - y0), sy = y0 < y1 ? 1 : -1;
-    int erro = (dx > dy ? dx : dy) / 2;
-    bool tagx = true, tagy = true;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      idx[pass][k] = -1;                                  // low_edge_at(-1) == 0
-      if (k < MAXo(max_step, 1) && (tagx || tagy)) {     // the first step is taken before the limit test
-        if (x0 == x1) tagx = false;
-        if (y0 == y1) tagy = false;
-        const int e2 = erro;
-        if (e2 > -dx) { erro -= dy; x0 += sx; }
-        if (e2 < dy) { erro += dx; y0 += sy; }
-        idx[pass][k] = x0 + y0 * width;
-      }
-    }
-  }
-  uint8_t hit = 0;
-#pragma unroll
-  for (int pass = 0; pass < 2; ++pass)
-#pragma unroll
-    for (int k = 0; k < 16; ++k) hit |= low_edge_at(pc, B, idx[pass][k]);
-  return !(ea || eb) && hit != 0;
-}
-
-#ifndef DPE_GN_ECACHE
-#define DPE_GN_ECACHE 0   // 1: the edge-test cache in HBM (slower: DESIGN.md §8)
-#endif
-#ifndef DPE_GN_PRECHECK
-#define DPE_GN_PRECHECK 0   // 1: skip the draws of radii none of whose possible targets can pass (slower)
-#endif
-#ifndef DPE_GNL_SPEC
-#define DPE_GNL_SPEC 4   // probe attempts drawn and loaded together (1, 2 or 4)
-#endif
-#ifndef DPE_GN_MINW
-#define DPE_GN_MINW 1
-#endif
-// Per-pixel durations of the scratch-free GenNeighbours (build with -DDPE_GN_TIMES=1;
-// tools/gn_times.py): shader clocks from the start to the end of the probes and to the pixel's end,
-// at the pixel's list index (one wave = 64 consecutive indices).  Off in the product.
-// GenNeighbours' probe walks shared by the wave (DPE_GN_COOP): every lane of the wave calls this
-// with the same control flow; the lanes with `want` set each get BresenhamLine(A, B) (bresenham()'s
-// result).  With at most DPE_GN_COOP_MAX lines pending, each line is walked by all active lanes
-// together, consecutive steps from the closed form (bres::walk_pos), one byte load each per round
-// and a ballot; with more, every lane walks its own line.
-#ifndef DPE_GN_COOP
-#define DPE_GN_COOP 0
-#endif
-// The probe's walk pair in the other order: BresenhamLine(A, B) is "an edge on the walk B -> A or
-// on the walk A -> B", whichever is walked first; with the pixel as B the first walk starts at the
-// pixel, where the edge that blocks a direction usually is, and stops there
-// RANSACToGetFitPlane's three edge walks of a try stopped at the first that crosses an edge
-#ifndef DPE_GN_RSC
-#define DPE_GN_RSC 0
-#endif
-#ifndef DPE_GN_PIXFIRST
-#define DPE_GN_PIXFIRST 1
-#endif
-#ifndef DPE_GN_COOP_MAX
-#define DPE_GN_COOP_MAX 8
-#endif
-DEV bool crosses_coop(const PassConst& pc, const DevBufs& B, bool want, int ax, int ay, int bx, int by, int max_step) {
-  const uint64_t act = __ballot(1);
-  uint64_t todo = __ballot(want);
-  if (todo == 0) return false;
-  if (__popcll(todo) > DPE_GN_COOP_MAX) return want ? bresenham(pc, B, ax, ay, bx, by) : false;
-  const int lane = (int)(threadIdx.x & 63);
-  const int rank = __popcll(act & ((1ull << lane) - 1ull)), nact = __popcll(act);
-  const int W = pc.W, width = pc.LW, height = pc.LH;
-  const float scale_x = 1.0f * pc.LW / (float)pc.W;
-  const float scale_y = 1.0f * pc.LH / (float)pc.H;
-  bool res = false;
-  while (todo) {
-    const int L = __builtin_ctzll(todo);
-    todo &= todo - 1;
-    const int Ax = __shfl(ax, L), Ay = __shfl(ay, L), Bx = __shfl(bx, L), By = __shfl(by, L);
-    bool hit = false;
-    if (!(B.edge[Ax + Ay * W] || B.edge[Bx + By * W])) {
-      for (int pass = 0; pass < 2 && !hit; ++pass) {
-        const int fx = pass == 0 ? Bx : Ax, fy = pass == 0 ? By : Ay;
-        const int tx = pass == 0 ? Ax : Bx, ty = pass == 0 ? Ay : By;
-        const int x0 = (int)MINo(__builtin_roundf(fx * scale_x), (float)(width - 1));
-        const int y0 = (int)MINo(__builtin_roundf(fy * scale_y), (float)(height - 1));
-        const int x1 = (int)MINo(__builtin_roundf(tx * scale_x), (float)(width - 1));
-        const int y1 = (int)MINo(__builtin_roundf(ty * scale_y), (float)(height - 1));
-        const bres::Walk w = bres::start(x0, y0, x1, y1, max_step);
-        const int K = bres::walk_steps(w);
-        for (int k0 = 0; k0 < K && !hit; k0 += nact) {
-          const int k = k0 + rank + 1;
-          uint8_t v = 0;
-          if (k <= K) {
-            int px, py;
-            bres::walk_pos(w, k, px, py);
-            const int idx = px + py * width;
-            if (idx >= 0 && idx < width * height) v = B.edge_low[idx];
-          }
-          hit = __ballot(v != 0) != 0;
-        }
-      }
-    }
-    if (lane == L) res = hit;
-  }
-  return res;
-}
-#ifndef DPE_GN_TIMES
-#define DPE_GN_TIMES 0
-#endif
-// direction walks from the per-pass tables and a fast angle test (k_gn_tables, gn_angle_ok, gn_mod)
-#ifndef DPE_GN_DIRTAB
-#define DPE_GN_DIRTAB 0
-#endif
-#ifndef DPE_GN_FASTANGLE
-#define DPE_GN_FASTANGLE 0
-#endif
+// Per-pixel durations of the scratch-free GenNeighbours (DPE_DIAG & 8; tools/gn_times.py): shader
+// clocks from the start to the end of the probes and to the pixel's end, at the pixel's list index
+// (one wave = 64 consecutive indices).  Off in the product.
 #if DPE_GN_TIMES
 // + per-pixel counts: [0] radius steps of the direction walks, [1] Bresenham walks of the probes,
 // [2] RANSAC tries, [3] Bresenham walks of the RANSAC, [4] / [5] shader clocks in the probes' / the
@@ -794,19 +529,18 @@ static __device__ uint32_t g_gncnt[6 << 20];
 #define GN_C(k, n) do {} while (0)
 #define GN_CLK() 0ull
 #endif
+// The probe's walk pair runs from the pixel: BresenhamLine(A, B) is "an edge on the walk B -> A or
+// on the walk A -> B", whichever is walked first; with the pixel as B the first walk starts at the
+// pixel, where the edge that blocks a direction usually is, and stops there (round 4).
 template <int K>
-__global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(const PassConst* __restrict__ pcp, DevBufs B,
-                                                                  const int* __restrict__ list, const int* __restrict__ nlist_p,
-                                                                  const float* __restrict__ gtab, int* __restrict__ ovf,
-                                                                  int* __restrict__ novf, uint8_t* __restrict__ ecache,
-                                                                  long estride) {   // DPE.cu:2103-2463
-  __shared__ uint32_t s_pt[K][DPE_GN_BT];       // support point (x | y << 16)
-#if DPE_GN_DP
-  __shared__ float s_dp[K][DPE_GN_BT];          // its depth, then (after the RANSAC) its weight
-#endif
+__global__ void __launch_bounds__(kGnBT) k_gen_neighbours_lds(const PassConst* __restrict__ pcp, DevBufs B,
+                                                              const int* __restrict__ list, const int* __restrict__ nlist_p,
+                                                              const float* __restrict__ gtab, int* __restrict__ ovf,
+                                                              int* __restrict__ novf) {   // DPE.cu:2103-2463
+  __shared__ uint32_t s_pt[K][kGnBT];           // support point (x | y << 16)
   const PassConst& pc = *pcp;
   const int t = threadIdx.x;
-  const int gi = xcd_remap(blockIdx.x, gridDim.x, B.xcd_rows * 64) * DPE_GN_BT + t;
+  const int gi = xcd_remap(blockIdx.x, gridDim.x, B.xcd_rows * 64) * kGnBT + t;
   if (gi >= *nlist_p) return;
   const int W = pc.W, H = pc.H;
   const int center = list[gi];
@@ -832,10 +566,7 @@ __global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(c
   const float cos_angle = pc.gn_cos, sin_angle = pc.gn_sin, threshhold = pc.gn_thr;
   const int shift_range = pc.gn_shift;
   const float ransac_threshold = pc.P.ransac_threshold * depth_diff;
-  const int max_step = pc.P.high_res_img ? (int)__builtin_round(MAXo(pc.LH, pc.LW) / 60.0) : MAXo(pc.LH, pc.LW);
-  auto crosses = [&](int ax, int ay, int bx, int by) -> bool {
-    return (DPE_GN_SHORT && max_step <= 16) ? bresenham_short(pc, B, ax, ay, bx, by, max_step) : bresenham(pc, B, ax, ay, bx, by);
-  };
+  auto crosses = [&](int ax, int ay, int bx, int by) -> bool { return bresenham(pc, B, ax, ay, bx, by); };
   bool edge_limit = false;
   float complex_new = -1.0f;                       // complex_[center] to write once the pixel is done
   if (pc.P.use_limit) {
@@ -851,7 +582,7 @@ __global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(c
   // found, radius past the image or 4096) moves on to its next direction at once, so a wave's time
   // is its slowest lane's total walk, not the sum over directions of each direction's slowest walk.
   // Each lane's sequence of probes (and of Philox draws) is the nested loops' sequence.  One radius
-  // of a walk is DPE_GNL_SPEC attempts at a time: their draws, targets and weak[] / nearest[] loads
+  // of a walk is kGnSpec attempts at a time: their draws, targets and weak[] / nearest[] loads
   // issued first, then tested in order; the stream is then positioned just after the attempt that
   // succeeded (each attempt draws 4 words; the stream is position-addressable).
   {
@@ -861,82 +592,6 @@ __global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(c
       normalize2(od);
       return od;
     };
-#if DPE_GN_COOP
-    // the same walks with the loop kept wave-uniform (a lane whose 8 x rotate_time walks are done
-    // idles through it), so the probes' Bresenham walks can be shared: a wave with few walks pending
-    // walks each line with all its lanes (crosses_coop), 64 steps per load round
-    static_assert(DPE_GNL_SPEC == 4, "one attempt batch per radius");
-    int oi = 0, ri = 0, radius = 2;
-    float2 od = origin_od(0);
-    while (__any(oi < 8)) {
-      const bool alive = oi < 8;
-      bool next = alive && radius > 4096;
-      if (alive) GN_C(0, 1);
-      if (alive && !next) {
-        const float tpx = (float)x + od.x * radius, tpy = (float)y + od.y * radius;
-        if (tpx < 0 || tpy < 0 || tpx >= W || tpy >= H) next = true;
-      }
-      const bool probe = alive && !next;
-      bool dir_found = false;
-      short2 cand[4], nnv[4];
-      uint8_t wkv[4];
-      bool inm[4];
-      uint32_t pos0 = 0;
-      if (probe) {
-        pos0 = rs.idx == 4 ? rs.ctr * 4u : (rs.ctr - 1u) * 4u + (uint32_t)rs.idx;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const uint32_t r1 = rng_u32(rs); const uint32_t r2 = rng_u32(rs);
-          const uint32_t r3 = rng_u32(rs); const uint32_t r4 = rng_u32(rs);
-          const int rxs = (int)(((r1 % 2 == 0) ? 1u : 0xFFFFFFFFu) * r2 % (uint32_t)shift_range);
-          const int rys = (int)(((r3 % 2 == 0) ? 1u : 0xFFFFFFFFu) * r4 % (uint32_t)shift_range);
-          float2 dir = make_float2(od.x * 20 + (float)rxs, od.y * 20 + (float)rys);
-          normalize2(dir);
-          const short2 np = make_short2((short)f2i((float)x + dir.x * radius), (short)f2i((float)y + dir.y * radius));
-          inm[q] = !(np.x < min_margin || np.y < min_margin || np.x >= W - min_margin || np.y >= H - min_margin);
-          const int npc = inm[q] ? np.x + np.y * W : center;
-          wkv[q] = B.weak[npc];
-          nnv[q] = B.nearest[npc];
-          cand[q] = np;
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        bool want = false;
-        short2 np = make_short2(0, 0);
-        if (probe && !dir_found && inm[q]) {
-          np = cand[q];
-          if (wkv[q] != DPE_STRONG) np = nnv[q];
-          if (!(np.x == -1 || np.y == -1)) want = gn_angle_ok((float)(np.x - x), (float)(np.y - y), od, threshhold);
-        }
-        if (want && edge_limit) GN_C(1, 1);
-        const uint64_t gn_b0_ = GN_CLK(); (void)gn_b0_;
-        const bool cr = DPE_GN_PIXFIRST ? crosses_coop(pc, B, want && edge_limit, np.x, np.y, x, y, max_step)
-                                        : crosses_coop(pc, B, want && edge_limit, x, y, np.x, np.y, max_step);
-        if (want && edge_limit) GN_C(4, (uint32_t)(GN_CLK() - gn_b0_));
-        if (want && (!edge_limit || !cr)) {
-          push(np);
-          dir_found = true;
-          rng_seek(rs, pos0 + 4u * (uint32_t)(q + 1));
-        }
-      }
-      if (probe) {
-        if (dir_found) next = true;
-        else radius = MINo(radius * 2, radius + 25);
-      }
-      if (alive && next) {
-        radius = 2;
-        if (++ri < rotate_time) {
-          float2 rd = make_float2(od.x * cos_angle - od.y * sin_angle, od.x * sin_angle + od.y * cos_angle);
-          normalize2(rd);
-          od = rd;
-        } else {
-          ri = 0;
-          if (++oi < 8) od = origin_od(oi);
-        }
-      }
-    }
-#else
     int oi = 0, ri = 0, radius = 2;
     float2 od = origin_od(0);
     while (oi < 8) {
@@ -946,70 +601,21 @@ __global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(c
         const float tpx = (float)x + od.x * radius, tpy = (float)y + od.y * radius;
         if (tpx < 0 || tpy < 0 || tpx >= W || tpy >= H) next = true;
       }
-#if DPE_GN_PRECHECK
-      // An attempt's shifts (rxs, rys) are residues mod shift_range, so at most shift_range^2 targets
-      // are possible at this radius.  When none of them can pass the tests that come before the
-      // Bresenham walk (margin, a STRONG pixel or its nearest STRONG point, the angle), all 4
-      // attempts fail whatever is drawn: the stream skips their 16 words without drawing them.
-      // (Tried for shift_range <= 3, i.e. rotate_time >= 2; 74 % of the reference's attempts fail
-      // on the angle, 2 % succeed.)
-      if (!next && shift_range <= 3) {
-        bool can[9];
-#pragma unroll
-        for (int k = 0; k < 9; ++k) {
-          const int a = k / 3, b = k % 3;
-          can[k] = false;
-          if (a < shift_range && b < shift_range) {
-            float2 dir = make_float2(od.x * 20 + (float)a, od.y * 20 + (float)b);
-            normalize2(dir);
-            short2 np = make_short2((short)f2i((float)x + dir.x * radius), (short)f2i((float)y + dir.y * radius));
-            const bool in = !(np.x < min_margin || np.y < min_margin || np.x >= W - min_margin || np.y >= H - min_margin);
-            const int npc = in ? np.x + np.y * W : center;
-            const uint8_t wk = B.weak[npc];
-            const short2 nn = B.nearest[npc];
-            if (in) {
-              if (wk != DPE_STRONG) np = nn;
-              if (np.x != -1 && np.y != -1) {
-                float2 td = make_float2((float)(np.x - x), (float)(np.y - y));
-                normalize2(td);
-                can[k] = td.x * od.x + td.y * od.y > threshhold;
-              }
-            }
-          }
-        }
-        bool any = false;
-#pragma unroll
-        for (int k = 0; k < 9; ++k) any = any || can[k];
-        if (!any) {
-          const uint32_t pos = rs.idx == 4 ? rs.ctr * 4u : (rs.ctr - 1u) * 4u + (uint32_t)rs.idx;
-          rng_seek(rs, pos + 16u);
-          radius = MINo(radius * 2, radius + 25);
-          continue;
-        }
-      }
-#endif
       if (!next) {
         bool dir_found = false;
-        for (int ra = 0; ra < 4 && !dir_found; ra += DPE_GNL_SPEC) {
-          short2 cand[DPE_GNL_SPEC], nnv[DPE_GNL_SPEC];
-          uint8_t wkv[DPE_GNL_SPEC];
-          bool inm[DPE_GNL_SPEC];
+        for (int ra = 0; ra < 4 && !dir_found; ra += kGnSpec) {
+          short2 cand[kGnSpec], nnv[kGnSpec];
+          uint8_t wkv[kGnSpec];
+          bool inm[kGnSpec];
           const uint32_t pos0 = rs.idx == 4 ? rs.ctr * 4u : (rs.ctr - 1u) * 4u + (uint32_t)rs.idx;
 #pragma unroll
-          for (int q = 0; q < DPE_GNL_SPEC; ++q) {
+          for (int q = 0; q < kGnSpec; ++q) {
             const uint32_t r1 = rng_u32(rs); const uint32_t r2 = rng_u32(rs);
             const uint32_t r3 = rng_u32(rs); const uint32_t r4 = rng_u32(rs);
-            float2 dir;
-            if (DPE_GN_DIRTAB && shift_range <= 8) {   // the table holds residues < 8 only
-              const uint32_t rxs = gn_mod(pc, ((r1 % 2 == 0) ? 1u : 0xFFFFFFFFu) * r2);
-              const uint32_t rys = gn_mod(pc, ((r3 % 2 == 0) ? 1u : 0xFFFFFFFFu) * r4);
-              dir = ((const float2*)(gtab + W + H + kGnDirOfs))[((oi * 4 + ri) * 8 + rxs) * 8 + rys];
-            } else {
-              const int rxs = (int)(((r1 % 2 == 0) ? 1u : 0xFFFFFFFFu) * r2 % (uint32_t)shift_range);
-              const int rys = (int)(((r3 % 2 == 0) ? 1u : 0xFFFFFFFFu) * r4 % (uint32_t)shift_range);
-              dir = make_float2(od.x * 20 + (float)rxs, od.y * 20 + (float)rys);
-              normalize2(dir);
-            }
+            const int rxs = (int)(((r1 % 2 == 0) ? 1u : 0xFFFFFFFFu) * r2 % (uint32_t)shift_range);
+            const int rys = (int)(((r3 % 2 == 0) ? 1u : 0xFFFFFFFFu) * r4 % (uint32_t)shift_range);
+            float2 dir = make_float2(od.x * 20 + (float)rxs, od.y * 20 + (float)rys);
+            normalize2(dir);
             const short2 np = make_short2((short)f2i((float)x + dir.x * radius), (short)f2i((float)y + dir.y * radius));
             inm[q] = !(np.x < min_margin || np.y < min_margin || np.x >= W - min_margin || np.y >= H - min_margin);
             const int npc = inm[q] ? np.x + np.y * W : center;
@@ -1018,7 +624,7 @@ __global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(c
             cand[q] = np;
           }
 #pragma unroll
-          for (int q = 0; q < DPE_GNL_SPEC; ++q) {
+          for (int q = 0; q < kGnSpec; ++q) {
             if (dir_found || !inm[q]) continue;
             short2 np = cand[q];
             if (wkv[q] != DPE_STRONG) {
@@ -1028,7 +634,7 @@ __global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(c
             const bool ang = gn_angle_ok((float)(np.x - x), (float)(np.y - y), od, threshhold);
             if (ang && edge_limit) GN_C(1, 1);
             const uint64_t gn_b0_ = GN_CLK(); (void)gn_b0_;
-            const bool pass_ = ang && (!edge_limit || !(DPE_GN_PIXFIRST ? crosses(np.x, np.y, x, y) : crosses(x, y, np.x, np.y)));
+            const bool pass_ = ang && (!edge_limit || !crosses(np.x, np.y, x, y));
             GN_C(4, (uint32_t)(GN_CLK() - gn_b0_));
             if (pass_) {
               push(np);
@@ -1052,7 +658,6 @@ __global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(c
         }
       }
     }
-#endif
   }
   PHASE(0);
   if (pc.P.use_label && B.label[center] > 0) {
@@ -1097,12 +702,7 @@ __global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(c
   if (valid_count <= 3) { finish_fail(); return; }
   // depths of the support points (the reference's spv3[].z); the 3-D points and normals of the
   // drawn triples are recomputed from (pixel, depth) / planes0[] with the reference's expressions
-#if DPE_GN_DP
-  for (int i = 0; i < valid_count; ++i) { const short2 sp = pt_at(i); s_dp[i][t] = B.planes0[sp.x + sp.y * W].w; }
-  auto depth_at = [&](int i) -> float { return s_dp[i][t]; };
-#else
   auto depth_at = [&](int i) -> float { const uint32_t v = s_pt[i][t]; return B.planes0[(v & 0xFFFFu) + (v >> 16) * W].w; };
-#endif
   float X[3];
   get3d(camera, x, y, B.planes0[center].w, X);
   const float cpz = X[2];
@@ -1132,35 +732,12 @@ __global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(c
       if (must_in_triangle && !point_in_triangle(pa, pb, pcc, x, y)) continue;
       if (edge_limit) {
         bool eab, ebc, eca;
-        if (DPE_GN_ECACHE && K <= 32 && ecache != nullptr) {
-          // the reference's edge_test[a][b] cache (DPE.cu:2307-2331) in HBM, one byte per point pair
-          // ([pair][thread], zeroed per pass: 0 untested, 1 no edge, 2 edge); BresenhamLine is
-          // symmetric in its end points (both directions are walked), so a pair has one entry
-          auto slot = [&](int u, int v) -> uint8_t* {
-            const int lo = MINo(u, v), hi = MAXo(u, v);
-            return ecache + (size_t)(hi * (hi - 1) / 2 + lo) * (size_t)estride + gi;
-          };
-          uint8_t* sab = slot(a, b); uint8_t* sbc = slot(b, c); uint8_t* sca = slot(c, a);
-          const uint8_t vab = *sab, vbc = *sbc, vca = *sca;
-          if (vab) eab = vab == 2; else { eab = crosses(pa.x, pa.y, pb.x, pb.y); *sab = eab ? 2 : 1; }
-          if (vbc) ebc = vbc == 2; else { ebc = crosses(pb.x, pb.y, pcc.x, pcc.y); *sbc = ebc ? 2 : 1; }
-          if (vca) eca = vca == 2; else { eca = crosses(pcc.x, pcc.y, pa.x, pa.y); *sca = eca ? 2 : 1; }
-        } else {
-          const uint64_t gn_b1_ = GN_CLK(); (void)gn_b1_;
-#if DPE_GN_RSC
-          // only their OR is used: the later walks are skipped once one crosses an edge
-          eab = crosses(pa.x, pa.y, pb.x, pb.y);
-          ebc = !eab && crosses(pb.x, pb.y, pcc.x, pcc.y);
-          eca = !eab && !ebc && crosses(pcc.x, pcc.y, pa.x, pa.y);
-          GN_C(3, 1 + (eab ? 0 : 1) + (eab || ebc ? 0 : 1));
-#else
-          eab = crosses(pa.x, pa.y, pb.x, pb.y);
-          ebc = crosses(pb.x, pb.y, pcc.x, pcc.y);
-          eca = crosses(pcc.x, pcc.y, pa.x, pa.y);
-          GN_C(3, 3);
-#endif
-          GN_C(5, (uint32_t)(GN_CLK() - gn_b1_));
-        }
+        const uint64_t gn_b1_ = GN_CLK(); (void)gn_b1_;
+        eab = crosses(pa.x, pa.y, pb.x, pb.y);
+        ebc = crosses(pb.x, pb.y, pcc.x, pcc.y);
+        eca = crosses(pcc.x, pcc.y, pa.x, pa.y);
+        GN_C(3, 3);
+        GN_C(5, (uint32_t)(GN_CLK() - gn_b1_));
         if (eab || ebc || eca) continue;
       }
       bool normal_consistency = false;
@@ -1246,21 +823,11 @@ __global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(c
   // first 8 points: the insertion sort is stable, so with no NaN weight the k-th output is the k-th
   // smallest (weight, index) -- outliers carry FLT_MAX and the point (-1, -1)
   bool wnan = false;
-#if DPE_GN_DP
-  for (int i = 0; i < valid_count; ++i) {
-    const float dist = resid_of(best_plane, i);
-    wnan |= dist != dist;
-    s_dp[i][t] = dist >= ransac_threshold ? 3.40282347e+38f : dist;
-    if (dist >= ransac_threshold) s_pt[i][t] = 0xFFFFFFFFu;
-  }
-  auto weight_at = [&](int i) -> float { return s_dp[i][t]; };
-#else
   for (int i = 0; i < valid_count; ++i) { const float dist = resid_of(best_plane, i); wnan |= dist != dist; }
   auto weight_at = [&](int i) -> float {
     const float dist = resid_of(best_plane, i);
     return dist >= ransac_threshold ? 3.40282347e+38f : dist;
   };
-#endif
   if (wnan) { defer(); return; }
   short2 out[DPE_NEIGHBOUR_NUM - 1];
   uint64_t taken = 0;
@@ -1272,11 +839,7 @@ __global__ void __launch_bounds__(DPE_GN_BT, DPE_GN_MINW) k_gen_neighbours_lds(c
       const float w = weight_at(i);
       if (bi < 0 || w < bw) { bi = i; bw = w; }
     }
-#if DPE_GN_DP
-    if (bi >= 0) { taken |= 1ull << bi; out[k] = pt_at(bi); }
-#else
     if (bi >= 0) { taken |= 1ull << bi; out[k] = bw >= ransac_threshold ? make_short2(-1, -1) : pt_at(bi); }
-#endif
     else out[k] = make_short2(-1, -1);
   }
   if (complex_new >= 0.0f) B.complex_[center] = complex_new;
@@ -1305,7 +868,7 @@ __global__ void __launch_bounds__(256) k_random_init(const PassConst* __restrict
   PIX2D_FULL();
   const DpeCamera& c0 = pc.cams[0];
   const int N = pc.N;
-  const bool fast = DPE_FAST_PATCH(pc);
+  const bool fast = FAST_PATCH(pc);
   Patch36 P;
   if (fast) make_patch36(P, pc, B, x, y); else { P.px = x; P.py = y; }
   if (pc.P.state == DPE_FIRST_INIT) {
@@ -1360,27 +923,17 @@ __global__ void __launch_bounds__(256) k_random_init(const PassConst* __restrict
 }
 
 // ------------------------------------------------------------------------------ RANSACToGetFitPlane
-constexpr int kRansacThreads = 128;   // 16 x 8 workgroups: 28 KB of LDS each
-// LISTED: one thread per entry of the WEAK list built before GenNeighbours (1-D workgroups; pixels
-// that NeigbourUpdate made UNKNOWN are skipped by the weak_info test), instead of one thread per
-// pixel of the image with ~80 % of them returning at once
-template <bool LISTED>
+constexpr int kRansacThreads = 128;   // 1-D workgroups: 28 KB of LDS each
+// One thread per entry of a weak list (the sweep's list of one colour), instead of the reference's
+// full-grid launch with ~80 % of the threads returning at once.  Only the colour's own weak update
+// reads a fit plane or radius, so the rows past the red/black grid (half_rows) need none.
 __global__ void __launch_bounds__(kRansacThreads) k_ransac_fit(const PassConst* __restrict__ pcp, DevBufs B, int iter,
                                                                const int* __restrict__ list, const int* __restrict__ nlist_p) {   // DPE.cu:2891-3124
   const PassConst& pc = *pcp;
-  int x, y, center;
-  if constexpr (LISTED) {
-    const int gi = xcd_remap(blockIdx.x, gridDim.x, B.xcd_rows * 16) * kRansacThreads + (int)threadIdx.x;
-    if (gi >= *nlist_p) return;
-    center = list[gi];
-    x = center % pc.W; y = center / pc.W;
-  } else {
-    const int lb_ = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y, B.xcd_rows * gridDim.x);
-    x = (lb_ % gridDim.x) * blockDim.x + threadIdx.x;
-    y = (lb_ / gridDim.x) * blockDim.y + threadIdx.y;
-    if (x >= pc.W || y >= pc.H) return;
-    center = x + y * pc.W;
-  }
+  const int gi = xcd_remap(blockIdx.x, gridDim.x, B.xcd_rows * 16) * kRansacThreads + (int)threadIdx.x;
+  if (gi >= *nlist_p) return;
+  const int center = list[gi];
+  const int x = center % pc.W, y = center / pc.W;
   const int W = pc.W;
   if (B.weak[center] != DPE_WEAK) return;
   Rng rs; rng_init(rs, (uint32_t)center, pc.seed32, STREAM_ITER_BASE + 4 * iter + 1, pc.salt);
@@ -1398,7 +951,7 @@ __global__ void __launch_bounds__(kRansacThreads) k_ransac_fit(const PassConst* 
   // array cannot do without scratch memory
   __shared__ short2 s_sp[8][kRansacThreads];
   __shared__ float3 s_sp3[8][kRansacThreads], s_spn[8][kRansacThreads];
-  const int tid = threadIdx.y * blockDim.x + threadIdx.x;
+  const int tid = threadIdx.x;
   struct Col2 { short2* p; DEV short2& operator[](int i) const { return p[i * kRansacThreads]; } } sp{&s_sp[0][tid]};
   struct Col3 { float3* p; DEV float3& operator[](int i) const { return p[i * kRansacThreads]; } } sp3{&s_sp3[0][tid]}, spn{&s_spn[0][tid]};
   int sc = 0;

@@ -65,7 +65,7 @@ DEV void patch_lds_pre(const float* pw, float& p_inv, float& p_mref, float& p_va
 // base + vofs + (ty * stride + tx) * texel bytes, 32-bit arithmetic).
 // Packed form: (r_src, r_rs) accumulate as one pair; weights are (w, w*grey) pairs in LDS; the two
 // taps of a row pair share each packed op (tap2_at).
-template <int U8, bool IN = false>
+template <int U8>
 DEV void taps36_at(const float* pw, int px, int py, f2v tmax, const uint8_t* base, uint32_t vofs, uint32_t stride,
                    const Homog& H0, float* acc) {
     const Homog H = scale_cols(H0);
@@ -74,15 +74,7 @@ DEV void taps36_at(const float* pw, int px, int py, f2v tmax, const uint8_t* bas
     const f2v* wp = (const f2v*)pw;
     f2v s_sr = f2s(0.0f);
     float s_ss = 0;
-#if DPE_UNROLL_ROWS == 1
 #pragma unroll
-#elif DPE_UNROLL_ROWS == 2
-#pragma unroll 2
-#elif DPE_UNROLL_ROWS == 3
-#pragma unroll 3
-#else
-#pragma unroll 1
-#endif
     for (int a = 0; a < 6; ++a) {
       const float x = (float)(px - 5 + 2 * a);
       const f2v bxy = fma2((f2v){H.h[0], H.h[3]}, f2s(x), (f2v){H.h[2], H.h[5]}) * f2s(kTexUnit);
@@ -91,7 +83,7 @@ DEV void taps36_at(const float* pw, int px, int py, f2v tmax, const uint8_t* bas
       float r_ss = 0;
 #pragma unroll
       for (int b = 0; b < 6; b += 2) {
-        const f2v sp = tap2_at<U8, IN>(base, vadj, stride, tmax, H.h, bxy, bz,
+        const f2v sp = tap2_at<U8>(base, vadj, stride, tmax, H.h, bxy, bz,
                                    (f2v){(float)(py - 5 + 2 * b), (float)(py - 3 + 2 * b)});
         const f2v w0 = wp[a * 6 + b], w1 = wp[a * 6 + b + 1];
         const float ws0 = w0.x * sp.x, ws1 = w1.x * sp.y;   // two plain multiplies: no operand packing
@@ -128,23 +120,20 @@ DEV void lds_taps_row(const float* pw, int px, int py, const PassConst& pc, cons
   }
   s_src += r_src; s_ss += r_ss; s_rs += r_rs;
 }
-#ifndef DPE_SLOW_ROWS
-#define DPE_SLOW_ROWS 0   // 1: every kernel's clamped / exact-reciprocal tap loop (rare) one patch row at a time
-#endif
 // Old NCC with the patch read from LDS (same arithmetic as ncc_old_patch36).  ROW1: the slow loop
 // (!FAST: a patch whose reciprocal range check failed) unrolled one row at a time, which lowers the
 // caller's register peak (same operations, same order)
-template <int U8, bool FAST, bool IN = false, bool ROW1 = false>
+template <int U8, bool FAST, bool ROW1 = false>
 DEV void lds_taps(const float* pw, int px, int py, const PassConst& pc, const DevBufs& B, int v, const Homog& H0,
                   float* acc) {
   const int W = pc.W, Hh = pc.H;
-  if constexpr (U8 != TEX_F32 && FAST && DPE_PACKED_TAP) {
-    taps36_at<U8, IN>(pw, px, py, tex_tmax2(W, Hh), tex_base<U8>(B), (uint32_t)v * tex_view<U8>(B),
+  if constexpr (U8 != TEX_F32 && FAST) {
+    taps36_at<U8>(pw, px, py, tex_tmax2(W, Hh), tex_base<U8>(B), (uint32_t)v * tex_view<U8>(B),
                       tex_stride<U8>(W), H0, acc);
   } else {
     const Homog H = scale_cols(H0);
     float s_src = 0, s_ss = 0, s_rs = 0;
-    if constexpr (ROW1 || DPE_SLOW_ROWS) {
+    if constexpr (ROW1) {
 #pragma unroll 1
       for (int a = 0; a < 6; ++a) lds_taps_row<U8, FAST>(pw, px, py, pc, B, v, H, a, s_src, s_ss, s_rs);
     } else {
@@ -184,7 +173,7 @@ DEV void lds_row(const float* pw, int px, int py, const PassConst& pc, const Dev
   const int W = pc.W, Hh = pc.H;
   const Homog H = scale_cols(H0);
   const float x = (float)(px - 5 + 2 * a);
-  if constexpr (U8 != TEX_F32 && FAST && DPE_PACKED_TAP) {
+  if constexpr (U8 != TEX_F32 && FAST) {
     const uint32_t stride = tex_stride<U8>(W), vadj = tex_vadj<U8>((uint32_t)v * tex_view<U8>(B), stride);
     const f2v tmax = tex_tmax2(W, Hh);
     const f2v* wp = (const f2v*)pw;
@@ -192,7 +181,6 @@ DEV void lds_row(const float* pw, int px, int py, const PassConst& pc, const Dev
     const float bz = __builtin_fmaf(H.h[6], x, H.h[8]);
     f2v r_sr = f2s(0.0f);
     float r_ss = 0;
-#if DPE_TAP_PAIR
 #pragma unroll
     for (int b = 0; b < 6; b += 2) {
       const f2v sp = tap2_fast<U8>(B, vadj, stride, tmax, H.h, bxy, bz, (f2v){(float)(py - 5 + 2 * b), (float)(py - 3 + 2 * b)});
@@ -203,16 +191,6 @@ DEV void lds_row(const float* pw, int px, int py, const PassConst& pc, const Dev
       r_sr = fma2(w1, f2s(sp.y), r_sr);
       r_ss = __builtin_fmaf(ws1, sp.y, r_ss);
     }
-#else
-#pragma unroll
-    for (int b = 0; b < 6; ++b) {
-      const float sp = tap_u8_fast<U8>(B, vadj, stride, tmax, H.h, bxy, bz, (float)(py - 5 + 2 * b));
-      const f2v w = wp[a * 6 + b];
-      r_sr = fma2(w, f2s(sp), r_sr);
-      const float ws = w.x * sp;
-      r_ss = __builtin_fmaf(ws, sp, r_ss);
-    }
-#endif
     r3[0] = r_sr.x; r3[1] = r_ss; r3[2] = r_sr.y;
   } else {
     const float bx = __builtin_fmaf(H.h[0], x, H.h[2]) * kTexUnit;
@@ -235,26 +213,7 @@ DEV void lds_row(const float* pw, int px, int py, const PassConst& pc, const Dev
     r3[0] = r_src; r3[1] = r_ss; r3[2] = r_rs;
   }
 }
-#ifndef DPE_CLAMP_ELIDE
-#define DPE_CLAMP_ELIDE 0
-#endif
-#ifndef DPE_ELIDE_UNIFORM
-#define DPE_ELIDE_UNIFORM 1
-#endif
-// clamp-free tap loop in the strong sweep's pools and LocalRefine (A/B knobs)
-#ifndef DPE_STRONG_ELIDE
-#define DPE_STRONG_ELIDE false
-#endif
-#ifndef DPE_D2W_ROW1
-#define DPE_D2W_ROW1 1   // DepthToWeak's slow tap loop one row at a time (lds_taps ROW1; A/B -0.3 ms)
-#endif
-#ifndef DPE_D2W_ELIDE
-#define DPE_D2W_ELIDE true
-#endif
-#ifndef DPE_LR_ELIDE
-#define DPE_LR_ELIDE false
-#endif
-template <int U8, bool ELIDE = false, bool ROW1 = false>
+template <int U8, bool ROW1 = false>
 DEV float ncc_old_lds(const float* pw, float s_ref, float s_rr, float s_w, int px, int py, const PassConst& pc,
                       const DevBufs& B, int v, const float4& pl) {
   const Homog H = make_homography(pc, v, pl);
@@ -262,41 +221,18 @@ DEV float ncc_old_lds(const float* pw, float s_ref, float s_rr, float s_w, int p
   count_work(B, 1, 36);
   float a[3];
   if (rcp_range_ok(H, (float)(px - 5), (float)(px + 5), (float)(py - 5), (float)(py + 5))) {
-#if DPE_CLAMP_ELIDE
-    // wave-uniform choice: the clamped loop gives the same bits for patches inside the image, so a
-    // wave whose lanes disagree runs that loop once instead of both loops under partial masks
-    bool in = false;
-    if constexpr (ELIDE) {
-      in = patch_inside(H, (float)(px - 5), (float)(px + 5), (float)(py - 5), (float)(py + 5), pc.W, pc.H);
-#if DPE_LINE_STATS   // row 0 of the statistics: [wave calls all inside, wave calls, lanes inside, lanes]
-      {
-        const uint64_t bi = __ballot(in), ba = __ballot(1);
-        if ((int)(threadIdx.x & 63) == __builtin_ctzll(ba)) {
-          atomicAdd(&g_lstat[0][0], bi == ba ? 1ull : 0ull); atomicAdd(&g_lstat[0][1], 1ull);
-          atomicAdd(&g_lstat[0][2], (unsigned long long)__popcll(bi)); atomicAdd(&g_lstat[0][3], (unsigned long long)__popcll(ba));
-        }
-      }
-#endif
-#if DPE_ELIDE_UNIFORM
-      in = __all(in);
-#endif
-    }
-    if (in)
-      lds_taps<U8, true, true>(pw, px, py, pc, B, v, H, a);
-    else
-#endif
-      lds_taps<U8, true>(pw, px, py, pc, B, v, H, a);
+    lds_taps<U8, true>(pw, px, py, pc, B, v, H, a);
   } else
-    lds_taps<U8, false, false, ROW1>(pw, px, py, pc, B, v, H, a);
+    lds_taps<U8, false, ROW1>(pw, px, py, pc, B, v, H, a);
   return ncc_finalize_pre(s_ref, s_rr, s_w, a[0], a[1], a[2]);   // (inv, mref, var_ref) of patch_lds_pre
 }
 
-// ELIDE: try the clamp-free tap loop on patches that project inside the image (patch_inside); it
-// pays in DepthToWeak and the weak sweep, not in the strong sweep or LocalRefine (A/B).
-template <int U8, bool ELIDE = false, bool ROW1 = false>
+// ROW1: the rare slow tap loop (clamped taps, IEEE reciprocal) one patch row at a time, which
+// lowers the caller's register peak (DepthToWeak, the weak sweep's final Old NCC)
+template <int U8, bool ROW1 = false>
 DEV float ncc_old_any(bool fast, const float* pw, float s_ref, float s_rr, float s_w, int px, int py,
                       const PassConst& pc, const DevBufs& B, int v, const float4& pl) {
-  if (fast) return ncc_old_lds<U8, ELIDE, ROW1>(pw, s_ref, s_rr, s_w, px, py, pc, B, v, pl);
+  if (fast) return ncc_old_lds<U8, ROW1>(pw, s_ref, s_rr, s_w, px, py, pc, B, v, pl);
   return ncc_old_generic<U8>(pc, B, px, py, v, pl);
 }
 
@@ -347,16 +283,8 @@ DEV uint8_t d2w_class(const PassConst& pc, const float* pcs, uint64_t is_peak) {
   return cls;
 }
 
-// grid: one wave per pixel, 4 waves per 256-thread workgroup.
-#ifndef DPE_BW_D2W
-#define DPE_BW_D2W 4
-#endif
-#ifndef DPE_BW_LR
-#define DPE_BW_LR 4
-#endif
-#ifndef DPE_D2W_WAVES
-#define DPE_D2W_WAVES DPE_TAP_WAVES
-#endif
+// grid: one wave per pixel, 4 waves per 256-thread workgroup (DepthToWeak); LocalRefine likewise
+constexpr int kBwD2W = 4, kBwLR = 4;
 // LocalRefine fused into DepthToWeak's epilogue (LR = true).  For an interior pixel LocalRefine's 11
 // hypotheses (p_disp -5..5, DPE.cu:2809-2831) are DepthToWeak's samples 25..35 (:2663-2686): same
 // plane, depth, selected views and weights, so every per-view NCC and geometric term is the same
@@ -367,12 +295,6 @@ DEV uint8_t d2w_class(const PassConst& pc, const float* pcs, uint64_t is_peak) {
 // depth maps, so doing LocalRefine right after the classification of the same pixel gives the
 // reference's results.  The 6-pixel border, where DepthToWeak stops at once (:2604-2607) but
 // LocalRefine runs, goes to k_local_refine_jobs over the border pixels (border_pixel).
-#ifndef DPE_GEOM_EARLY
-#define DPE_GEOM_EARLY 0   // 1: DepthToWeak issues the geometric term's depth gather before the NCC (A/B)
-#endif
-#ifndef DPE_FUSE_LR
-#define DPE_FUSE_LR 1
-#endif
 constexpr int kD2WMargin = 6;
 // pixels outside DepthToWeak's interior (x or y within kD2WMargin of the edge), enumerated: top rows,
 // bottom rows, then the left and right margins of the rows in between (every pixel if no interior)
@@ -392,14 +314,14 @@ DEV long border_pixel(long i, int W, int H) {
   return (long)row * W + (c < m ? c : W - 2 * m + c);
 }
 template <int U8, bool LR = false>
-__global__ void __launch_bounds__(64 * DPE_BW_D2W, DPE_D2W_WAVES) k_depth_to_weak(const PassConst* __restrict__ pcp, DevBufs B) {   // DPE.cu:2593-2747
-  __shared__ float s_patch[DPE_BW_D2W][108];
-  __shared__ float s_pc[DPE_BW_D2W][64];          // [0..60] cost curve, [61] LocalRefine's cost_now
-  __shared__ float s_lr[DPE_BW_D2W][11];          // LocalRefine's hypothesis costs (pd -5..5)
+__global__ void __launch_bounds__(64 * kBwD2W, kTapWaves) k_depth_to_weak(const PassConst* __restrict__ pcp, DevBufs B) {   // DPE.cu:2593-2747
+  __shared__ float s_patch[kBwD2W][108];
+  __shared__ float s_pc[kBwD2W][64];              // [0..60] cost curve, [61] LocalRefine's cost_now
+  __shared__ float s_lr[kBwD2W][11];              // LocalRefine's hypothesis costs (pd -5..5)
   const PassConst& pc = *pcp;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int W = pc.W, H = pc.H;
-  const long pix = (long)xcd_remap(blockIdx.x, gridDim.x, B.xcd_rows * 16 * ((pc.W + DPE_BW_D2W - 1) / DPE_BW_D2W)) * DPE_BW_D2W + wave;
+  const long pix = (long)xcd_remap(blockIdx.x, gridDim.x, B.xcd_rows * 16 * ((pc.W + kBwD2W - 1) / kBwD2W)) * kBwD2W + wave;
   if (pix >= (long)W * H) return;                 // wave-uniform
   const int x = (int)(pix % W), y = (int)(pix / W);
   const int center = (int)pix;
@@ -420,7 +342,7 @@ __global__ void __launch_bounds__(64 * DPE_BW_D2W, DPE_D2W_WAVES) k_depth_to_wea
   if (valid == 0) { if (lane == 0) B.weak[center] = DPE_UNKNOWN; return; }
   base_line /= valid;
   const float disp = c0.K[0] * base_line / od;
-  const bool fast = DPE_FAST_PATCH(pc);
+  const bool fast = FAST_PATCH(pc);
   float* pw = s_patch[wave];
   if (fast) patch_lds_build<64>(pw, pc, B, x, y, lane);
   wave_sync();
@@ -444,20 +366,12 @@ __global__ void __launch_bounds__(64 * DPE_BW_D2W, DPE_D2W_WAVES) k_depth_to_wea
         const int vi = si - 1;
         if (isSet(sel, vi)) {
           float tcst = 0.0f;
-#if DPE_GEOM_EARLY   // the source-depth gather in flight during the NCC
-          GeomFetch gfe;
-          if (pc.P.geom_consistency) gfe = geom_fetch(pc, B, si, fw);
-#endif
-          const float c = ncc_old_any<U8, DPE_D2W_ELIDE, DPE_D2W_ROW1 != 0>(fast, pw, s_ref, s_rr, s_w, x, y, pc, B, si, tp);
+          const float c = ncc_old_any<U8, true>(fast, pw, s_ref, s_rr, s_w, x, y, pc, B, si, tp);
           tcst += c;
           PHASE(1);
           if constexpr (LR) lr += (c * vw[vi]);                       // DPE.cu:2820
           if (pc.P.geom_consistency) {
-#if DPE_GEOM_EARLY
-            const float g = pc.P.geom_factor * geom_finish(pc, B, x, y, si, gfe);
-#else
             const float g = pc.P.geom_factor * geom_cost_at(pc, B, x, y, si, fw);
-#endif
             tcst += g;
             if constexpr (LR) lr += (g * vw[vi]);                     // :2822
           }
@@ -501,13 +415,10 @@ __global__ void __launch_bounds__(64 * DPE_BW_D2W, DPE_D2W_WAVES) k_depth_to_wea
 // view counts are.  Per-hypothesis sums over views then run on one lane each, in ascending view
 // order (the reference's si loop), and the arg-min on the pixel's first lane.
 constexpr int kLrPix = 4;
-#ifndef DPE_LR_VIEW_MAJOR
-#define DPE_LR_VIEW_MAJOR 1
-#endif
 template <int U8>
-__global__ void __launch_bounds__(64 * DPE_BW_LR, DPE_TAP_WAVES) k_local_refine_jobs(const PassConst* __restrict__ pcp, DevBufs B,
+__global__ void __launch_bounds__(64 * kBwLR, kTapWaves) k_local_refine_jobs(const PassConst* __restrict__ pcp, DevBufs B,
                                                                                      int border) {   // DPE.cu:2749-2835
-  constexpr int BW = DPE_BW_LR;
+  constexpr int BW = kBwLR;
   __shared__ float s_patch[BW][kLrPix][108];
   __shared__ float s_sum[BW][kLrPix][3];
   __shared__ float4 s_hyp[BW][kLrPix][12];
@@ -527,7 +438,7 @@ __global__ void __launch_bounds__(64 * DPE_BW_LR, DPE_TAP_WAVES) k_local_refine_
                            : ((long)xcd_remap(blockIdx.x, gridDim.x, B.xcd_rows * 16 * ((pc.W + BW * kLrPix - 1) / (BW * kLrPix))) * BW + wave) * kLrPix;
   if (base >= L) return;                          // wave-uniform
   const DpeCamera& c0 = pc.cams[0];
-  const bool fast = DPE_FAST_PATCH(pc);
+  const bool fast = FAST_PATCH(pc);
   const uint32_t vmask = (pc.N - 1) >= 32 ? 0xFFFFFFFFu : ((1u << (pc.N - 1)) - 1u);
   const int nv = pc.N - 1;
   float* res = s_dyn + (size_t)wave * kLrPix * 12 * nv * 2;   // res[((p * 12 + h) * nv + k) * 2 + {0, 1}]
@@ -590,23 +501,18 @@ __global__ void __launch_bounds__(64 * DPE_BW_LR, DPE_TAP_WAVES) k_local_refine_
     }
     const int ns = s_cnt[wave][p][0];
     unsigned m = (unsigned)s_cnt[wave][p][1];
-#if DPE_LR_VIEW_MAJOR
     // view-major: a pixel's hypotheses (depths a disparity step apart, one normal) of one view sit
     // on adjacent lanes, so their taps gather from neighbouring texels
     const int nh = __popc(m);
     for (int q = r % nh; q > 0; --q) m &= m - 1;      // the (r % nh)-th valid hypothesis
     const int h = __builtin_ctz(m), k = r / nh;
-#else
-    for (int q = r / ns; q > 0; --q) m &= m - 1;     // the (r / ns)-th valid hypothesis
-    const int h = __builtin_ctz(m), k = r % ns;
-#endif
     const uint32_t jxy = (uint32_t)s_xy[wave][p];
     const int jx = (int)(jxy & 0xFFFFu), jy = (int)(jxy >> 16);
     const int si = s_sel[wave][p][k] + 1;
     const float4 tp = s_hyp[wave][p][h];
     const float* sm = s_sum[wave][p];
     float* rr = res + ((p * 12 + h) * nv + k) * 2;
-    rr[0] = ncc_old_any<U8, DPE_LR_ELIDE>(fast, s_patch[wave][p], sm[0], sm[1], sm[2], jx, jy, pc, B, si, tp);
+    rr[0] = ncc_old_any<U8>(fast, s_patch[wave][p], sm[0], sm[1], sm[2], jx, jy, pc, B, si, tp);
     if (pc.P.geom_consistency) rr[1] = geom_cost_at(pc, B, jx, jy, si, s_fw[wave][p][h]);
   }
   wave_sync();
@@ -673,26 +579,6 @@ __global__ void __launch_bounds__(64) k_strong_tables_scan(const PassConst* __re
     const unsigned long long ge = m & from;
     if (t < len) out[idx] = ge ? t0 + __builtin_ctzll(ge) : carry;
     if (m) carry = t0 + __builtin_ctzll(m);
-  }
-}
-__global__ void k_strong_tables_rows(const PassConst* __restrict__ pcp, DevBufs B, int* __restrict__ next_right) {
-  const PassConst& pc = *pcp;
-  const int y = blockIdx.x * blockDim.x + threadIdx.x;
-  if (y >= pc.H) return;
-  int nxt = pc.W;
-  for (int x = pc.W - 1; x >= 0; --x) {
-    if (B.weak[y * pc.W + x] == DPE_STRONG) nxt = x;
-    next_right[y * pc.W + x] = nxt;
-  }
-}
-__global__ void k_strong_tables_cols(const PassConst* __restrict__ pcp, DevBufs B, int* __restrict__ next_down) {
-  const PassConst& pc = *pcp;
-  const int x = blockIdx.x * blockDim.x + threadIdx.x;
-  if (x >= pc.W) return;
-  int nxt = pc.H;
-  for (int y = pc.H - 1; y >= 0; --y) {
-    if (B.weak[y * pc.W + x] == DPE_STRONG) nxt = y;
-    next_down[y * pc.W + x] = nxt;
   }
 }
 __global__ void k_find_nearest_strong(const PassConst* __restrict__ pcp, DevBufs B, const int* __restrict__ next_right,

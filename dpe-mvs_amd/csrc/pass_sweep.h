@@ -25,18 +25,13 @@ namespace dpe {
 // MODE 2: colour-0 pixels of the red/black grid whose GenNeighbours failed (weak_rel == 0; the
 //         pixels NeigbourUpdate turns UNKNOWN), for the iteration-0 colour-0 strong sweep that runs
 //         beside GenNeighbours on the pre-GenNeighbours list (see dpe_pm_execute).
-// MODE 3: the WEAK pixels in two lists, [0] colour 0 of the red/black grid, [1] all others, so that
-//         GenNeighbours can finish the colour-0 pixels first (dpe_pm_execute, DPE_GN_SPLIT).
-// MODE 4: MODE 2 for colour 1.
 // Row-major order; one wave per row; ballot compaction keeps the order deterministic.
-template <int MODE> constexpr int list_count() { return MODE == 0 ? 4 : (MODE == 3 ? 2 : 1); }
-template <int MODE> DEV int list_rows(const PassConst& pc) { return (MODE == 1 || MODE == 3) ? pc.H : pc.half_rows; }
+template <int MODE> constexpr int list_count() { return MODE == 0 ? 4 : 1; }
+template <int MODE> DEV int list_rows(const PassConst& pc) { return MODE == 1 ? pc.H : pc.half_rows; }
 template <int MODE> DEV int list_key(const PassConst& pc, const DevBufs& B, int x, int y) {
   if constexpr (MODE == 2) return (((x + y) & 1) == 0 && B.weak_rel[y * pc.W + x] == 0) ? 0 : -1;
-  if constexpr (MODE == 4) return (((x + y) & 1) == 1 && B.weak_rel[y * pc.W + x] == 0) ? 0 : -1;
   const bool wk = B.weak[y * pc.W + x] == DPE_WEAK;
   if constexpr (MODE == 1) return wk ? 0 : -1;
-  else if constexpr (MODE == 3) return wk ? ((((x + y) & 1) == 0 && y < pc.half_rows) ? 0 : 1) : -1;
   else return (((x + y) & 1) << 1) | (wk ? 1 : 0);
 }
 template <int MODE>
@@ -288,15 +283,9 @@ DEV int acmh_candidate(const PassConst& pc, const float* __restrict__ costs, int
 }
 
 // ------------------------------------------------------------------------------ strong sweep
-#ifndef DPE_TAIL_SPLIT
-#define DPE_TAIL_SPLIT 1
-#endif
-#ifndef DPE_STRONG_PRE
-#define DPE_STRONG_PRE 1   // refinement draws on lanes 1..4 beside lane 0's acceptance (0: all on lane 0)
-#endif
 constexpr int kTailJobs = 16;   // a last round of at most this many jobs is split by patch rows
 // the strong sweep's LDS carve per wave (lds_layout.h: P pixels, C candidate lanes, nv source views)
-template <int P, int C> using StrongCarveT = lds::StrongCarve<P, C, DPE_TAIL_SPLIT ? kTailJobs : 0>;
+template <int P, int C> using StrongCarveT = lds::StrongCarve<P, C, kTailJobs>;
 __host__ __device__ inline int strong_lds_per_wave(int P, int C, int nv) {
   return P == 4 && C == 16 ? StrongCarveT<4, 16>::total(nv) : StrongCarveT<8, 8>::total(nv);
 }
@@ -315,11 +304,9 @@ DEV bool job_decode(const int* cnt, int j, int& p, int& r) {
   return false;
 }
 
-#ifndef DPE_BW_STRONG
-#define DPE_BW_STRONG 4
-#endif
+constexpr int kBwStrong = 4;   // waves per workgroup
 template <int U8, bool EDGE>
-__global__ void __launch_bounds__(64 * DPE_BW_STRONG, DPE_TAP_WAVES) k_strong_coop(const PassConst* __restrict__ pcp, DevBufs B, int iter,
+__global__ void __launch_bounds__(64 * kBwStrong, kTapWaves) k_strong_coop(const PassConst* __restrict__ pcp, DevBufs B, int iter,
                                                      const int* __restrict__ list, const int* __restrict__ nlist_p) {
   extern __shared__ float4 lds4[];
   float* lds = (float*)lds4;
@@ -331,7 +318,7 @@ __global__ void __launch_bounds__(64 * DPE_BW_STRONG, DPE_TAP_WAVES) k_strong_co
   const int ps = lane / C, c = lane % C;
   const int W = pc.W, nv = pc.N - 1;
   const DpeCamera& c0 = pc.cams[0];
-  const int wbase = (xcd_remap(blockIdx.x, gridDim.x, B.xcd_rows * 16) * DPE_BW_STRONG + wave) * P;
+  const int wbase = (xcd_remap(blockIdx.x, gridDim.x, B.xcd_rows * 16) * kBwStrong + wave) * P;
   if (wbase >= nlist) return;                          // wave-uniform tail
   const int gi = wbase + ps;
   const bool active = gi < nlist;
@@ -358,7 +345,7 @@ __global__ void __launch_bounds__(64 * DPE_BW_STRONG, DPE_TAP_WAVES) k_strong_co
   int* slots = ib + SC::ib_slots(nv);                    // [C + 1] cost-vector jobs: candidate slots, then C
   float4* cpl_all = (float4*)(wl + SC::cpl(nv));         // [P][C + 1] candidate planes, slot C = current
   int* alias_all = (int*)(wl + SC::alias(nv));           // [P][C + 1]
-  float* rnd = wl + SC::rnd(nv) + ps * 12;               // [P][12] refinement draws (DPE_STRONG_PRE)
+  float* rnd = wl + SC::rnd(nv) + ps * 12;               // [P][12] refinement draws
   float4* cpl = cpl_all + ps * (C + 1);
   int* alias = alias_all + ps * (C + 1);
   float4* hyp = hyp_all + ps * 5;
@@ -368,7 +355,7 @@ __global__ void __launch_bounds__(64 * DPE_BW_STRONG, DPE_TAP_WAVES) k_strong_co
 
   const float* __restrict__ costs_s = B.costs_snap;
   const float4* __restrict__ planes_s = B.planes_snap;
-  const bool fast = DPE_FAST_PATCH(pc);
+  const bool fast = FAST_PATCH(pc);
   bool on_edge = false;
   PHASE_BEGIN();
   // ---- phase 1: reference patch + candidate scans
@@ -452,7 +439,7 @@ __global__ void __launch_bounds__(64 * DPE_BW_STRONG, DPE_TAP_WAVES) k_strong_co
     const int total = S * nv, tail = total & 63;
     // a last round with at most kTailJobs jobs: each job's 6 patch rows go to 64 / tail lanes (rows
     // per lane 1 or 2), the row sums meet in LDS, and one lane per job adds them in row order
-    const bool split = DPE_TAIL_SPLIT && fast && tail > 0 && tail <= kTailJobs;
+    const bool split = fast && tail > 0 && tail <= kTailJobs;
     const int jend = split ? total - tail : total;
     for (int j = lane; j < jend; j += 64) {
       job_decode<P>(cnt, j % S, q, r);
@@ -463,7 +450,7 @@ __global__ void __launch_bounds__(64 * DPE_BW_STRONG, DPE_TAP_WAVES) k_strong_co
       const float4 pl = cpl_all[q * (C + 1) + slot];
       const float* sm = sums_all + q * 4;
       cost_all[(q * (C + 1) + slot) * nv + v - 1] =
-          ncc_old_any<U8, DPE_STRONG_ELIDE>(fast, pw_all + q * 108, sm[0], sm[1], sm[2], qx, qy, pc, B, v, pl);
+          ncc_old_any<U8>(fast, pw_all + q * 108, sm[0], sm[1], sm[2], qx, qy, pc, B, v, pl);
     }
     if (split) {
       float* tb = wl + SC::tail(nv);                     // [job][row][3]
@@ -604,7 +591,6 @@ __global__ void __launch_bounds__(64 * DPE_BW_STRONG, DPE_TAP_WAVES) k_strong_co
   float cost_now = 0.0f, cost_written = 0.0f, depth_now = 0.0f;
   float4 pnow = make_float4(0, 0, 0, 0);
   const float pert = (float)(0.02f * 3.14159265358979323846);
-#if DPE_STRONG_PRE
   // lanes 1..4 evaluate the refinement draws (refine_draws: stream words 15.. after the view
   // sampling) while lane 0 runs the acceptance; lane 0 then finishes the hypotheses from them
   if (active && c >= 1 && c <= 4) {
@@ -612,7 +598,6 @@ __global__ void __launch_bounds__(64 * DPE_BW_STRONG, DPE_TAP_WAVES) k_strong_co
     if (c == 1) { rnd[0] = d.u_depth; rnd[1] = d.n[0]; rnd[2] = d.n[1]; rnd[3] = d.n[2]; rnd[4] = d.u_pert; }
     else refine_angle(rs, d.w_angles, c - 2, pert, &rnd[5 + 2 * (c - 2)], &rnd[6 + 2 * (c - 2)]);
   }
-#endif
   if (active && c == 0) {
     int mi = 0; float mcost = fc[0];
     for (int i = 1; i < 8; ++i) if (fc[i] <= mcost) { mcost = fc[i]; mi = i; }
@@ -631,23 +616,7 @@ __global__ void __launch_bounds__(64 * DPE_BW_STRONG, DPE_TAP_WAVES) k_strong_co
         depth_now = db; pnow = cand; cost_now = fc[mi]; B.sel[center] = tsv;
       }
     }
-#if !DPE_STRONG_PRE
-    const float dmin = pc.P.depth_min, dmax = pc.P.depth_max;
-    const float depth_rand = rng_uniform(rs) * (dmax - dmin) + dmin;
-    const float4 prand = random_normal(c0, x, y, rs, depth_now);
-    const float dminp = (1 - 0.02f) * depth_now, dmaxp = (1 + 0.02f) * depth_now;
-    const float depth_perturbed = rng_uniform(rs) * (dmaxp - dminp) + dminp;
-    const float4 ppert = perturbed_normal(c0, x, y, pnow, rs, pert);
-    float4 h0 = pnow, h1 = prand, h2 = prand, h3 = ppert, h4 = pnow;
-    h0.w = dist2origin(c0, x, y, depth_rand, h0);
-    h1.w = dist2origin(c0, x, y, depth_now, h1);
-    h2.w = dist2origin(c0, x, y, depth_rand, h2);
-    h3.w = dist2origin(c0, x, y, depth_now, h3);
-    h4.w = dist2origin(c0, x, y, depth_perturbed, h4);
-    hyp[0] = h0; hyp[1] = h1; hyp[2] = h2; hyp[3] = h3; hyp[4] = h4;
-#endif
   }
-#if DPE_STRONG_PRE
   wave_sync();
   if (active && c == 0) {
     const float dmin = pc.P.depth_min, dmax = pc.P.depth_max;
@@ -664,7 +633,6 @@ __global__ void __launch_bounds__(64 * DPE_BW_STRONG, DPE_TAP_WAVES) k_strong_co
     h4.w = dist2origin(c0, x, y, depth_perturbed, h4);
     hyp[0] = h0; hyp[1] = h1; hyp[2] = h2; hyp[3] = h3; hyp[4] = h4;
   }
-#endif
   wave_sync();
   PHASE(9);
   // ---- phase 6: refinement NCCs, one flat pool of (pixel, hypothesis, selected view)
@@ -678,7 +646,7 @@ __global__ void __launch_bounds__(64 * DPE_BW_STRONG, DPE_TAP_WAVES) k_strong_co
       const int h = r % 5, k = r / 5;                      // the 5 hypotheses of one view adjacent
       const int cq = list[wbase + q];
       const float* sm = sums_all + q * 4;
-      ref_all[(q * 5 + h) * nv + k] = ncc_old_any<U8, DPE_STRONG_ELIDE>(fast, pw_all + q * 108, sm[0], sm[1], sm[2], cq % W, cq / W, pc,
+      ref_all[(q * 5 + h) * nv + k] = ncc_old_any<U8>(fast, pw_all + q * 108, sm[0], sm[1], sm[2], cq % W, cq / W, pc,
                                                       B, iq[SC::IB_SEL + k] + 1, hyp_all[q * 5 + h]);
     }
   }
@@ -731,20 +699,17 @@ struct WeakTab {
   float nbox[4];                          // x0, x1, y0, y1 of the union of the neighbour patches
 };
 
-#ifndef DPE_WEAK_NBMAX
-#define DPE_WEAK_NBMAX 0   // the neighbour loop's patch_ncc_tab without the side-4..6 cases (tab_n implies side <= 3)
-#endif
 // patch NCC with tabulated weights; the same tap order and arithmetic as patch_ncc_generic.
 // NN > 0: the patch side n is the compile-time NN, so the tap loop unrolls and the gathers of a
 // patch are in flight together (the weak sweep's patches are 3x3 and 4..6 square).
-template <int U8, bool FAST, int NN = 0, bool IN = false>
+template <int U8, bool FAST, int NN = 0>
 DEV void tab_taps(const PassConst& pc, const DevBufs& B, int v, const Homog& H0, int cx, int cy, int rad, int inc,
                   int n_rt, const float* __restrict__ tw, float* acc) {
   const int W = pc.W, Hh = pc.H;
   const Homog H = scale_cols(H0);
   const int n = NN > 0 ? NN : n_rt;
   const f2v* wp = (const f2v*)tw;            // (w, w*grey) pairs
-  if constexpr (U8 != TEX_F32 && FAST && DPE_PACKED_TAP) {
+  if constexpr (U8 != TEX_F32 && FAST) {
     const uint32_t stride = tex_stride<U8>(W), vadj = tex_vadj<U8>((uint32_t)v * tex_view<U8>(B), stride);
     const f2v tmax = tex_tmax2(W, Hh);
     f2v s_sr = f2s(0.0f);
@@ -758,7 +723,7 @@ DEV void tab_taps(const PassConst& pc, const DevBufs& B, int v, const Homog& H0,
       float r_ss = 0;
 #pragma unroll
       for (int b = 0; b < (NN > 0 ? NN : n); ++b) {
-        const float sp = tap_u8_fast<U8, IN>(B, vadj, stride, tmax, H.h, bxy, bz, (float)(cy - rad + b * inc));
+        const float sp = tap_u8_fast<U8>(B, vadj, stride, tmax, H.h, bxy, bz, (float)(cy - rad + b * inc));
         const f2v w = wp[a * n + b];
         r_sr = fma2(w, f2s(sp), r_sr);
         const float ws = w.x * sp;
@@ -792,66 +757,12 @@ DEV void tab_taps(const PassConst& pc, const DevBufs& B, int v, const Homog& H0,
     acc[0] = s_src; acc[1] = s_ss; acc[2] = s_rs;
   }
 }
-// The fast tap loop of a runtime side n <= NMAX on one code path: rows and columns beyond n are
-// masked off, so lanes whose patches differ in size run together (same per-lane tap sequence and
-// sums as tab_taps<U8, true, n>).
-#ifndef DPE_WEAK_MASKED
-#define DPE_WEAK_MASKED 0
-#endif
-template <int U8, int NMAX>
-DEV void tab_taps_masked(const PassConst& pc, const DevBufs& B, int v, const Homog& H0, int cx, int cy, int rad, int inc,
-                         int n, const float* __restrict__ tw, float* acc) {
-  const int W = pc.W, Hh = pc.H;
-  const Homog H = scale_cols(H0);
-  const f2v* wp = (const f2v*)tw;
-  const uint32_t stride = tex_stride<U8>(W), vadj = tex_vadj<U8>((uint32_t)v * tex_view<U8>(B), stride);
-  const f2v tmax = tex_tmax2(W, Hh);
-  f2v s_sr = f2s(0.0f);
-  float s_ss = 0;
-#pragma unroll
-  for (int a = 0; a < NMAX; ++a) {
-    if (a < n) {
-      const float xf = (float)(cx - rad + a * inc);
-      const f2v bxy = fma2((f2v){H.h[0], H.h[3]}, f2s(xf), (f2v){H.h[2], H.h[5]}) * f2s(kTexUnit);
-      const float bz = __builtin_fmaf(H.h[6], xf, H.h[8]);
-      f2v r_sr = f2s(0.0f);
-      float r_ss = 0;
-#pragma unroll
-      for (int b = 0; b < NMAX; ++b) {
-        if (b < n) {
-          const float sp = tap_u8_fast<U8, false>(B, vadj, stride, tmax, H.h, bxy, bz, (float)(cy - rad + b * inc));
-          const f2v w = wp[a * n + b];
-          r_sr = fma2(w, f2s(sp), r_sr);
-          const float ws = w.x * sp;
-          r_ss = __builtin_fmaf(ws, sp, r_ss);
-        }
-      }
-      s_sr += r_sr; s_ss += r_ss;
-    }
-  }
-  acc[0] = s_sr.x; acc[1] = s_ss; acc[2] = s_sr.y;
-}
-
 // NMAX: the largest side the caller can pass (the neighbour patches are tabulated only up to 3)
 template <int U8, int NMAX = 6>
 DEV float patch_ncc_tab(const PassConst& pc, const DevBufs& B, int v, const Homog& H, int cx, int cy, int rad, int inc,
                         int n, const float* __restrict__ tw, const float* sm) {
   float a[3];
   if (rcp_range_ok(H, (float)(cx - rad), (float)(cx + rad), (float)(cy - rad), (float)(cy + rad))) {
-    if constexpr (DPE_WEAK_MASKED && U8 != TEX_F32 && DPE_PACKED_TAP) {
-      if (n >= 3 && n <= 6) {
-        tab_taps_masked<U8, 6>(pc, B, v, H, cx, cy, rad, inc, n, tw, a);
-        count_work(B, 0, (unsigned long long)(n * n));
-        return ncc_finalize_pre(sm[0], sm[1], sm[2], a[0], a[1], a[2]);
-      }
-    }
-#if DPE_WEAK_NBMAX
-    if (n == 3) tab_taps<U8, true, 3>(pc, B, v, H, cx, cy, rad, inc, n, tw, a);
-    else if (NMAX >= 4 && n == 4) tab_taps<U8, true, (NMAX >= 4 ? 4 : 1)>(pc, B, v, H, cx, cy, rad, inc, n, tw, a);
-    else if (NMAX >= 5 && n == 5) tab_taps<U8, true, (NMAX >= 5 ? 5 : 1)>(pc, B, v, H, cx, cy, rad, inc, n, tw, a);
-    else if (NMAX >= 6 && n == 6) tab_taps<U8, true, (NMAX >= 6 ? 6 : 1)>(pc, B, v, H, cx, cy, rad, inc, n, tw, a);
-    else tab_taps<U8, true>(pc, B, v, H, cx, cy, rad, inc, n, tw, a);
-#else
     switch (n) {
       case 3: tab_taps<U8, true, 3>(pc, B, v, H, cx, cy, rad, inc, n, tw, a); break;
       case 4: tab_taps<U8, true, 4>(pc, B, v, H, cx, cy, rad, inc, n, tw, a); break;
@@ -859,7 +770,6 @@ DEV float patch_ncc_tab(const PassConst& pc, const DevBufs& B, int v, const Homo
       case 6: tab_taps<U8, true, 6>(pc, B, v, H, cx, cy, rad, inc, n, tw, a); break;
       default: tab_taps<U8, true>(pc, B, v, H, cx, cy, rad, inc, n, tw, a); break;
     }
-#endif
   } else {
     tab_taps<U8, false>(pc, B, v, H, cx, cy, rad, inc, n, tw, a);
   }
@@ -867,12 +777,9 @@ DEV float patch_ncc_tab(const PassConst& pc, const DevBufs& B, int v, const Homo
   return ncc_finalize_pre(sm[0], sm[1], sm[2], a[0], a[1], a[2]);
 }
 
-// Weak-sweep path statistics (build with -DDPE_WEAK_STATS=1; tools/weak_stats.py): per NCC-New,
+// Weak-sweep path statistics (DPE_DIAG & 4; tools/weak_stats.py): per NCC-New,
 // the centre patch side and path, the neighbour-patch paths, and per wave the number of distinct
 // centre-patch variants its lanes execute one after another.  Off in the product.
-#ifndef DPE_WEAK_STATS
-#define DPE_WEAK_STATS 0
-#endif
 #if DPE_WEAK_STATS
 // 0 jobs, 1 centre outside, 2..11 n_c histogram (n 0..9, 9 = larger), 12 centre generic (untabulated),
 // 13 centre tabulated but slow reciprocal, 14 neighbour box fast, 15 neighbour patches, 16 neighbour
@@ -945,7 +852,7 @@ DEV float ncc_new_tab(const PassConst& pc, const DevBufs& B, const WeakTab& T, i
       const float* sm = T.sums + 3 * k;
       tc = ncc_finalize_pre(sm[0], sm[1], sm[2], a[0], a[1], a[2]);
     } else {
-      tc = T.tab_n ? patch_ncc_tab<U8, DPE_WEAK_NBMAX ? 3 : 6>(pc, B, v, H, np.x, np.y, T.rad_n, T.inc_n, T.n_n, T.tn + (k - 1) * 18,
+      tc = T.tab_n ? patch_ncc_tab<U8, 6>(pc, B, v, H, np.x, np.y, T.rad_n, T.inc_n, T.n_n, T.tn + (k - 1) * 18,
                                        T.sums + 3 * k)
                    : patch_ncc_generic<U8>(pc, B, v, H, np.x, np.y, T.rc, T.rad_n, T.inc_n);
     }
@@ -957,51 +864,17 @@ DEV float ncc_new_tab(const PassConst& pc, const DevBufs& B, const WeakTab& T, i
   return (float)(0.25 * (double)center_cost + 0.75 * (double)strong_cost);
 }
 
-#ifndef DPE_WEAK_VIEW_MAJOR
-#define DPE_WEAK_VIEW_MAJOR 1
-#endif
-#ifndef DPE_WEAK_POOL
-#define DPE_WEAK_POOL 1
-#endif
 // LDS floats per weak pixel (lds_layout.h WeakCarve: fixed part, then [8][nv] costs, [nv] sampling
 // probabilities, [nv] selected views, [7][nv] hypothesis values; multiple of 4).  At 9 source views a
 // pixel takes 636 floats, so four 4-wave workgroups (4 x 40.7 KB) fit a CU's LDS.
-#ifndef DPE_WEAK_OLD_ELIDE
-#define DPE_WEAK_OLD_ELIDE 1   // the final Old NCC with the clamp-free loop for patches inside the image
-                               // (its slow loop one row at a time, lds_taps ROW1: no scratch)
-#endif
-#ifndef DPE_WEAK_ROW1
-#define DPE_WEAK_ROW1 1     // the final Old NCC's slow tap loop one row at a time (lds_taps ROW1)
-#endif
-#ifndef DPE_WEAK_TPC
-#define DPE_WEAK_TPC 0      // pooled jobs read the neighbour-patch parameters from the pass constants
-#endif
-#ifndef DPE_WEAK_TCOPY
-#define DPE_WEAK_TCOPY 0    // plain copies of the patch parameters for the per-patch selects (no scratch for T)
-#endif
-#ifndef DPE_WEAK_TBATCH
-#define DPE_WEAK_TBATCH 0   // patch weight tables filled 8 entries per lane at a time (loads batched)
-#endif
-#ifndef DPE_WEAK_SROWS
-#define DPE_WEAK_SROWS 0    // the centre patch's reference sums split by rows over lanes 0..5
-#endif
-#ifndef DPE_WEAK_GPOOL
-#define DPE_WEAK_GPOOL 0   // the final candidate costs' geometric terms as one wave pool (0: 8 lanes per pixel, serial)
-#endif
-#ifndef DPE_WEAK_PRE
-#define DPE_WEAK_PRE 1   // refinement draws on lanes 1..4 beside lane 0's acceptance (0: all on lane 0)
-#endif
-using WC = lds::WeakCarveT<DPE_WEAK_PRE != 0>;
+using WC = lds::WeakCarveT<true>;
 constexpr int kWeakFixed = WC::FIXED;
 __host__ __device__ inline int weak_lds_per_pixel(int nv) { return WC::per_pixel(nv); }
 
 // CheckerboardPropagationWeak (DPE.cu:1668-1862) + PlaneHypothesisRefinementWeak (:1120-1212).
 // C lanes per pixel, 64/C pixels per wave, blockDim.x/64 waves per workgroup.
-#ifndef DPE_WEAK_WAVES
-#define DPE_WEAK_WAVES DPE_TAP_WAVES
-#endif
 template <int U8, int C>
-__global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassConst* __restrict__ pcp, DevBufs B, int iter,
+__global__ void __launch_bounds__(256, kTapWaves) k_weak_coop(const PassConst* __restrict__ pcp, DevBufs B, int iter,
                                                    const int* __restrict__ list, const int* __restrict__ nlist_p) {
   extern __shared__ float4 lds4[];
   static_assert(C == 16 || C == 32, "the per-pixel phases give lanes 0..8 the patch sums and lanes 8..15 the alias rows");
@@ -1053,19 +926,13 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
   T.n_n = T.rad_n >= 0 ? (2 * T.rad_n) / T.inc_n + 1 : 0;
   T.tab_c = T.n_c >= 1 && T.n_c <= 6;
   T.tab_n = T.n_n >= 1 && T.n_n <= 3;
-  // plain copies for the per-patch selects below: a select between two fields of T takes their
-  // addresses, which keeps T in scratch (24 B/lane) for the whole kernel
-#if DPE_WEAK_TCOPY
-  const int rad_c = T.rad_c, inc_c = T.inc_c, n_c = T.n_c, rad_n = T.rad_n, inc_n = T.inc_n, n_n = T.n_n;
-  const bool tab_c = T.tab_c, tab_n = T.tab_n;
-#else   // references: the selects below take field addresses and keep T in scratch (the round-3 code)
+  // references: the selects below take field addresses and keep T in scratch (24 B/lane; plain
+  // copies measured 1 ms slower)
   const int &rad_c = T.rad_c, &inc_c = T.inc_c, &n_c = T.n_c, &rad_n = T.rad_n, &inc_n = T.inc_n, &n_n = T.n_n;
   const bool &tab_c = T.tab_c, &tab_n = T.tab_n;
-#endif
   T.rc = active ? ref_texel(B.ref, W, Hh, x, y) : 0.0f;
   T.tc = tcp; T.tn = tnp; T.sums = sums; T.nbl = nbl; T.nsv = nsv;
   const short2* nbg = B.nb + (size_t)center * 9;
-#if DPE_WEAK_POOL
   // pooled phases: the NCCs of all the wave's pixels are dealt round-robin over its 64 lanes (as
   // in the strong sweep), so a job carries its pixel q; pix(q) = that pixel's LDS block
   auto pix = [&](int q) -> float* { return (float*)lds4 + (size_t)(wave * P + q) * S; };
@@ -1074,13 +941,7 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
     const int* h = (const int*)(qb + WC::MISC);
     WeakTab t;
     t.rad_c = h[WC::M_RADC]; t.inc_c = h[WC::M_INCC]; t.n_c = h[WC::M_NC]; t.nb3 = h[WC::M_NB3] != 0;
-#if DPE_WEAK_TPC
-    // the neighbour-patch parameters are pass constants: scalar loads here instead of registers
-    // held across the pools
-    t.rad_n = pc.P.weak_radius; t.inc_n = pc.P.weak_increment; t.n_n = pc.weak_nn; t.tab_n = t.n_n >= 1 && t.n_n <= 3;
-#else
     t.rad_n = T.rad_n; t.inc_n = T.inc_n; t.n_n = T.n_n; t.tab_n = T.tab_n;
-#endif
     t.tab_c = t.n_c >= 1 && t.n_c <= 6;
     t.rc = qb[WC::RC];
     t.nbox[0] = qb[WC::NBOX_A]; t.nbox[1] = qb[WC::NBOX_A + 1]; t.nbox[2] = qb[WC::NBOX_A + 2]; t.nbox[3] = qb[WC::NBOX_B];
@@ -1089,7 +950,6 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
     return t;
   };
   int pcnt[P];
-#endif
 
   PHASE_BEGIN();
   // ---- phase 1: neighbours, weight tables, Old-NCC patch, candidate rows
@@ -1102,34 +962,6 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
     }
     const int ntc = tab_c ? n_c * n_c : 0, ntn = tab_n ? n_n * n_n : 0;
     const float ss = pc.P.sigma_spatial, sc = pc.P.sigma_color;
-#if DPE_WEAK_TBATCH
-    // the same entries in batches of 8 per lane: neighbour pixels, then grey levels, then weights
-    // (two dependent loads per entry issued 8 at a time instead of one entry after another)
-    const int nt = ntc + 8 * ntn;
-    for (int t0 = c; t0 < nt; t0 += 8 * C) {
-      short2 npv[8]; int iv[8], jv[8], dv[8]; float rpv[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int t = t0 + u * C;
-        int k = 0, tt = 0, n = 1, rad = 0, inc = 0;
-        if (t < ntc) { tt = t; n = n_c; rad = rad_c; inc = inc_c; }
-        else if (t < nt) { k = 1 + (t - ntc) / ntn; tt = (t - ntc) % ntn; n = n_n; rad = rad_n; inc = inc_n; }
-        iv[u] = -rad + (tt / n) * inc; jv[u] = -rad + (tt % n) * inc;
-        dv[u] = k == 0 ? 2 * tt : WC::TN - WC::TC + 2 * ((k - 1) * 9 + tt);   // float offset from tcp
-        npv[u] = t < nt ? nbg[k] : make_short2(-1, -1);
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        rpv[u] = (npv[u].x == -1 || npv[u].y == -1) ? 0.0f : ref_texel(B.ref, W, Hh, npv[u].x + iv[u], npv[u].y + jv[u]);
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        if (npv[u].x == -1 || npv[u].y == -1) continue;
-        const float w = bilateral_weight(iv[u], jv[u], rpv[u], T.rc, ss, sc);
-        float* dst = tcp + dv[u];
-        dst[0] = w; dst[1] = w * rpv[u];
-      }
-    }
-#else
     for (int t = c; t < ntc + 8 * ntn; t += C) {
       int k, tt, n, rad, inc;
       if (t < ntc) { k = 0; tt = t; n = n_c; rad = rad_c; inc = inc_c; }
@@ -1142,7 +974,6 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
       float* dst = k == 0 ? tcp + 2 * tt : tnp + 2 * ((k - 1) * 9 + tt);
       dst[0] = w; dst[1] = w * rp;
     }
-#endif
     for (int i = c; i < 8; i += C) {
       const short2 np = nbg[i + 1];
       const bool fl = !(np.x == -1 || np.y == -1) && B.weak[np.x + np.y * W] == DPE_STRONG;
@@ -1169,34 +1000,13 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
     }
   }
   // ---- phase 1b: reference sums of every tabulated patch (tap order of patch_ncc_generic)
-  float cr_ref = 0.0f, cr_rr = 0.0f, cr_w = 0.0f;   // DPE_WEAK_SROWS: this lane's centre-patch row
-  (void)cr_ref; (void)cr_rr; (void)cr_w;
   if (active) {
     if (c == C - 2) {
       misc[WC::M_RADC] = T.rad_c; misc[WC::M_INCC] = T.inc_c; misc[WC::M_NC] = T.n_c; misc[WC::M_NB3] = T.nb3 ? 1 : 0;
       pb[WC::NBOX_A] = T.nbox[0]; pb[WC::NBOX_A + 1] = T.nbox[1]; pb[WC::NBOX_A + 2] = T.nbox[2]; pb[WC::NBOX_B] = T.nbox[3];
       pb[WC::RC] = T.rc;
     }
-#if DPE_WEAK_SROWS
-    // the centre patch's rows on lanes 0..5 (row sums combined in row order below), the 8 neighbour
-    // patches on lanes 6..13
-    if (c < 6) {
-      const short2 np = nbl[0];
-      if (!(np.x == -1 || np.y == -1) && tab_c && c < n_c) {
-        const int a = c;
-        for (int b = 0; b < n_c; ++b) {
-          const float rp = ref_texel(B.ref, W, Hh, np.x - rad_c + a * inc_c, np.y - rad_c + b * inc_c);
-          const float w = tcp[2 * (a * n_c + b)], wr = tcp[2 * (a * n_c + b) + 1];
-          cr_ref = cr_ref + wr;
-          cr_rr = __builtin_fmaf(wr, rp, cr_rr);
-          cr_w = cr_w + w;
-        }
-      }
-    }
-    for (int k = c - 5; k >= 1 && k < 9; k += C) {
-#else
     for (int k = c; k < 9; k += C) {
-#endif
       const short2 np = nbl[k];
       if (np.x == -1 || np.y == -1 || !(k == 0 ? tab_c : tab_n)) continue;
       const int n = k == 0 ? n_c : n_n, rad = k == 0 ? rad_c : rad_n, inc = k == 0 ? inc_c : inc_n;
@@ -1230,23 +1040,9 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
       alias[i] = a;
     }
   }
-#if DPE_WEAK_SROWS
-  {   // every lane: the pixel's centre rows 0..5 from lanes ps*C + a, added in row order on lane 0
-    float a_ref = 0, a_rr = 0, a_w = 0;
-#pragma unroll
-    for (int a = 0; a < 6; ++a) {
-      const int src = ps * C + a;
-      const float r0 = __shfl(cr_ref, src), r1 = __shfl(cr_rr, src), r2 = __shfl(cr_w, src);
-      if (a < n_c) { a_ref += r0; a_rr += r1; a_w += r2; }
-    }
-    if (active && c == 0 && tab_c && !(nbl[0].x == -1 || nbl[0].y == -1))
-      ncc_pre(a_ref, a_rr, a_w, sums[0], sums[1], sums[2]);
-  }
-#endif
   wave_sync();
   PHASE(1);
   // ---- phase 2: candidate cost vectors, jobs (unique flagged neighbour plane, view)
-#if DPE_WEAK_POOL
   if (active && c == 0) {
     uint32_t um = 0;
     for (int i = 0; i < 8; ++i) if (misc[WC::M_FLAGS + i] && alias[i] == i) um |= 1u << i;
@@ -1273,24 +1069,6 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
       (qb + WC::cost(nv))[i * nv + v - 1] = ncc_new_tab<U8>(pc, B, tab_of(q), cq % W, cq / W, v, ((const float4*)(qb + WC::CPL))[i]);
     }
   }
-#else
-  if (active) {
-    uint32_t um = 0;
-    for (int i = 0; i < 8; ++i) if (misc[WC::M_FLAGS + i] && alias[i] == i) um |= 1u << i;
-    const int ncand = __builtin_popcount(um);
-    for (int j = c; j < ncand * nv; j += C) {
-      uint32_t m = um;
-#if DPE_WEAK_VIEW_MAJOR
-      for (int q = j % ncand; q > 0; --q) m &= m - 1;     // view-major: a round's lanes share views
-      const int i = __builtin_ctz(m), v = j / ncand + 1;
-#else
-      for (int q = j / nv; q > 0; --q) m &= m - 1;
-      const int i = __builtin_ctz(m), v = j % nv + 1;
-#endif
-      cost[i * nv + v - 1] = ncc_new_tab<U8>(pc, B, T, x, y, v, cpl[i]);
-    }
-  }
-#endif
   wave_sync();
   PHASE(2);
   if (active)
@@ -1325,9 +1103,7 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
     for (int i = 0; i < nv; ++i) if (vwl[i] > 0) { setBit(tsv, i); wnorm += vwl[i]; sel_list[ns++] = i; }
     misc[WC::M_NSEL] = ns;
     misc[WC::M_WNORM] = __float_as_int(wnorm);
-#if DPE_WEAK_POOL
     hyp[6] = B.fit_plane[center];
-#endif
   }
   wave_sync();
   PHASE(5);
@@ -1336,13 +1112,8 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
   const float4 cur = active ? B.planes[center] : make_float4(0, 0, 0, 1);
   const float4 fp = active ? B.fit_plane[center] : make_float4(0, 0, 0, 0);
   const bool has_fit = !(fp.x == 0 && fp.y == 0 && fp.z == 0);
-  auto hyp_val = [&](int v, const float4& pl) __attribute__((always_inline)) -> float {   // one term of hyp_cost (DPE.cu:1140-1150)
-    const float cn = ncc_new_tab<U8>(pc, B, T, x, y, v, pl);
-    return geom ? cn + gf * geom_cost(pc, B, x, y, v, pl) : cn;
-  };
   // ---- phase 4: current plane and fit plane over the selected views; final candidate costs
-#if DPE_WEAK_POOL
-  // pixel q's hyp_cost term (view v, plane pl) into its hv row
+  // pixel q's hyp_cost term (DPE.cu:1140-1150) (view v, plane pl) into its hv row
   auto hyp_val_q = [&](int q, int v, const float4& pl) __attribute__((always_inline)) -> float {
     const int cq = list[wbase + q];
     const int qx = cq % W, qy = cq / W;
@@ -1366,50 +1137,9 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
       (qb + WC::hv(nv))[h * nv + k] = hyp_val_q(q, v, h ? ((const float4*)(qb + WC::HYP))[6] : B.planes[list[wbase + q]]);
     }
   }
-#if DPE_WEAK_GPOOL
-  // the final candidate costs' geometric terms, one pool of (pixel, candidate, selected view): each
-  // flagged candidate's cost[i][view] becomes cost + gf * geom in place (the same two roundings as
-  // the sum below would do), so the per-candidate sums only add
-  if (geom) {
-#pragma unroll
-    for (int q = 0; q < P; ++q) pcnt[q] = 8 * nsel_of(q);
-    int q, r;
-    for (int j = lane; job_decode<P>(pcnt, j, q, r); j += 64) {
-      float* qb = pix(q);
-      const int* qm = (const int*)(qb + WC::MISC);
-      const int ns = qm[WC::M_NSEL];
-      const int i = r / ns, k = r % ns;
-      if (!qm[WC::M_FLAGS + i]) continue;
-      const int vj = ((const int*)(qb + WC::sel(nv)))[k];
-      const int cq = list[wbase + q];
-      const int qx = cq % W, qy = cq / W;
-      float* cp = qb + WC::cost(nv) + i * nv + vj;
-      const float gterm = gf * geom_cost_at(pc, B, qx, qy, vj + 1, geom_point(pc, qx, qy, ((const float4*)(qb + WC::CPL))[i]));
-      *cp = *cp + gterm;
-    }
-  }
-  wave_sync();
-#endif
   if (active) {
-#else
-  if (active) {
-    const int nj = (has_fit ? 2 : 1) * nsel;
-    for (int j = c; j < nj; j += C) {
-      const int h = j / nsel, k = j % nsel;
-      hv[h * nv + k] = hyp_val(sel_list[k] + 1, h ? fp : cur);
-    }
-#endif
     for (int i = c; i < 8; i += C) {
       const bool fl = misc[WC::M_FLAGS + i] != 0;
-#if DPE_WEAK_POOL && DPE_WEAK_GPOOL
-      float f = 0.0f;                                    // geometric terms already in cost (pool above)
-      for (int j = 0; j < nv; ++j) {
-        const int w = vwl[j];
-        if (w > 0) {
-          if (geom) {
-            if (fl) f += w * cost[i * nv + j];
-            else f += w * (cost[i * nv + j] + gf * 3.0f);
-#else
       const float3 fwi = (geom && fl) ? geom_point(pc, x, y, cpl[i]) : make_float3(0.0f, 0.0f, 0.0f);
       float f = 0.0f;
       for (int j = 0; j < nv; ++j) {
@@ -1418,7 +1148,6 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
           if (geom) {
             if (fl) f += w * (cost[i * nv + j] + gf * geom_cost_at(pc, B, x, y, j + 1, fwi));
             else f += w * (cost[i * nv + j] + gf * 3.0f);
-#endif
           } else {
             f += w * cost[i * nv + j];
           }
@@ -1434,7 +1163,6 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
   float4 pnow = cur;
   const float dmin = pc.P.depth_min, dmax = pc.P.depth_max;
   const float pert = (float)(0.02f * 3.14159265358979323846);
-#if DPE_WEAK_PRE
   // lanes 1..4 evaluate the refinement draws (refine_draws: stream words 15.. after the view
   // sampling) while lane 0 runs the acceptance; lane 0 then finishes the hypotheses from them
   float* rnd = pb + WC::RND;
@@ -1443,7 +1171,6 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
     if (c == 1) { rnd[0] = d.u_depth; rnd[1] = d.n[0]; rnd[2] = d.n[1]; rnd[3] = d.n[2]; rnd[4] = d.u_pert; }
     else refine_angle(rs, d.w_angles, c - 2, pert, &rnd[5 + 2 * (c - 2)], &rnd[6 + 2 * (c - 2)]);
   }
-#endif
   if (active && c == 0) {
     int mi = 0; float mcost = fc[0];
     for (int i = 1; i < 8; ++i) if (fc[i] <= mcost) { mcost = fc[i]; mi = i; }
@@ -1464,23 +1191,8 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
       tc /= wnorm;
       const float db = depth_from_plane(c0, fp, x, y);
       if (db >= dmin && db <= dmax && tc < cost_now) { depth_now = db; pnow = fp; cost_now = tc; }
-#if !DPE_WEAK_PRE
-      const float depth_rand = rng_uniform(rs) * (dmax - dmin) + dmin;
-      const float4 prand = random_normal(c0, x, y, rs, depth_now);
-      const float dminp = (1 - 0.02f) * depth_now, dmaxp = (1 + 0.02f) * depth_now;
-      const float depth_perturbed = rng_uniform(rs) * (dmaxp - dminp) + dminp;
-      const float4 ppert = perturbed_normal(c0, x, y, pnow, rs, pert);
-      float4 h0 = pnow, h1 = prand, h2 = prand, h3 = ppert, h4 = pnow;
-      h0.w = dist2origin(c0, x, y, depth_rand, h0);
-      h1.w = dist2origin(c0, x, y, depth_now, h1);
-      h2.w = dist2origin(c0, x, y, depth_rand, h2);
-      h3.w = dist2origin(c0, x, y, depth_now, h3);
-      h4.w = dist2origin(c0, x, y, depth_perturbed, h4);
-      hyp[0] = h0; hyp[1] = h1; hyp[2] = h2; hyp[3] = h3; hyp[4] = h4;
-#endif
     }
   }
-#if DPE_WEAK_PRE
   wave_sync();
   if (active && c == 0 && has_fit) {
     const float depth_rand = rnd[0] * (dmax - dmin) + dmin;
@@ -1496,11 +1208,9 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
     h4.w = dist2origin(c0, x, y, depth_perturbed, h4);
     hyp[0] = h0; hyp[1] = h1; hyp[2] = h2; hyp[3] = h3; hyp[4] = h4;
   }
-#endif
   wave_sync();
   PHASE(7);
   // ---- phase 5: refinement NCCs, jobs (hypothesis, selected view)
-#if DPE_WEAK_POOL
   {
 #pragma unroll
     for (int q = 0; q < P; ++q) pcnt[q] = fit_of(q) ? 5 * nsel_of(q) : 0;
@@ -1511,15 +1221,6 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
       const int h = r / ns, k = r % ns;
       const int v = ((const int*)(qb + WC::sel(nv)))[k] + 1;
       (qb + WC::hv(nv))[(2 + h) * nv + k] = hyp_val_q(q, v, ((const float4*)(qb + WC::HYP))[h]);
-    }
-  }
-  if (false) {
-#else
-  if (active && has_fit) {
-#endif
-    for (int j = c; j < 5 * nsel; j += C) {
-      const int h = j / nsel, k = j % nsel;
-      hv[(2 + h) * nv + k] = hyp_val(sel_list[k] + 1, hyp[h]);
     }
   }
   wave_sync();
@@ -1548,7 +1249,6 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
   wave_sync();
   PHASE(9);
   // ---- phase 6: the stored cost is the Old NCC of the final plane (DPE.cu:1845-1861)
-#if DPE_WEAK_POOL
   {
 #pragma unroll
     for (int q = 0; q < P; ++q) pcnt[q] = nsel_of(q);
@@ -1557,17 +1257,9 @@ __global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassCon
       float* qb = pix(q);
       const int cq = list[wbase + q];
       const int v = ((const int*)(qb + WC::sel(nv)))[r] + 1;
-      (qb + WC::hv(nv))[r] = ncc_old_any<U8, DPE_WEAK_OLD_ELIDE != 0, DPE_WEAK_ROW1 != 0>(fast_old, qb + WC::PW, qb[WC::OSUM], qb[WC::OSUM + 1], qb[WC::OSUM + 2], cq % W,
+      (qb + WC::hv(nv))[r] = ncc_old_any<U8, true>(fast_old, qb + WC::PW, qb[WC::OSUM], qb[WC::OSUM + 1], qb[WC::OSUM + 2], cq % W,
                                                    cq / W, pc, B, v, ((const float4*)(qb + WC::HYP))[5]);
     }
-  }
-  if (false) {
-#else
-  if (active) {
-#endif
-    const float4 fin = hyp[5];
-    for (int k = c; k < nsel; k += C)
-      hv[k] = ncc_old_any<U8, DPE_WEAK_OLD_ELIDE != 0, DPE_WEAK_ROW1 != 0>(fast_old, pw, osum[0], osum[1], osum[2], x, y, pc, B, sel_list[k] + 1, fin);
   }
   wave_sync();
   PHASE(10);

@@ -3,7 +3,7 @@
 // (-mllvm -amdgpu-sched-strategy=iterative-maxocc, see the Makefile).
 //
 // A scheduler is chosen per compilation, so the kernels that gain from it live here.  At the
-// 4 waves/SIMD of __launch_bounds__(256, DPE_TAP_WAVES) the default scheduler hoists the gathers of
+// 4 waves/SIMD of __launch_bounds__(256, kTapWaves) the default scheduler hoists the gathers of
 // the unrolled 36-tap loop until it needs more than 128 VGPRs and spills (strong 56, DepthToWeak
 // 68, LocalRefine 36 B/lane of scratch, whose stores reach HBM); the iterative scheduler fits the
 // same code in 106-110 VGPRs with no scratch.  Interleaved A/B on the bench pass (bit-identical
@@ -18,7 +18,7 @@ namespace dpe {
 
 void launch_strong(bool edge, bool img8, unsigned grid, size_t lds, hipStream_t s, const PassConst* dpc,
                    const DevBufs& B, int it, const int* list, const int* count) {
-  constexpr int T = 64 * DPE_BW_STRONG;
+  constexpr int T = 64 * kBwStrong;
   if (lds > 65536) {   // dynamic LDS beyond the default limit (gfx950 has 160 KB per CU)
     static bool once = false;
     if (!once) {
@@ -39,19 +39,18 @@ void launch_strong(bool edge, bool img8, unsigned grid, size_t lds, hipStream_t 
 }
 
 void launch_depth_to_weak(bool img8, long L, hipStream_t s, const PassConst* dpc, const DevBufs& B) {
-  const unsigned g = (unsigned)((L + DPE_BW_D2W - 1) / DPE_BW_D2W);
-  constexpr bool LR = DPE_FUSE_LR != 0;
-  if (img8) k_depth_to_weak<kTexD2W, LR><<<g, 64 * DPE_BW_D2W, 0, s>>>(dpc, B);
-  else k_depth_to_weak<TEX_F32, LR><<<g, 64 * DPE_BW_D2W, 0, s>>>(dpc, B);
+  const unsigned g = (unsigned)((L + kBwD2W - 1) / kBwD2W);
+  if (img8) k_depth_to_weak<kTexD2W, true><<<g, 64 * kBwD2W, 0, s>>>(dpc, B);
+  else k_depth_to_weak<TEX_F32, true><<<g, 64 * kBwD2W, 0, s>>>(dpc, B);
 }
 
 void launch_local_refine(bool img8, long L, int W, int H, int nv, hipStream_t s, const PassConst* dpc, const DevBufs& B) {
   // with the fused DepthToWeak only its border pixels are left
-  const int border = DPE_FUSE_LR ? 1 : 0;
-  if (border) L = border_count(W, H);
-  const unsigned g = (unsigned)((L + DPE_BW_LR * kLrPix - 1) / (DPE_BW_LR * kLrPix));
+  const int border = 1;
+  L = border_count(W, H);
+  const unsigned g = (unsigned)((L + kBwLR * kLrPix - 1) / (kBwLR * kLrPix));
   if (g == 0) return;
-  const size_t lds = (size_t)DPE_BW_LR * kLrPix * 12 * nv * 2 * sizeof(float);
+  const size_t lds = (size_t)kBwLR * kLrPix * 12 * nv * 2 * sizeof(float);
   if (lds > 65536) {
     static bool once = false;
     if (!once) {
@@ -60,8 +59,8 @@ void launch_local_refine(bool img8, long L, int W, int H, int nv, hipStream_t s,
       (void)hipFuncSetAttribute((const void*)k_local_refine_jobs<TEX_F32>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     }
   }
-  if (img8) k_local_refine_jobs<kTexLR><<<g, 64 * DPE_BW_LR, lds, s>>>(dpc, B, border);
-  else k_local_refine_jobs<TEX_F32><<<g, 64 * DPE_BW_LR, lds, s>>>(dpc, B, border);
+  if (img8) k_local_refine_jobs<kTexLR><<<g, 64 * kBwLR, lds, s>>>(dpc, B, border);
+  else k_local_refine_jobs<TEX_F32><<<g, 64 * kBwLR, lds, s>>>(dpc, B, border);
 }
 
 }  // namespace dpe

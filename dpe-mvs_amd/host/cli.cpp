@@ -67,6 +67,14 @@ int rccl_allgather_dev(void* user, const float* dsend, size_t count, float* drec
   return hipStreamSynchronize(r->stream) == hipSuccess ? 0 : -1;
 }
 
+// a failed collective on this rank: abort the communicator so that peers blocked in theirs fail
+// fast (dpe_abort_fn) instead of waiting for RCCL's timeout
+int rccl_abort(void* user) {
+  Rccl* r = static_cast<Rccl*>(user);
+  if (r->comm) { (void)ncclCommAbort(r->comm); r->comm = nullptr; }
+  return 0;
+}
+
 bool rccl_init(Rccl& r, int rank, int world, int device) {
   r.world = world;
   if (hipSetDevice(device) != hipSuccess) return false;
@@ -112,6 +120,8 @@ int main(int argc, char** argv) {
     o.allgather_user = &rccl;
     o.allgather_device = rccl_allgather_dev;   // the per-pass depth maps, HBM to HBM
     o.allgather_device_user = &rccl;
+    o.abort_collectives = rccl_abort;
+    o.abort_user = &rccl;
   }
   const int rc = dpe_run_pipeline(argv[1], &o);
   if (rc != 0) std::fprintf(stderr, "DPE pipeline failed: %s\n", dpe_pipeline_last_error());

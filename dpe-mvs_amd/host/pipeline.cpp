@@ -45,8 +45,10 @@ namespace {
 
 thread_local std::string g_err;
 const char* kOutName = "DPE";
-// wall seconds of the last run's phases: total, decode, GetProblemEdges pre-pass, passes, outputs + fusion
-double g_times[5] = {0, 0, 0, 0, 0};
+// wall seconds of the last run's phases: total, decode, GetProblemEdges pre-pass, passes (incl. the
+// exchanges), outputs + fusion, then (multi-rank) the depth exchanges alone and the pass work alone
+constexpr int kNumTimes = 7;
+double g_times[kNumTimes] = {0, 0, 0, 0, 0, 0, 0};
 double now_s() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
 
 struct Problem {   // main.h:108-118
@@ -462,6 +464,10 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
   bool failed = false;
   std::string first_err;
   auto fail = [&](const std::string& e) { if (!failed) { failed = true; first_err = e; } };
+  // A collective that fails on this rank may leave peers waiting in theirs: the optional abort hook
+  // (ncclCommAbort in bin/dpe) makes them fail fast instead of waiting for RCCL's timeout.  Without
+  // one (torch / gloo hooks from Python) the peers wait for their backend's own timeout.
+  auto abort_peers = [&]() { if (opt.abort_collectives) (void)opt.abort_collectives(opt.abort_user); };
   // all-gather of `per` floats per rank plus one status float; false (err set) when any rank failed
   auto exchange = [&](std::vector<float>& send, std::vector<float>& recv) -> bool {
     const size_t per = send.size();
@@ -469,6 +475,7 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
     recv.assign((per + 1) * world, 0.0f);
     if (opt.allgather(opt.allgather_user, send.data(), per + 1, recv.data()) != 0) {
       err = "all-gather failed";
+      abort_peers();
       return false;
     }
     send.pop_back();
@@ -489,14 +496,14 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
   auto status_exchange = [&]() -> bool {
     float flag = failed ? 1.0f : 0.0f;
     std::vector<float> all(world, 0.0f);
-    if (opt.allgather(opt.allgather_user, &flag, 1, all.data()) != 0) { err = "all-gather failed"; return false; }
+    if (opt.allgather(opt.allgather_user, &flag, 1, all.data()) != 0) { err = "all-gather failed"; abort_peers(); return false; }
     for (int r = 0; r < world; ++r)
       if (all[r] != 0.0f) { err = r == rank ? first_err : "rank " + std::to_string(r) + " failed"; return false; }
     return true;
   };
   // DPE_FAULT_INJECT="before:R" / "after:R" (tests): rank R fails locally just before / after the
-  // first resident depth exchange's collectives
-  static const std::pair<int, int> fault = [] {
+  // first resident depth exchange's collectives (read per run)
+  const std::pair<int, int> fault = [] {
     const char* e = std::getenv("DPE_FAULT_INJECT");
     if (!e) return std::make_pair(-1, -1);
     const std::string v(e);
@@ -573,8 +580,10 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
   std::map<int, DepthMap> depth_cur;
   int iteration_index = 0;
   const bool resident = runner.ctx != nullptr;
+  double t_pass = 0.0, t_xchg = 0.0;   // g_times[6] / [5]
   for (int i = 0; i < round_num; ++i) {
     for (int j = -1; j < 3; ++j) {
+      const double tp0 = now_s();
       if (resident && jacobi && !failed && dpe_state_snapshot(runner.ctx) != 0) fail(dpe_last_error());
       const std::map<int, DepthMap> snapshot = (jacobi && !resident) ? depth_cur : std::map<int, DepthMap>{};
       const auto& depth_src = jacobi ? snapshot : depth_cur;
@@ -604,6 +613,10 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
         }
       }
       if (world == 1 && failed) { err = first_err; return 1; }
+      // multi-rank: the pass round's GPU work is finished before the exchange's clock starts
+      if (world > 1 && resident && !failed && dpe_sync(runner.ctx) != 0) fail(dpe_last_error());
+      const double tx0 = now_s();
+      t_pass += tx0 - tp0;
       if (world > 1 && resident) {   // all-gather of the depth maps from / into the HBM-resident states
         // Two collectives per exchange, both joined by every rank whatever happened locally:
         //  1. the ranks' status flags over the host hook (one float each).  A local error before it
@@ -628,11 +641,19 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
         if (fault_at(0, rank)) fail("injected fault before the exchange");
         if (!status_exchange()) return 1;
         if (opt.allgather_device) {
-          if (opt.allgather_device(opt.allgather_device_user, dsend, cnt, drecv) != 0) { err = "all-gather failed"; return 1; }
+          if (opt.allgather_device(opt.allgather_device_user, dsend, cnt, drecv) != 0) {
+            err = "all-gather failed";
+            abort_peers();
+            return 1;
+          }
         } else {   // host hook: one device -> host -> device hop of the packed maps
           std::vector<float> hs(cnt, 0.0f), hr(cnt * world, 0.0f);
           if (dpe_device_copy(runner.ctx, hs.data(), dsend, cnt * sizeof(float), 1) != 0) fail(dpe_last_error());
-          if (opt.allgather(opt.allgather_user, hs.data(), cnt, hr.data()) != 0) { err = "all-gather failed"; return 1; }
+          if (opt.allgather(opt.allgather_user, hs.data(), cnt, hr.data()) != 0) {
+            err = "all-gather failed";
+            abort_peers();
+            return 1;
+          }
           if (!failed && dpe_device_copy(runner.ctx, drecv, hr.data(), hr.size() * sizeof(float), 0) != 0)
             fail(dpe_last_error());
         }
@@ -644,6 +665,7 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
                                                   drecv + (size_t)r * cnt + k * per, nullptr) != 0)
               fail(dpe_last_error());   // reported at the next exchange's status step
         }
+        if (!failed && dpe_sync(runner.ctx) != 0) fail(dpe_last_error());   // imports done: the exchange's end
       } else if (world > 1) {   // all-gather of the depth maps (the pass's only cross-image data)
         size_t nmax = 0;
         for (auto& b : blocks) nmax = std::max(nmax, b.size());
@@ -660,11 +682,14 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
             depth_cur[problems[blocks[r][k]].ref_image_id] = DepthMap{pw, ph, std::vector<float>(src, src + per)};
           }
       }
+      if (world > 1) t_xchg += now_s() - tx0;
       if (opt.verbose && rank == 0) std::cout << "Iteration " << iteration_index + 1 << " / " << round_num * 4 << " done" << std::endl;
       iteration_index++;
     }
   }
   g_times[3] = now_s() - t_mark;
+  g_times[5] = t_xchg;
+  g_times[6] = t_pass;
   t_mark = now_s();
   if (resident && !failed)   // the final states come back from HBM once
     for (int pi : blocks[rank]) {
@@ -829,7 +854,7 @@ const char* dpe_pipeline_last_error(void) { return dpe_host::g_err.c_str(); }
 
 int dpe_pipeline_last_timings(double* out, int n) {
   int k = 0;
-  for (; k < n && k < 5; ++k) out[k] = dpe_host::g_times[k];
+  for (; k < n && k < dpe_host::kNumTimes; ++k) out[k] = dpe_host::g_times[k];
   return k;
 }
 

@@ -11,6 +11,7 @@
 #include <unistd.h>
 
 #include <cerrno>
+#include <cstdio>
 #include <vector>
 
 #include <algorithm>
@@ -69,15 +70,38 @@ inline uint64_t run_token() {
   return h;
 }
 
-// Rank 0 listens on MASTER_ADDR and serves the id to each rank 1..world-1 once, after checking its
+// The address rank 0 listens on, given MASTER_ADDR (`addr`) and the address it resolved to
+// (`resolved`, host order).  Normally that address.  The one exception: MASTER_ADDR is a host NAME
+// (not a numeric literal, not "localhost") that resolves to a loopback address (/etc/hosts often
+// maps a host's own name to 127.0.1.1) while some ranks may run on other hosts (LOCAL_WORLD_SIZE
+// unset or below the world size): remote ranks could then never connect, so rank 0 listens on
+// every interface -- but only when the launcher gave the ranks DPE_RDZV_SECRET, which makes the
+// hello token a secret.  Without it the run token is built from non-secret values, so widening
+// would hand the communicator id to anyone on the network who guesses them: the listener stays on
+// loopback and a warning says why.  A numeric loopback literal or "localhost" never widens.
+inline uint32_t listen_addr(const char* addr, uint32_t resolved, int world, bool* warned = nullptr) {
+  if (warned) *warned = false;
+  if ((resolved >> 24) != 127) return resolved;
+  const char* lws = std::getenv("LOCAL_WORLD_SIZE");
+  if (lws && std::atoi(lws) >= world) return resolved;
+  in_addr tmp;
+  if (!addr || ::inet_pton(AF_INET, addr, &tmp) == 1 || std::strcmp(addr, "localhost") == 0) return resolved;
+  const char* sec = std::getenv("DPE_RDZV_SECRET");
+  if (!(sec && *sec)) {
+    if (warned) *warned = true;
+    std::fprintf(stderr, "dpe rendezvous: MASTER_ADDR %s resolves to a loopback address; remote ranks cannot reach it, "
+                         "and without DPE_RDZV_SECRET rank 0 does not listen on every interface\n", addr);
+    return resolved;
+  }
+  return INADDR_ANY;
+}
+
+// Rank 0 listens (listen_addr) and serves the id to each rank 1..world-1 once, after checking its
 // hello; connections that fail the check are dropped and do not use up a slot.  Pending connections
 // are served concurrently (poll), each with a 2 s budget for its hello, so connections that send
-// nothing cannot use up the 120 s window of the legitimate ranks.  If MASTER_ADDR resolves to a
-// loopback address while some ranks may run on other hosts (LOCAL_WORLD_SIZE unset or below the
-// world size; /etc/hosts often maps a host's own name to 127.0.1.1), rank 0 listens on every
-// interface instead (the hello check still filters peers).  The others connect (retrying for up to
-// 120 s while rank 0 starts).  Every socket call is bounded, so a missing peer ends in an error,
-// not a hang.
+// nothing cannot use up the 120 s window of the legitimate ranks.  The others connect (retrying for
+// up to 120 s while rank 0 starts).  Every socket call is bounded, so a missing peer ends in an
+// error, not a hang.
 inline bool exchange_blob(void* id, size_t id_bytes, int rank, int world) {
   const char* addr = std::getenv("MASTER_ADDR");
   const char* rp = std::getenv("DPE_RDZV_PORT");
@@ -100,9 +124,7 @@ inline bool exchange_blob(void* id, size_t id_bytes, int rank, int world) {
     sockaddr_in sa;
     std::memcpy(&sa, res->ai_addr, sizeof(sa));
     ::freeaddrinfo(res);
-    const char* lws = std::getenv("LOCAL_WORLD_SIZE");
-    const bool all_local = lws && std::atoi(lws) >= world;
-    if ((ntohl(sa.sin_addr.s_addr) >> 24) == 127 && !all_local) sa.sin_addr.s_addr = htonl(INADDR_ANY);
+    sa.sin_addr.s_addr = htonl(listen_addr(addr, ntohl(sa.sin_addr.s_addr), world));
     bool ok = ::bind(srv, (const sockaddr*)&sa, sizeof(sa)) == 0 && ::listen(srv, 64) == 0 &&
               ::fcntl(srv, F_SETFL, ::fcntl(srv, F_GETFL) | O_NONBLOCK) == 0;
     struct Pending { int fd; clock::time_point deadline; Hello h; size_t got; };

@@ -48,6 +48,9 @@ typedef int (*dpe_allgather_fn)(void* user, const float* send, size_t count, flo
  * returns once recv is complete.  With the default runner the depth maps then go from each rank's
  * HBM-resident state to the others' without a host copy. */
 typedef int (*dpe_allgather_dev_fn)(void* user, const float* dev_send, size_t count, float* dev_recv);
+/* Optional: called once when one of this rank's collectives failed, before dpe_run_pipeline returns,
+ * so that peers blocked in theirs fail fast (bin/dpe: ncclCommAbort).  Return value ignored. */
+typedef int (*dpe_abort_fn)(void* user);
 
 /* Fusion projection tests of one reference view: same contract as dpe_fusion_candidates
  * (include/dpe_mvs.h) over the given views (the default runs the HIP kernel on gpu_index). */
@@ -73,6 +76,7 @@ typedef struct DpePipelineOptions {
                                reference always runs its geometric passes, main.cpp:549) */
   dpe_allgather_dev_fn allgather_device; void* allgather_device_user;   /* optional (see above); with the
                                default runner it is used instead of `allgather` for the depth maps */
+  dpe_abort_fn abort_collectives; void* abort_user;   /* optional (see dpe_abort_fn) */
 } DpePipelineOptions;
 
 void dpe_pipeline_default_options(DpePipelineOptions* opt);
@@ -80,8 +84,10 @@ void dpe_pipeline_default_options(DpePipelineOptions* opt);
 int dpe_run_pipeline(const char* dense_folder, const DpePipelineOptions* opt);
 const char* dpe_pipeline_last_error(void);
 /* Wall seconds of the last successful dpe_run_pipeline on this process: [0] total, [1] image decode,
- * [2] the GetProblemEdges pre-pass (EdgeSegment), [3] the passes, [4] outputs + fusion.  Returns the
- * number of entries written (<= n, at most 5). */
+ * [2] the GetProblemEdges pre-pass (EdgeSegment), [3] the passes (with the depth exchanges),
+ * [4] outputs + fusion, [5] the depth exchanges alone (multi-rank: status all-gather, export,
+ * all-gather, import, summed over the pass rounds; 0 for one rank), [6] the pass work alone (each
+ * pass round up to its GPU work's end).  Returns the number of entries written (<= n, at most 7). */
 int dpe_pipeline_last_timings(double* out, int n);
 
 /* Grey-level decode of a JPEG (baseline/extended, luma plane) or binary PGM.  Writes up to `cap`

@@ -118,3 +118,26 @@ def test_shared_secret_authenticates(driver):
     assert mine.stdout.strip() == EXPECTED and r0_out.strip() == EXPECTED
     nosecret.kill()
     nosecret.wait()
+
+
+@pytest.mark.parametrize("addr,resolved,lws,secret,expect", [
+    ("127.0.0.1", "127.0.0.1", None, "s3", "127.0.0.1"),      # numeric loopback literal: never widened
+    ("localhost", "127.0.0.1", None, "s3", "127.0.0.1"),      # "localhost": never widened
+    ("node7", "127.0.1.1", None, None, "127.0.1.1"),          # hostname -> loopback, no secret: kept (warning)
+    ("node7", "127.0.1.1", None, "s3", "0.0.0.0"),            # hostname -> loopback, secret: every interface
+    ("node7", "127.0.1.1", "4", "s3", "127.0.1.1"),           # all ranks local: kept
+    ("node7", "10.1.2.3", None, "s3", "10.1.2.3"),            # a routable address: itself
+])
+def test_listen_address(driver, addr, resolved, lws, secret, expect):
+    """rank 0 widens its listener only for a host name that resolves to loopback, with ranks
+    off this host and DPE_RDZV_SECRET set (the only case where the hello token authenticates)."""
+    e = dict(os.environ)
+    for k in ("LOCAL_WORLD_SIZE", "DPE_RDZV_SECRET"):
+        e.pop(k, None)
+    if lws:
+        e["LOCAL_WORLD_SIZE"] = lws
+    if secret:
+        e["DPE_RDZV_SECRET"] = secret
+    out = subprocess.run([driver, "bind", addr, resolved, "4"], env=e, capture_output=True, text=True, check=True)
+    assert out.stdout.strip() == expect
+    assert ("DPE_RDZV_SECRET" in out.stderr) == (addr == "node7" and resolved.startswith("127.") and not secret and not lws)

@@ -1,5 +1,5 @@
 """Per-pixel / per-wave durations of the scratch-free GenNeighbours on the bench workload (a
--DDPE_GN_TIMES=1 build of libdpe_mvs.so): how long each WEAK pixel's probes and whole job take
+-DDPE_DIAG=8 build of libdpe_mvs.so): how long each WEAK pixel's probes and whole job take
 (shader clocks), and how long each wave lives (its slowest lane), to tell a few stragglers from a
 uniform load.  One timed, one-stream execute; prints quantiles.
 Usage: python tools/gn_times.py lib/variants/gntimes.so"""

@@ -1,4 +1,4 @@
-"""Gather locality of the tap kernels (a -DDPE_LINE_STATS=1 build of libdpe_mvs.so): distinct 128-B
+"""Gather locality of the tap kernels (a -DDPE_DIAG=2 build of libdpe_mvs.so): distinct 128-B
 lines per wave gather and the sum over lane quads of the lines each quad touches (the TA cost, tools/td_probe2.hip), per texel layout (P16: strong sweep; F16: DepthToWeak +
 LocalRefine + RandomInitialization; U8: weak sweep), one timed bench-workload pass.
 Usage: python tools/line_stats.py lib/variants/lstat.so"""

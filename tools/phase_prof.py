@@ -1,4 +1,4 @@
-"""Shader-clock phase sums of the cooperative kernels (a -DDPE_PHASE_PROF=1 build of libdpe_mvs.so):
+"""Shader-clock phase sums of the cooperative kernels (a -DDPE_DIAG=1 build of libdpe_mvs.so):
 one bench-workload pass, the library prints 'PHASE kernel.phase cycles share' lines to stderr.
 Usage: python tools/phase_prof.py lib/variants/phase.so"""
 import ctypes as C

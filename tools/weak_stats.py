@@ -1,4 +1,4 @@
-"""Weak-sweep path statistics (a -DDPE_WEAK_STATS=1 build of libdpe_mvs.so) over one bench-workload
+"""Weak-sweep path statistics (a -DDPE_DIAG=4 build of libdpe_mvs.so) over one bench-workload
 pass: centre-patch sides and paths of the NCC-New jobs, neighbour-patch paths, and the distinct
 centre-patch variants a wave executes one after another.
 Usage: python tools/weak_stats.py lib/variants/wstat.so"""
