@@ -163,6 +163,39 @@ def end_to_end(local_rank: int, n_images: int, W: int, H: int, scene=None) -> di
             "note": "dpe_mvs() wall clock incl. JPEG decode, EdgeSegment, host I/O; value is per-pass HBM-resident"}
 
 
+def coarse_level_pass(native, _abi, synthetic, local_rank: int, sp, W: int, H: int, nv: int = 10, reps: int = 3) -> dict:
+    """A coarse pyramid level of the schedule (main.cpp:494-501): the REFINE_ITER + geom pass at
+    (W/2) x (H/2), its images the host pipeline's INTER_LINEAR 1/2 downscale (DPE.cpp:798-809) of an
+    8-bit W x H rendering -- quarter-integer grey levels, i.e. the f16 texel layouts
+    (DPE_STAT_TEX_CLASS 1) -- with the cameras, priors and source depths of the same synthetic scene
+    rendered at (W/2) x (H/2).  Rate = pixels / wall time of one execute (timed after a warm-up)."""
+    import torch
+    from DPE_MVS import pipeline
+    w, h = W // 2, H // 2
+    full = synthetic.make_scene(W, H, nv)
+    sc = synthetic.make_scene(w, h, nv)
+    sc["images"] = [pipeline.resize_linear(im.astype(np.float32), w, h) for im in full["images"]]
+    del full
+    p = workload_params(_abi, nv)
+    p.max_scale_size = 2
+    inp = synthetic.pass_input(sc, p, depths=synthetic.src_depths(sc))
+    st = synthetic.gt_state(sc)
+    c = native.PatchMatchContext(local_rank)
+    try:
+        c.stage(inp, st)
+        cls = c.last_stat(_abi.DPE_STAT_TEX_CLASS)
+        c.execute(sp)                                   # warm-up
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):                           # each execute restarts from the staged state
+            c.execute(sp)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / reps
+    finally:
+        c.close()
+    return {"mpix_s": round(w * h / dt / 1e6, 4), "ms": round(dt * 1e3, 3), "tex_class": int(cls)}
+
+
 def pipeline_config4(dist, rank: int, world: int, local_rank: int, n: int = 16, W: int = 2688, H: int = 1792) -> dict:
     """BASELINE configs[3] at the pipeline level: 16 reference images at 2688x1792 (ETH3D high-res
     size, 9 source views each) through DPE_MVS.run_dpe_pipeline -- decode, EdgeSegment, the full
@@ -394,6 +427,11 @@ def main():
             exec_s += time.perf_counter() - t1
         ck.close()
         per_type[kind] = round(2 * Wd * Hd / exec_s / 1e6, 4)
+    # the coarse pyramid levels (configs 2/3 at 800x600, config 4 at 1344x896), f16 texel layouts
+    levels = {}
+    if not args.no_pass_types:
+        for (Wl, Hl) in ((Wd, Hd), (2688, 1792)):
+            levels[f"{Wl // 2}x{Hl // 2}"] = coarse_level_pass(native, _abi, synthetic, local_rank, sp, Wl, Hl)
     dom = max(("strong", "weak", "depth_to_weak", "local_refine", "init", "ransac", "setup"), key=lambda k: tim.get(k, 0.0))
     launches = max(1, cnt[dom]["launches"])
     flop_per_launch = algorithmic_flops(cnt[dom]) / launches
@@ -459,6 +497,7 @@ def main():
         "stage_ms": round(stage_ms, 3),
         "pcie_inclusive_mpix_s": round(Wd * Hd / ((stage_ms + ms_per_step) * 1e-3) / 1e6, 4),
         "pass_types_mpix_s": per_type,
+        "pass_levels": levels,
         "kernel_ms": {k: round(v, 3) for k, v in tim.items()},
         "work": {k: v for k, v in cnt.items() if v["launches"]},
     }

@@ -18,6 +18,7 @@ WEAK, STRONG, UNKNOWN = 0, 1, 2                          # main.h:72-76 PixelSta
 DPE_OK = 0
 DPE_OPT_GN_SLOTS = 1          # dpe_set_option: GenNeighbours support-point slots (include/dpe_mvs.h)
 DPE_STAT_GN_DEFERRED = 1      # dpe_pm_last_stat: WEAK pixels handed to the scratch GenNeighbours
+DPE_STAT_TEX_CLASS = 2        # dpe_pm_last_stat: 2 u8 / f16 texels, 1 f16 (quarter-integer grey levels), 0 f32
 
 
 class DpeCamera(C.Structure):

@@ -97,9 +97,21 @@ DEV float d_rcp_fast(float z) {
   const float r = __builtin_amdgcn_rcpf(z);
   return __builtin_fmaf(__builtin_fmaf(-z, r, 1.0f), r, r);
 }
-template <bool FAST> DEV float rcp_sel(float z) {
-  if constexpr (FAST) return d_rcp_fast(z);
-  else return 1.0f / z;
+// The tap reciprocal (restatement choice 8): the hardware's v_rcp_f32 for every
+// denominator whose biased exponent is in [1, 252] (results normal; the result is a function of
+// the mantissa alone there, within 1 ulp of 1/z, and the oracle carries its table), IEEE 1.0f / z
+// otherwise (zero, denormals, |z| >= 2^126, inf, NaN).  The reference divides under
+// --use_fast_math (CMakeLists.txt:72), itself an approximate reciprocal (DPE.cu:515-522).
+// FAST: the caller has checked the range for the whole patch (rcp_range_ok), so no per-tap test.
+DEV float rcp_model(float z) {
+  const uint32_t e = (__float_as_uint(z) >> 23) & 0xFFu;
+  float r = __builtin_amdgcn_rcpf(z);
+  if (__builtin_expect(e - 1u >= 252u, 0)) r = 1.0f / z;   // rare: a branch, not a select
+  return r;
+}
+template <bool FAST> DEV float rcp_tap(float z) {
+  if constexpr (FAST) return __builtin_amdgcn_rcpf(z);
+  else return rcp_model(z);
 }
 DEV float d_rsqrtf(float x) { return 1.0f / __builtin_sqrtf(x); }
 

@@ -72,7 +72,7 @@ struct DevArr {
 // layouts built from them.
 struct CachedImage {
   int id = 0, W = 0, H = 0;
-  bool is8 = false;
+  int cls = IMG_F32;          // ImgClass of the grey levels
   DevArr<float> plain;
   DevArr<uint32_t> q8;      // TEX_U8 quad texels (8-bit images)
   DevArr<uint2> q16;        // TEX_F16 quad texels (8-bit images)
@@ -135,7 +135,7 @@ struct DpeContext {
   DevArr<uint32_t> imgq8_all;        // all 8-bit quad images, TEX_U8 layout, one allocation
   DevArr<uint2> imgq16_all;          //   and TEX_F16 layout (32-bit tap offsets)
   DevArr<uint32_t> imgqp_all;        //   and TEX_P16 column pairs
-  bool img8 = false;                 // all images are 8-bit grey levels -> u8 quad layout
+  int img_cls = IMG_F32;             // ImgClass of the pass (the widest class of its views)
   DevArr<float> depth[DPE_MAX_IMAGES];
   DevArr<uint8_t> edge, edge_low;
   DevArr<int> label;
@@ -354,6 +354,12 @@ struct StageSrc {
 };
 static int stage_impl(DpeContext* c, const DpePassInput* in, const StageSrc& src);
 
+#if DPE_POOL_STATS
+extern "C" void dpe_dbg_pool_stats_main(unsigned long long out[24], int reset) {
+  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(dpe::g_pool), sizeof(dpe::g_pool));
+  if (reset) { unsigned long long z[24] = {}; (void)hipMemcpyToSymbol(HIP_SYMBOL(dpe::g_pool), z, sizeof(z)); }
+}
+#endif
 #if DPE_LINE_STATS
 extern "C" void dpe_dbg_line_stats_main(unsigned long long out[16], int reset) {
   (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(dpe::g_lstat), sizeof(dpe::g_lstat));
@@ -467,14 +473,21 @@ static int stage_impl(DpeContext* c, const DpePassInput* in, const StageSrc& src
   DevBufs& B = c->bufs;
   std::memset(&B, 0, sizeof(B));
   const dim3 qb(16, 16), qg((W + 2 + 15) / 16, (H + 2 + 15) / 16);
-  // u8 layout when every grey level is an integer in [0, 255] (images decoded from 8-bit files;
-  // a rescaled pyramid level is not): identical sample values, a quarter of the gather bytes
-  auto all_8bit = [&](const float* im) {
+  // The half-precision layouts hold every grey level exactly when it is a multiple of 1/4 in
+  // [0, 255] (IMG_Q: the exact 1/2 and 1/4 INTER_LINEAR downscales of an 8-bit image, the coarse
+  // pyramid levels of every BASELINE config; the differences b - a of the F16 / P16 texels are then
+  // exact too); the u8 layout needs integers (IMG_U8: images decoded from 8-bit files).  Identical
+  // sample values in every layout; the smaller ones gather fewer bytes.
+  auto image_class = [&](const float* im) -> int {
+    bool integer = true;
     for (size_t k = 0; k < L; ++k) {
       const float v = im[k];
-      if (!(v >= 0.0f && v <= 255.0f) || v != (float)(int)v) return false;
+      if (!(v >= 0.0f && v <= 255.0f)) return IMG_F32;
+      const float v4 = v * 4.0f;   // exact (power of two)
+      if (v4 != (float)(int)v4) return IMG_F32;
+      integer = integer && v == (float)(int)v;
     }
-    return true;
+    return integer ? IMG_U8 : IMG_Q;
   };
   const size_t plane = (size_t)(W + 2) * (H + 2);
   const size_t pplane = (size_t)(W + 3) * (H + 2);        // TEX_P16
@@ -500,13 +513,14 @@ static int stage_impl(DpeContext* c, const DpePassInput* in, const StageSrc& src
         }
         e = new CachedImage();
         e->id = in->image_ids[i]; e->W = W; e->H = H;
-        e->is8 = all_8bit(in->images[i]);
+        e->cls = image_class(in->images[i]);
         c->icache.push_back(e);
         HIPC(e->plain.ensure(L));
         HIPC(hipMemcpyAsync(e->plain.p, in->images[i], L * sizeof(float), hipMemcpyHostToDevice, c->stream));
-        if (e->is8) {
-          HIPC(e->q8.ensure(plane)); HIPC(e->q16.ensure(plane)); HIPC(e->qp.ensure(pplane));
-          k_build_quad8<<<qg, qb, 0, c->stream>>>(e->plain.p, e->q8.p, e->q16.p, W, H);
+        if (e->cls != IMG_F32) {
+          if (e->cls == IMG_U8) HIPC(e->q8.ensure(plane));
+          HIPC(e->q16.ensure(plane)); HIPC(e->qp.ensure(pplane));
+          k_build_quad8<<<qg, qb, 0, c->stream>>>(e->plain.p, e->cls == IMG_U8 ? e->q8.p : nullptr, e->q16.p, W, H);
           k_build_pair16<<<pg, qb, 0, c->stream>>>(e->plain.p, e->qp.p, W, H);
           HIPC(hipGetLastError());
         }
@@ -514,19 +528,20 @@ static int stage_impl(DpeContext* c, const DpePassInput* in, const StageSrc& src
       e->last_use = ++c->icache_clock;
       ent[i] = e;
     }
-    bool img8 = (size_t)(W + 2) * (H + 2) * 8 * N < (1ull << 32);
-    for (int i = 0; i < N; ++i) img8 = img8 && ent[i]->is8;
-    c->img8 = img8;
-    if (img8) {
-      HIPC(c->imgq8_all.ensure(plane * N));
+    int cls = (size_t)(W + 2) * (H + 2) * 8 * N < (1ull << 32) ? IMG_U8 : IMG_F32;   // 32-bit tap offsets
+    for (int i = 0; i < N; ++i) cls = std::min(cls, ent[i]->cls);
+    c->img_cls = cls;
+    if (cls != IMG_F32) {
+      if (cls == IMG_U8) HIPC(c->imgq8_all.ensure(plane * N));
       HIPC(c->imgq16_all.ensure(plane * N));
       HIPC(c->imgqp_all.ensure(pplane * N));
       for (int i = 0; i < N; ++i) {   // the per-pass views in one allocation (32-bit tap offsets)
-        HIPC(hipMemcpyAsync(c->imgq8_all.p + plane * i, ent[i]->q8.p, plane * 4, hipMemcpyDeviceToDevice, c->stream));
+        if (cls == IMG_U8)
+          HIPC(hipMemcpyAsync(c->imgq8_all.p + plane * i, ent[i]->q8.p, plane * 4, hipMemcpyDeviceToDevice, c->stream));
         HIPC(hipMemcpyAsync(c->imgq16_all.p + plane * i, ent[i]->q16.p, plane * 8, hipMemcpyDeviceToDevice, c->stream));
         HIPC(hipMemcpyAsync(c->imgqp_all.p + pplane * i, ent[i]->qp.p, pplane * 4, hipMemcpyDeviceToDevice, c->stream));
       }
-      B.img8 = (const uint8_t*)c->imgq8_all.p; B.img8_view = (uint32_t)(plane * 4);
+      if (cls == IMG_U8) { B.img8 = (const uint8_t*)c->imgq8_all.p; B.img8_view = (uint32_t)(plane * 4); }
       B.img16 = (const uint8_t*)c->imgq16_all.p; B.img16_view = (uint32_t)(plane * 8);
       B.imgp = (const uint8_t*)c->imgqp_all.p; B.imgp_view = (uint32_t)(pplane * 4);
     } else {
@@ -541,22 +556,24 @@ static int stage_impl(DpeContext* c, const DpePassInput* in, const StageSrc& src
     }
     B.ref = ent[0]->plain.p;
   }
-  bool img8 = !in->image_ids;
-  for (int i = 0; i < N && img8 && !in->image_ids; ++i) img8 = all_8bit(in->images[i]);
-  if ((size_t)(W + 2) * (H + 2) * 8 * N >= (1ull << 32)) img8 = false;   // 32-bit tap offsets
-  if (!in->image_ids) c->img8 = img8;
+  int cls = IMG_U8;
+  for (int i = 0; i < N && cls != IMG_F32 && !in->image_ids; ++i) cls = std::min(cls, image_class(in->images[i]));
+  if ((size_t)(W + 2) * (H + 2) * 8 * N >= (1ull << 32)) cls = IMG_F32;   // 32-bit tap offsets
+  if (!in->image_ids) c->img_cls = cls;
   for (int i = 0; i < N && !in->image_ids; ++i) {
     HIPC(c->img_plain[i].ensure(L));
     HIPC(hipMemcpyAsync(c->img_plain[i].p, in->images[i], L * sizeof(float), hipMemcpyHostToDevice, c->stream));
-    if (img8) {
-      HIPC(c->imgq8_all.ensure(plane * N));
+    if (cls != IMG_F32) {
+      if (cls == IMG_U8) HIPC(c->imgq8_all.ensure(plane * N));
       HIPC(c->imgq16_all.ensure(plane * N));
       HIPC(c->imgqp_all.ensure(pplane * N));
-      k_build_quad8<<<qg, qb, 0, c->stream>>>(c->img_plain[i].p, c->imgq8_all.p + plane * i,
+      k_build_quad8<<<qg, qb, 0, c->stream>>>(c->img_plain[i].p, cls == IMG_U8 ? c->imgq8_all.p + plane * i : nullptr,
                                               c->imgq16_all.p + plane * i, W, H);
       k_build_pair16<<<pg, qb, 0, c->stream>>>(c->img_plain[i].p, c->imgqp_all.p + pplane * i, W, H);
-      B.img8 = (const uint8_t*)c->imgq8_all.p;
-      B.img8_view = (uint32_t)(plane * 4);
+      if (cls == IMG_U8) {
+        B.img8 = (const uint8_t*)c->imgq8_all.p;
+        B.img8_view = (uint32_t)(plane * 4);
+      }
       B.img16 = (const uint8_t*)c->imgq16_all.p;
       B.img16_view = (uint32_t)(plane * 8);
       B.imgp = (const uint8_t*)c->imgqp_all.p;
@@ -788,7 +805,7 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   }
   end();
   Bc = begin(DPE_CLASS_INIT);
-  if (c->img8) k_random_init<kTexInit><<<fg, fb, 0, s>>>(dpc, Bc); else k_random_init<TEX_F32><<<fg, fb, 0, s>>>(dpc, Bc);
+  if (c->img_cls != IMG_F32) k_random_init<kTexInit><<<fg, fb, 0, s>>>(dpc, Bc); else k_random_init<TEX_F32><<<fg, fb, 0, s>>>(dpc, Bc);
   end();
   if (overlap) HIPC(hipStreamWaitEvent(s, c->ev_ei, 0));   // the strong sweeps read GenEdgeInform's rays
   HIPC(hipGetLastError());
@@ -797,7 +814,7 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
     const int P = edge ? 4 : 8, C = edge ? 16 : 8;
     const size_t lds = (size_t)kBwStrong * strong_lds_per_wave(P, C, nv) * sizeof(float);
     const unsigned grid = (unsigned)((L / 2 + 1 + kBwStrong * P - 1) / (kBwStrong * P));
-    launch_strong(edge, c->img8, grid, lds, s, dpc, Bs, it, lst, cnt);
+    launch_strong(edge, c->img_cls, grid, lds, s, dpc, Bs, it, lst, cnt);
   };
   for (int it = 0; it < pc.P.max_iterations; ++it) {
     for (int colour = 0; colour < 2; ++colour) {
@@ -844,7 +861,9 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
         const size_t per_wave = (size_t)P * weak_lds_per_pixel(nv) * sizeof(float);
         const int wpb = per_wave * 4 <= 64 * 1024 ? 4 : (per_wave * 2 <= 64 * 1024 ? 2 : 1);
         const unsigned grid = (unsigned)((L / 2 + 1 + wpb * P - 1) / (wpb * P));
-        if (c->img8) k_weak_coop<kTexWeak, C><<<grid, 64 * wpb, per_wave * wpb, sw>>>(dpc, Bc, it, lst, cnt);
+        // U8 texels for 8-bit images; F16 (exact for quarter-integer grey levels) for the coarse levels
+        if (c->img_cls == IMG_U8) k_weak_coop<kTexWeak, C><<<grid, 64 * wpb, per_wave * wpb, sw>>>(dpc, Bc, it, lst, cnt);
+        else if (c->img_cls == IMG_Q) k_weak_coop<TEX_F16, C><<<grid, 64 * wpb, per_wave * wpb, sw>>>(dpc, Bc, it, lst, cnt);
         else k_weak_coop<TEX_F32, C><<<grid, 64 * wpb, per_wave * wpb, sw>>>(dpc, Bc, it, lst, cnt);
       }
       end();
@@ -860,10 +879,10 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   for (int colour = 0; colour < 2; ++colour) k_filter<<<hg, hb, 0, s>>>(dpc, Bc, colour);   // hb: 32 x 4 = kFilterThreads
   end();
   Bc = begin(DPE_CLASS_DEPTH_TO_WEAK);
-  launch_depth_to_weak(c->img8, (long)L, s, dpc, Bc);
+  launch_depth_to_weak(c->img_cls, (long)L, s, dpc, Bc);
   end();
   Bc = begin(DPE_CLASS_LOCAL_REFINE);
-  launch_local_refine(c->img8, (long)L, W, H, nv, s, dpc, Bc);
+  launch_local_refine(c->img_cls, (long)L, W, H, nv, s, dpc, Bc);
   end();
   HIPC(hipGetLastError());
   if (slot_overflow) {   // per-class times would silently miss launches
@@ -1352,6 +1371,7 @@ extern "C" int dpe_set_option(DpeContext* c, int option, int value) {
 }
 
 extern "C" long long dpe_pm_last_stat(DpeContext* c, int stat) {
+  if (c && c->staged && stat == DPE_STAT_TEX_CLASS) return c->img_cls;
   if (!c || !c->staged || stat != DPE_STAT_GN_DEFERRED || !c->list_totals.p) return -1;
   int v = 0;   // waits for this context's pass only (not the whole device)
   if (hipSetDevice(c->device) != hipSuccess || wait_pending(c) != hipSuccess || hipStreamSynchronize(c->aux) != hipSuccess ||

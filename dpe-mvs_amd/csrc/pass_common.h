@@ -66,9 +66,11 @@ struct DevBufs {
 //   2  gather-line statistics of the fast tap loops (tools/line_stats.py)
 //   4  weak-sweep path statistics (tools/weak_stats.py)
 //   8  GenNeighbours per-pixel clocks and counts (tools/gn_times.py)
+//  16  job-pool statistics of the cooperative kernels (tools/pool_stats.py)
 #ifndef DPE_DIAG
 #define DPE_DIAG 0
 #endif
+#define DPE_POOL_STATS (((DPE_DIAG) >> 4) & 1)
 #define DPE_PHASE_PROF ((DPE_DIAG) & 1)
 #define DPE_LINE_STATS (((DPE_DIAG) >> 1) & 1)
 #define DPE_WEAK_STATS (((DPE_DIAG) >> 2) & 1)
@@ -102,6 +104,25 @@ struct DevBufs {
 #define PHASE(k) do {} while (0)
 #define PHASE_END(kernel) do {} while (0)
 #define PHASE_END_ALL(kernel) do {} while (0)
+#endif
+// Job-pool statistics (DPE_DIAG & 16): per pool, the jobs dealt, the 64-lane rounds they take and
+// the waves (utilisation = jobs / (64 rounds)); pools: 0 strong cost vectors, 1 strong refinement,
+// 2 weak candidates, 3 weak current / fit plane, 4 weak refinement, 5 weak final Old NCC.
+#if DPE_POOL_STATS
+static __device__ unsigned long long g_pool[8][3];
+DEV void pool_stat(int k, int jobs) {
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(&g_pool[k][0], (unsigned long long)jobs);
+    atomicAdd(&g_pool[k][1], (unsigned long long)((jobs + 63) / 64));
+    atomicAdd(&g_pool[k][2], 1ull);
+  }
+}
+#define POOL_STAT(k, n) pool_stat(k, n)
+// Old NCC patches read from LDS (ncc_old_lds): all, and those whose reciprocal range check failed
+#define PATCH_STAT(ok) do { atomicAdd(&g_pool[6][0], 1ull); if (!(ok)) atomicAdd(&g_pool[6][1], 1ull); } while (0)
+#else
+#define POOL_STAT(k, n) do {} while (0)
+#define PATCH_STAT(ok) do {} while (0)
 #endif
 DEV void count_work(const DevBufs& B, unsigned long long ncc, unsigned long long taps) {
   if (B.cnt) { atomicAdd(B.cnt + 0, ncc); atomicAdd(B.cnt + 1, taps); }
@@ -510,7 +531,7 @@ template <int T>
 DEV float tap_u8_fast(const DevBufs& B, uint32_t vadj, uint32_t stride, f2v tmax, const float* h, f2v bxy, float bz,
                       float yf) {
   const f2v q = fma2((f2v){h[1], h[4]}, f2s(yf), bxy);
-  const float iz = d_rcp_fast(__builtin_fmaf(h[7], yf, bz));
+  const float iz = rcp_tap<true>(__builtin_fmaf(h[7], yf, bz));
   const f2v t = fma2(q, f2s(iz), f2s(kTexMagic + kTexUnit));
   const float ctx = tex_t_fast(t.x, tmax.x), cty = tex_t_fast(t.y, tmax.y);
   const uint32_t ux = __float_as_uint(ctx), uy = __float_as_uint(cty);
@@ -540,8 +561,7 @@ DEV f2v tap2_at(const uint8_t* base, uint32_t vadj, uint32_t stride, f2v tmax, c
   const f2v qx = fma2(f2s(h[1]), yf, f2s(bxy.x));
   const f2v qy = fma2(f2s(h[4]), yf, f2s(bxy.y));
   const f2v qz = fma2(f2s(h[7]), yf, f2s(bz));
-  const f2v r = (f2v){__builtin_amdgcn_rcpf(qz.x), __builtin_amdgcn_rcpf(qz.y)};
-  const f2v iz = fma2(fma2(-qz, r, f2s(1.0f)), r, r);
+  const f2v iz = (f2v){rcp_tap<true>(qz.x), rcp_tap<true>(qz.y)};
   const f2v tx = fma2(qx, iz, f2s(kTexMagic + kTexUnit)), ty = fma2(qy, iz, f2s(kTexMagic + kTexUnit));
   const float cx0 = tex_t_fast(tx.x, tmax.x), cx1 = tex_t_fast(tx.y, tmax.x);
   const float cy0 = tex_t_fast(ty.x, tmax.y), cy1 = tex_t_fast(ty.y, tmax.y);
@@ -630,7 +650,7 @@ DEV void generic_taps(const PassConst& pc, const DevBufs& B, int v, const Homog&
       const float yf = (float)y;
       const float qx = __builtin_fmaf(H.h[1], yf, bx);
       const float qy = __builtin_fmaf(H.h[4], yf, by);
-      const float iz = rcp_sel<FAST>(__builtin_fmaf(H.h[7], yf, bz));
+      const float iz = rcp_tap<FAST>(__builtin_fmaf(H.h[7], yf, bz));
       const float sp = sample_src<U8>(B, v, W, Hh, qx, qy, iz);
       const float w = bilateral_weight(i, j, rp, rcp, ss, sc);
       const float wr = w * rp;
@@ -719,7 +739,7 @@ DEV void make_patch36(Patch36& P, const PassConst& pc, const DevBufs& B, int px,
   }
   P.s_ref = s_ref; P.s_rr = s_rr; P.s_w = s_w;
 }
-template <int U8, bool FAST>
+template <int U8>
 DEV void patch36_taps(const Patch36& P, const PassConst& pc, const DevBufs& B, int v, const Homog& H0, float* acc) {
   const int W = pc.W, Hh = pc.H;
   const Homog H = scale_cols(H0);
@@ -736,7 +756,7 @@ DEV void patch36_taps(const Patch36& P, const PassConst& pc, const DevBufs& B, i
       const float y = (float)(P.py - 5 + 2 * b);
       const float qx = __builtin_fmaf(H.h[1], y, bx);
       const float qy = __builtin_fmaf(H.h[4], y, by);
-      const float iz = rcp_sel<FAST>(__builtin_fmaf(H.h[7], y, bz));
+      const float iz = rcp_tap<true>(__builtin_fmaf(H.h[7], y, bz));
       const float sp = sample_src<U8>(B, v, W, Hh, qx, qy, iz);
       const float w = P.w[a * 6 + b], wr = P.wr[a * 6 + b];
       r_src = __builtin_fmaf(w, sp, r_src);
@@ -754,10 +774,17 @@ DEV float ncc_old_patch36(const Patch36& P, const PassConst& pc, const DevBufs& 
   if (center_outside(pc, v, H, P.px, P.py)) { count_work(B, 1, 0); return 2.0f; }
   count_work(B, 1, 36);
   float a[3];
-  if (rcp_range_ok(H, (float)(P.px - 5), (float)(P.px + 5), (float)(P.py - 5), (float)(P.py + 5)))
-    patch36_taps<U8, true>(P, pc, B, v, H, a);
-  else
-    patch36_taps<U8, false>(P, pc, B, v, H, a);
+  if (rcp_range_ok(H, (float)(P.px - 5), (float)(P.px + 5), (float)(P.py - 5), (float)(P.py + 5))) {
+    patch36_taps<U8>(P, pc, B, v, H, a);
+  } else {
+    // the rare slow patch (per-tap reciprocal range test) through the rolled generic loop: the same
+    // weights (bilateral_weight of the same texels) summed in the same order, so the same bits, and
+    // the cached patch's 75 registers stay out of an unrolled slow loop (random init at occupancy 2)
+    float g[6];
+    generic_taps<U8, false>(pc, B, v, H, P.px, P.py, ref_texel(B.ref, pc.W, pc.H, P.px, P.py), pc.P.strong_radius,
+                            pc.P.strong_increment, g);
+    a[0] = g[2]; a[1] = g[3]; a[2] = g[4];
+  }
   return ncc_finalize(P.s_ref, P.s_rr, P.s_w, a[0], a[1], a[2]);
 }
 

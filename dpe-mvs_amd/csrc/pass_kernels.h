@@ -1137,7 +1137,8 @@ __global__ void __launch_bounds__(kFilterThreads) k_filter(const PassConst* __re
 }
 
 // ------------------------------------------------------------------------------ staging kernels
-// padded quad-texel images of 8-bit grey levels, both layouts (pass_common.h: TEX_U8, TEX_F16)
+// padded quad-texel images of 8-bit (or quarter-integer: q8 == nullptr) grey levels, both layouts
+// (pass_common.h: TEX_U8, TEX_F16)
 __global__ void k_build_quad8(const float* __restrict__ img, uint32_t* __restrict__ q8, uint2* __restrict__ q16,
                               int W, int H) {
   const int X = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1147,7 +1148,7 @@ __global__ void k_build_quad8(const float* __restrict__ img, uint32_t* __restric
   const int x0 = cl(X - 1, W), x1 = cl(X, W), y0 = cl(Y - 1, H), y1 = cl(Y, H);
   const float a = img[y0 * W + x0], b = img[y0 * W + x1], c = img[y1 * W + x0], d = img[y1 * W + x1];
   const size_t o = (size_t)Y * (W + 2) + X;
-  q8[o] = (uint32_t)a | ((uint32_t)b << 8) | ((uint32_t)c << 16) | ((uint32_t)d << 24);
+  if (q8) q8[o] = (uint32_t)a | ((uint32_t)b << 8) | ((uint32_t)c << 16) | ((uint32_t)d << 24);
   const h2v lo = (h2v){(_Float16)a, (_Float16)c};
   const h2v df = (h2v){(_Float16)(b - a), (_Float16)(d - c)};
   q16[o] = make_uint2(__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, df));

@@ -96,69 +96,47 @@ DEV void taps36_at(const float* pw, int px, int py, f2v tmax, const uint8_t* bas
     }
     acc[0] = s_sr.x; acc[1] = s_ss; acc[2] = s_sr.y;
 }
-// row a of the generic (scalar) tap loop of lds_taps, added to the running sums in row order
+// Old NCC with the patch read from LDS (same arithmetic as ncc_old_patch36).  FAST: the caller has
+// checked the reciprocal range for the whole patch (rcp_range_ok).  A slow patch (rare: 2316 of
+// 1.3e9 on the bench workload, profiles/r05d_pool_stats.log) goes through the rolled generic loop,
+// which sums the same weights (bilateral_weight of the same texels) in the same order, so the same
+// bits, and keeps an unrolled per-tap-tested loop out of every caller's register budget.
 template <int U8, bool FAST>
-DEV void lds_taps_row(const float* pw, int px, int py, const PassConst& pc, const DevBufs& B, int v, const Homog& H, int a,
-                      float& s_src, float& s_ss, float& s_rs) {
-  const float x = (float)(px - 5 + 2 * a);
-  const float bx = __builtin_fmaf(H.h[0], x, H.h[2]) * kTexUnit;
-  const float by = __builtin_fmaf(H.h[3], x, H.h[5]) * kTexUnit;
-  const float bz = __builtin_fmaf(H.h[6], x, H.h[8]);
-  float r_src = 0, r_ss = 0, r_rs = 0;
-#pragma unroll
-  for (int b = 0; b < 6; ++b) {
-    const float y = (float)(py - 5 + 2 * b);
-    const float qx = __builtin_fmaf(H.h[1], y, bx);
-    const float qy = __builtin_fmaf(H.h[4], y, by);
-    const float iz = rcp_sel<FAST>(__builtin_fmaf(H.h[7], y, bz));
-    const float sp = sample_src<U8>(B, v, pc.W, pc.H, qx, qy, iz);
-    const float w = pw[2 * (a * 6 + b)], wr = pw[2 * (a * 6 + b) + 1];
-    r_src = __builtin_fmaf(w, sp, r_src);
-    const float ws = w * sp;
-    r_ss = __builtin_fmaf(ws, sp, r_ss);
-    r_rs = __builtin_fmaf(wr, sp, r_rs);
-  }
-  s_src += r_src; s_ss += r_ss; s_rs += r_rs;
-}
-// Old NCC with the patch read from LDS (same arithmetic as ncc_old_patch36).  ROW1: the slow loop
-// (!FAST: a patch whose reciprocal range check failed) unrolled one row at a time, which lowers the
-// caller's register peak (same operations, same order)
-template <int U8, bool FAST, bool ROW1 = false>
 DEV void lds_taps(const float* pw, int px, int py, const PassConst& pc, const DevBufs& B, int v, const Homog& H0,
                   float* acc) {
   const int W = pc.W, Hh = pc.H;
   if constexpr (U8 != TEX_F32 && FAST) {
     taps36_at<U8>(pw, px, py, tex_tmax2(W, Hh), tex_base<U8>(B), (uint32_t)v * tex_view<U8>(B),
                       tex_stride<U8>(W), H0, acc);
+  } else if constexpr (!FAST) {
+    float g[6];
+    generic_taps<U8, false>(pc, B, v, H0, px, py, ref_texel(B.ref, W, Hh, px, py), pc.P.strong_radius,
+                            pc.P.strong_increment, g);
+    acc[0] = g[2]; acc[1] = g[3]; acc[2] = g[4];
   } else {
     const Homog H = scale_cols(H0);
     float s_src = 0, s_ss = 0, s_rs = 0;
-    if constexpr (ROW1) {
-#pragma unroll 1
-      for (int a = 0; a < 6; ++a) lds_taps_row<U8, FAST>(pw, px, py, pc, B, v, H, a, s_src, s_ss, s_rs);
-    } else {
 #pragma unroll
-      for (int a = 0; a < 6; ++a) {
-        const float x = (float)(px - 5 + 2 * a);
-        const float bx = __builtin_fmaf(H.h[0], x, H.h[2]) * kTexUnit;
-        const float by = __builtin_fmaf(H.h[3], x, H.h[5]) * kTexUnit;
-        const float bz = __builtin_fmaf(H.h[6], x, H.h[8]);
-        float r_src = 0, r_ss = 0, r_rs = 0;
+    for (int a = 0; a < 6; ++a) {
+      const float x = (float)(px - 5 + 2 * a);
+      const float bx = __builtin_fmaf(H.h[0], x, H.h[2]) * kTexUnit;
+      const float by = __builtin_fmaf(H.h[3], x, H.h[5]) * kTexUnit;
+      const float bz = __builtin_fmaf(H.h[6], x, H.h[8]);
+      float r_src = 0, r_ss = 0, r_rs = 0;
 #pragma unroll
-        for (int b = 0; b < 6; ++b) {
-          const float y = (float)(py - 5 + 2 * b);
-          const float qx = __builtin_fmaf(H.h[1], y, bx);
-          const float qy = __builtin_fmaf(H.h[4], y, by);
-          const float iz = rcp_sel<FAST>(__builtin_fmaf(H.h[7], y, bz));
-          const float sp = sample_src<U8>(B, v, W, Hh, qx, qy, iz);
-          const float w = pw[2 * (a * 6 + b)], wr = pw[2 * (a * 6 + b) + 1];
-          r_src = __builtin_fmaf(w, sp, r_src);
-          const float ws = w * sp;
-          r_ss = __builtin_fmaf(ws, sp, r_ss);
-          r_rs = __builtin_fmaf(wr, sp, r_rs);
-        }
-        s_src += r_src; s_ss += r_ss; s_rs += r_rs;
+      for (int b = 0; b < 6; ++b) {
+        const float y = (float)(py - 5 + 2 * b);
+        const float qx = __builtin_fmaf(H.h[1], y, bx);
+        const float qy = __builtin_fmaf(H.h[4], y, by);
+        const float iz = rcp_tap<true>(__builtin_fmaf(H.h[7], y, bz));
+        const float sp = sample_src<U8>(B, v, W, Hh, qx, qy, iz);
+        const float w = pw[2 * (a * 6 + b)], wr = pw[2 * (a * 6 + b) + 1];
+        r_src = __builtin_fmaf(w, sp, r_src);
+        const float ws = w * sp;
+        r_ss = __builtin_fmaf(ws, sp, r_ss);
+        r_rs = __builtin_fmaf(wr, sp, r_rs);
       }
+      s_src += r_src; s_ss += r_ss; s_rs += r_rs;
     }
     acc[0] = s_src; acc[1] = s_ss; acc[2] = s_rs;
   }
@@ -202,7 +180,7 @@ DEV void lds_row(const float* pw, int px, int py, const PassConst& pc, const Dev
       const float y = (float)(py - 5 + 2 * b);
       const float qx = __builtin_fmaf(H.h[1], y, bx);
       const float qy = __builtin_fmaf(H.h[4], y, by);
-      const float iz = rcp_sel<FAST>(__builtin_fmaf(H.h[7], y, bz));
+      const float iz = rcp_tap<FAST>(__builtin_fmaf(H.h[7], y, bz));
       const float sp = sample_src<U8>(B, v, W, Hh, qx, qy, iz);
       const float w = pw[2 * (a * 6 + b)], wr = pw[2 * (a * 6 + b) + 1];
       r_src = __builtin_fmaf(w, sp, r_src);
@@ -213,26 +191,26 @@ DEV void lds_row(const float* pw, int px, int py, const PassConst& pc, const Dev
     r3[0] = r_src; r3[1] = r_ss; r3[2] = r_rs;
   }
 }
-template <int U8, bool ROW1 = false>
+template <int U8>
 DEV float ncc_old_lds(const float* pw, float s_ref, float s_rr, float s_w, int px, int py, const PassConst& pc,
                       const DevBufs& B, int v, const float4& pl) {
   const Homog H = make_homography(pc, v, pl);
   if (center_outside(pc, v, H, px, py)) { count_work(B, 1, 0); return 2.0f; }
   count_work(B, 1, 36);
   float a[3];
-  if (rcp_range_ok(H, (float)(px - 5), (float)(px + 5), (float)(py - 5), (float)(py + 5))) {
+  const bool ok = rcp_range_ok(H, (float)(px - 5), (float)(px + 5), (float)(py - 5), (float)(py + 5));
+  PATCH_STAT(ok);
+  if (ok) {
     lds_taps<U8, true>(pw, px, py, pc, B, v, H, a);
   } else
-    lds_taps<U8, false, ROW1>(pw, px, py, pc, B, v, H, a);
+    lds_taps<U8, false>(pw, px, py, pc, B, v, H, a);
   return ncc_finalize_pre(s_ref, s_rr, s_w, a[0], a[1], a[2]);   // (inv, mref, var_ref) of patch_lds_pre
 }
 
-// ROW1: the rare slow tap loop (clamped taps, IEEE reciprocal) one patch row at a time, which
-// lowers the caller's register peak (DepthToWeak, the weak sweep's final Old NCC)
-template <int U8, bool ROW1 = false>
+template <int U8>
 DEV float ncc_old_any(bool fast, const float* pw, float s_ref, float s_rr, float s_w, int px, int py,
                       const PassConst& pc, const DevBufs& B, int v, const float4& pl) {
-  if (fast) return ncc_old_lds<U8, ROW1>(pw, s_ref, s_rr, s_w, px, py, pc, B, v, pl);
+  if (fast) return ncc_old_lds<U8>(pw, s_ref, s_rr, s_w, px, py, pc, B, v, pl);
   return ncc_old_generic<U8>(pc, B, px, py, v, pl);
 }
 
@@ -366,7 +344,7 @@ __global__ void __launch_bounds__(64 * kBwD2W, kTapWaves) k_depth_to_weak(const 
         const int vi = si - 1;
         if (isSet(sel, vi)) {
           float tcst = 0.0f;
-          const float c = ncc_old_any<U8, true>(fast, pw, s_ref, s_rr, s_w, x, y, pc, B, si, tp);
+          const float c = ncc_old_any<U8>(fast, pw, s_ref, s_rr, s_w, x, y, pc, B, si, tp);
           tcst += c;
           PHASE(1);
           if constexpr (LR) lr += (c * vw[vi]);                       // DPE.cu:2820

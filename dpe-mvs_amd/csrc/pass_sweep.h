@@ -440,6 +440,7 @@ __global__ void __launch_bounds__(64 * kBwStrong, kTapWaves) k_strong_coop(const
     // a last round with at most kTailJobs jobs: each job's 6 patch rows go to 64 / tail lanes (rows
     // per lane 1 or 2), the row sums meet in LDS, and one lane per job adds them in row order
     const bool split = fast && tail > 0 && tail <= kTailJobs;
+    POOL_STAT(0, total);
     const int jend = split ? total - tail : total;
     for (int j = lane; j < jend; j += 64) {
       job_decode<P>(cnt, j % S, q, r);
@@ -640,6 +641,7 @@ __global__ void __launch_bounds__(64 * kBwStrong, kTapWaves) k_strong_coop(const
     int cnt[P];
 #pragma unroll
     for (int q = 0; q < P; ++q) cnt[q] = 5 * ib_all[q * ibs + SC::IB_MISC];
+    POOL_STAT(1, [&] { int t = 0; for (int q = 0; q < P; ++q) t += cnt[q]; return t; }());
     int q, r;
     for (int j = lane; job_decode<P>(cnt, j, q, r); j += 64) {
       const int* iq = ib_all + q * ibs;
@@ -744,7 +746,7 @@ DEV void tab_taps(const PassConst& pc, const DevBufs& B, int v, const Homog& H0,
         const float yf = (float)(cy - rad + b * inc);
         const float qx = __builtin_fmaf(H.h[1], yf, bx);
         const float qy = __builtin_fmaf(H.h[4], yf, by);
-        const float iz = rcp_sel<FAST>(__builtin_fmaf(H.h[7], yf, bz));
+        const float iz = rcp_tap<FAST>(__builtin_fmaf(H.h[7], yf, bz));
         const float sp = sample_src<U8>(B, v, W, Hh, qx, qy, iz);
         const f2v w = wp[a * n + b];
         r_src = __builtin_fmaf(w.x, sp, r_src);
@@ -1057,6 +1059,7 @@ __global__ void __launch_bounds__(256, kTapWaves) k_weak_coop(const PassConst* _
       Sj += pcnt[q];
     }
     int q, r;
+    POOL_STAT(2, Sj * nv);
     // view-major: the lanes of one round gather from the same source images
     for (int j = lane; j < Sj * nv; j += 64) {
       job_decode<P>(pcnt, j % Sj, q, r);
@@ -1128,6 +1131,7 @@ __global__ void __launch_bounds__(256, kTapWaves) k_weak_coop(const PassConst* _
   {
 #pragma unroll
     for (int q = 0; q < P; ++q) pcnt[q] = (fit_of(q) ? 2 : 1) * nsel_of(q);
+    POOL_STAT(3, [&] { int t = 0; for (int q = 0; q < P; ++q) t += pcnt[q]; return t; }());
     int q, r;
     for (int j = lane; job_decode<P>(pcnt, j, q, r); j += 64) {
       float* qb = pix(q);
@@ -1137,6 +1141,7 @@ __global__ void __launch_bounds__(256, kTapWaves) k_weak_coop(const PassConst* _
       (qb + WC::hv(nv))[h * nv + k] = hyp_val_q(q, v, h ? ((const float4*)(qb + WC::HYP))[6] : B.planes[list[wbase + q]]);
     }
   }
+  PHASE(12);   // (phase 6 from here: the final candidate costs)
   if (active) {
     for (int i = c; i < 8; i += C) {
       const bool fl = misc[WC::M_FLAGS + i] != 0;
@@ -1214,6 +1219,7 @@ __global__ void __launch_bounds__(256, kTapWaves) k_weak_coop(const PassConst* _
   {
 #pragma unroll
     for (int q = 0; q < P; ++q) pcnt[q] = fit_of(q) ? 5 * nsel_of(q) : 0;
+    POOL_STAT(4, [&] { int t = 0; for (int q = 0; q < P; ++q) t += pcnt[q]; return t; }());
     int q, r;
     for (int j = lane; job_decode<P>(pcnt, j, q, r); j += 64) {
       float* qb = pix(q);
@@ -1252,12 +1258,13 @@ __global__ void __launch_bounds__(256, kTapWaves) k_weak_coop(const PassConst* _
   {
 #pragma unroll
     for (int q = 0; q < P; ++q) pcnt[q] = nsel_of(q);
+    POOL_STAT(5, [&] { int t = 0; for (int q = 0; q < P; ++q) t += pcnt[q]; return t; }());
     int q, r;
     for (int j = lane; job_decode<P>(pcnt, j, q, r); j += 64) {
       float* qb = pix(q);
       const int cq = list[wbase + q];
       const int v = ((const int*)(qb + WC::sel(nv)))[r] + 1;
-      (qb + WC::hv(nv))[r] = ncc_old_any<U8, true>(fast_old, qb + WC::PW, qb[WC::OSUM], qb[WC::OSUM + 1], qb[WC::OSUM + 2], cq % W,
+      (qb + WC::hv(nv))[r] = ncc_old_any<U8>(fast_old, qb + WC::PW, qb[WC::OSUM], qb[WC::OSUM + 1], qb[WC::OSUM + 2], cq % W,
                                                    cq / W, pc, B, v, ((const float4*)(qb + WC::HYP))[5]);
     }
   }

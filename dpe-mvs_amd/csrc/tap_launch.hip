@@ -16,7 +16,7 @@
 
 namespace dpe {
 
-void launch_strong(bool edge, bool img8, unsigned grid, size_t lds, hipStream_t s, const PassConst* dpc,
+void launch_strong(bool edge, int cls, unsigned grid, size_t lds, hipStream_t s, const PassConst* dpc,
                    const DevBufs& B, int it, const int* list, const int* count) {
   constexpr int T = 64 * kBwStrong;
   if (lds > 65536) {   // dynamic LDS beyond the default limit (gfx950 has 160 KB per CU)
@@ -30,21 +30,21 @@ void launch_strong(bool edge, bool img8, unsigned grid, size_t lds, hipStream_t 
     }
   }
   if (edge) {
-    if (img8) k_strong_coop<kTexStrong, true><<<grid, T, lds, s>>>(dpc, B, it, list, count);
+    if (cls != IMG_F32) k_strong_coop<kTexStrong, true><<<grid, T, lds, s>>>(dpc, B, it, list, count);
     else k_strong_coop<TEX_F32, true><<<grid, T, lds, s>>>(dpc, B, it, list, count);
   } else {
-    if (img8) k_strong_coop<kTexStrong, false><<<grid, T, lds, s>>>(dpc, B, it, list, count);
+    if (cls != IMG_F32) k_strong_coop<kTexStrong, false><<<grid, T, lds, s>>>(dpc, B, it, list, count);
     else k_strong_coop<TEX_F32, false><<<grid, T, lds, s>>>(dpc, B, it, list, count);
   }
 }
 
-void launch_depth_to_weak(bool img8, long L, hipStream_t s, const PassConst* dpc, const DevBufs& B) {
+void launch_depth_to_weak(int cls, long L, hipStream_t s, const PassConst* dpc, const DevBufs& B) {
   const unsigned g = (unsigned)((L + kBwD2W - 1) / kBwD2W);
-  if (img8) k_depth_to_weak<kTexD2W, true><<<g, 64 * kBwD2W, 0, s>>>(dpc, B);
+  if (cls != IMG_F32) k_depth_to_weak<kTexD2W, true><<<g, 64 * kBwD2W, 0, s>>>(dpc, B);
   else k_depth_to_weak<TEX_F32, true><<<g, 64 * kBwD2W, 0, s>>>(dpc, B);
 }
 
-void launch_local_refine(bool img8, long L, int W, int H, int nv, hipStream_t s, const PassConst* dpc, const DevBufs& B) {
+void launch_local_refine(int cls, long L, int W, int H, int nv, hipStream_t s, const PassConst* dpc, const DevBufs& B) {
   // with the fused DepthToWeak only its border pixels are left
   const int border = 1;
   L = border_count(W, H);
@@ -59,12 +59,18 @@ void launch_local_refine(bool img8, long L, int W, int H, int nv, hipStream_t s,
       (void)hipFuncSetAttribute((const void*)k_local_refine_jobs<TEX_F32>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     }
   }
-  if (img8) k_local_refine_jobs<kTexLR><<<g, 64 * kBwLR, lds, s>>>(dpc, B, border);
+  if (cls != IMG_F32) k_local_refine_jobs<kTexLR><<<g, 64 * kBwLR, lds, s>>>(dpc, B, border);
   else k_local_refine_jobs<TEX_F32><<<g, 64 * kBwLR, lds, s>>>(dpc, B, border);
 }
 
 }  // namespace dpe
 
+#if DPE_POOL_STATS
+extern "C" void dpe_dbg_pool_stats_tap(unsigned long long out[24], int reset) {
+  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(dpe::g_pool), sizeof(dpe::g_pool));
+  if (reset) { unsigned long long z[24] = {}; (void)hipMemcpyToSymbol(HIP_SYMBOL(dpe::g_pool), z, sizeof(z)); }
+}
+#endif
 #if DPE_LINE_STATS
 extern "C" void dpe_dbg_line_stats_tap(unsigned long long out[16], int reset) {
   (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(dpe::g_lstat), sizeof(dpe::g_lstat));

@@ -278,9 +278,12 @@ int dpe_pm_last_counts(DpeContext* ctx, unsigned long long* out, int n);
  *   kernel).  Results are the same for every setting.
  * DPE_STAT_GN_DEFERRED: WEAK pixels the scratch-free GenNeighbours of the last execute handed to the
  *   scratch kernel (more points than slots, or a NaN in its sorts).  Synchronises with the pass.
+ * DPE_STAT_TEX_CLASS: texel layouts of the staged images: 2 = every grey level an integer in
+ *   [0, 255] (u8 / f16 texels), 1 = every grey level a multiple of 1/4 in [0, 255] (the exact 1/2
+ *   and 1/4 downscales of the coarse pyramid levels: f16 texels), 0 = f32 texels.
  * dpe_set_option returns DPE_OK or DPE_ERR_ARG; dpe_pm_last_stat returns the value or -1. */
 enum { DPE_OPT_GN_SLOTS = 1 };
-enum { DPE_STAT_GN_DEFERRED = 1 };
+enum { DPE_STAT_GN_DEFERRED = 1, DPE_STAT_TEX_CLASS = 2 };
 int dpe_set_option(DpeContext* ctx, int option, int value);
 long long dpe_pm_last_stat(DpeContext* ctx, int stat);
 

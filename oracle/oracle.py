@@ -37,6 +37,8 @@ def _load(path: str = LIB):
     lib.oracle_last_error.restype = C.c_char_p
     lib.oracle_ncc_old.argtypes = [C.POINTER(_abi.DpePassInput), C.c_int, C.c_int, C.c_int, C.POINTER(C.c_float)]
     lib.oracle_ncc_old.restype = C.c_float
+    lib.oracle_rcp_tap.argtypes = [C.c_void_p, C.c_void_p, C.c_long]
+    lib.oracle_rcp_tap.restype = None
     lib.oracle_expf.argtypes = [C.c_float]
     lib.oracle_expf.restype = C.c_float
     lib.oracle_sinf.argtypes = [C.c_float]

@@ -18,11 +18,12 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 from DPE_MVS import _abi, synthetic  # noqa: E402
 import oracle  # noqa: E402
 
+# v5 (round 5): restatement choice 8, the tap reciprocal as gfx950's v_rcp_f32 (oracle_math.h)
 CASES = {
     # name: (W, H, num_images, pass kind)
-    "first_init_64x48_v3": (64, 48, 3, "first"),
-    "refine_init_64x48_v3": (64, 48, 3, "refine_init"),
-    "refine_iter_geom_80x60_v4": (80, 60, 4, "refine_iter"),
+    "first_init_64x48_v5": (64, 48, 3, "first"),
+    "refine_init_64x48_v5": (64, 48, 3, "refine_init"),
+    "refine_iter_geom_80x60_v5": (80, 60, 4, "refine_iter"),
 }
 
 

@@ -186,13 +186,33 @@ def test_error_paths(ctx):
 
 
 def test_gpu_non_integer_images(ctx):
-    # rescaled pyramid levels are not 8-bit integers: exercises the f32 quad-texel layout
+    # grey levels that are not multiples of 1/4: exercises the f32 quad-texel layout
     sc = synthetic.make_scene(96, 72, 4)
     sc["images"] = [(im * np.float32(0.73) + np.float32(0.31)).astype(np.float32) for im in sc["images"]]
     p = _params("refine_iter")
     st = synthetic.gt_state(sc)
     inp = synthetic.pass_input(sc, p, depths=synthetic.src_depths(sc))
     assert_same(ctx.run(inp, st), oracle.run_pass(inp, st), "f32 images")
+    assert ctx.last_stat(_abi.DPE_STAT_TEX_CLASS) == 0
+
+
+@pytest.mark.parametrize("kind", ["refine_iter", "refine_init", "first"])
+def test_gpu_quarter_integer_images(ctx, kind):
+    """A coarse pyramid level: the host pipeline's INTER_LINEAR 1/2 downscale (DPE.cpp:798-809) of 8-bit
+    images has grey levels in multiples of 1/4, which the f16 texel layouts hold exactly (strong sweep
+    P16, DepthToWeak / LocalRefine / init F16, weak sweep F16 instead of U8): bit-exact vs the oracle."""
+    from DPE_MVS import pipeline
+    full = synthetic.make_scene(192, 144, 4)
+    sc = synthetic.make_scene(96, 72, 4)
+    sc["images"] = [pipeline.resize_linear(im.astype(np.float32), 96, 72) for im in full["images"]]
+    q = np.concatenate([im.ravel() for im in sc["images"]])
+    assert np.all(q * 4 == np.round(q * 4)) and not np.all(q == np.round(q))   # quarter-integers, not 8-bit
+    p = _params(kind)
+    st = synthetic.first_init_state(sc) if kind == "first" else synthetic.gt_state(sc)
+    depths = synthetic.src_depths(sc) if p.geom_consistency else None
+    inp = synthetic.pass_input(sc, p, depths=depths)
+    assert_same(ctx.run(inp, st), oracle.run_pass(inp, st), f"quarter-integer images ({kind})")
+    assert ctx.last_stat(_abi.DPE_STAT_TEX_CLASS) == 1
 
 
 def test_image_ids_keep_images_resident(ctx):

@@ -18,7 +18,7 @@ def test_oracle_reproduces_golden(name):
 
 
 def test_thread_count_invariance():
-    inp, st, _ = load("refine_iter_geom_80x60_v4")
+    inp, st, _ = load("refine_iter_geom_80x60_v5")
     a = oracle.run_pass(inp, st, threads=1)
     b = oracle.run_pass(inp, st, threads=7)
     for k in a:
@@ -26,7 +26,7 @@ def test_thread_count_invariance():
 
 
 def test_seed_changes_result_salt_too():
-    inp, st, _ = load("first_init_64x48_v3")
+    inp, st, _ = load("first_init_64x48_v5")
     a = oracle.run_pass(inp, st)
     inp["seed"] = 99
     b = oracle.run_pass(inp, st)
@@ -48,7 +48,7 @@ def test_first_init_reconstructs_scene():
 
 
 def test_refine_keeps_depth_in_range_and_classifies():
-    inp, st, _ = load("refine_iter_geom_80x60_v4")
+    inp, st, _ = load("refine_iter_geom_80x60_v5")
     out = oracle.run_pass(inp, st)
     classes = set(np.unique(out["weak"]).tolist())
     assert classes <= {0, 1, 2} and _abi.STRONG in classes
