@@ -154,6 +154,7 @@ struct DpeContext {
   DevArr<int> gn_ovf;                // GenNeighbours pixels left to the scratch kernel (k_gen_neighbours_lds)
   DevArr<float> gn_tab;              // normalised image coordinates per column / row (k_gn_tables)
   DevArr<int> lists, row_counts, list_totals;   // per-colour pixel lists for the sweeps
+  DevArr<int> part_cnt;                          // per colour: chunk counts / offsets of the weak-list partition
   DevBufs bufs;
   // fusion (dpe_fusion_stage / dpe_fusion_candidates)
   std::vector<DevArr<float>> fz_depth, fz_normal;
@@ -282,7 +283,7 @@ void dpe_destroy(DpeContext* c) {
   c->e_ftab.release(); c->e_stab.release();
   c->cnt.release();
   c->tab_right.release(); c->tab_down.release(); c->gn_ovf.release(); c->gn_tab.release();
-  c->lists.release(); c->row_counts.release(); c->list_totals.release();
+  c->lists.release(); c->row_counts.release(); c->list_totals.release(); c->part_cnt.release();
   (void)hipStreamSynchronize(c->aux);
   (void)hipEventDestroy(c->ev_fork); (void)hipEventDestroy(c->ev_join); (void)hipEventDestroy(c->ev_ei);
   (void)hipStreamDestroy(c->aux);
@@ -645,6 +646,7 @@ static int stage_impl(DpeContext* c, const DpePassInput* in, const StageSrc& src
   HIPC(c->tab_right.ensure(L)); HIPC(c->tab_down.ensure(L));
   HIPC(c->gn_ovf.ensure(L + 64)); HIPC(c->gn_tab.ensure((size_t)W + H));
   HIPC(c->lists.ensure(6 * (L / 2 + 64) + 3 * (L + 64))); HIPC(c->row_counts.ensure(4 * (size_t)H + 4)); HIPC(c->list_totals.ensure(16));
+  HIPC(c->part_cnt.ensure(2 * ((L / 2 + 1) / kPartChunk + 2)));
   B.planes = c->planes.p; B.planes_snap = c->planes_snap.p; B.fit_plane = c->fit_plane.p;
   B.planes0 = c->planes0.p;
   B.costs = c->costs.p; B.costs_snap = c->costs_snap.p; B.complex_ = c->complex_.p;
@@ -745,6 +747,7 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   const long list_stride = (long)(L / 2 + 64);
   int* weak_list = c->lists.p + 4 * list_stride;     // all WEAK pixels (list_totals slot 4)
   int* failed_list = weak_list + L + 64;             // colour-0 pixels whose GenNeighbours failed (slot 5)
+  int* side_lists = failed_list + list_stride;       // per colour: the weak list partitioned by patch side
   // The whole setup chain (GenEdgeInform, FindNearestStrongPoint's tables, the WEAK list,
   // GenNeighbours, NeigbourUpdate) runs on the aux stream `a`, forked at the start of the pass beside
   // RandomInitialization; the first strong half-sweep waits for GenEdgeInform's edge rays only.
@@ -857,6 +860,15 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
         const hipStream_t sw = colour == 1 ? a : s;
         const int* lst = c->lists.p + (colour * 2 + 1) * list_stride;
         const int* cnt = c->list_totals.p + colour * 2 + 1;
+        if (pc.P.use_radius) {   // the fits just set the radii: partition the list by centre-patch side
+          const unsigned pg = (unsigned)((L / 2 + 1 + kPartChunk - 1) / kPartChunk);
+          int* pcnt = c->part_cnt.p + colour * (pg + 2);
+          int* out = side_lists + colour * list_stride;
+          k_part_count<<<pg, 256, 0, sw>>>(dpc, Bc, lst, cnt, pcnt);
+          k_part_scan<<<1, 256, 0, sw>>>(cnt, pcnt, c->list_totals.p + 8 + colour);
+          k_part_fill<<<pg, 256, 0, sw>>>(dpc, Bc, lst, cnt, pcnt, c->list_totals.p + 8 + colour, out);
+          lst = out;
+        }
         constexpr int C = kWeakLanes, P = 64 / C;
         const size_t per_wave = (size_t)P * weak_lds_per_pixel(nv) * sizeof(float);
         const int wpb = per_wave * 4 <= 64 * 1024 ? 4 : (per_wave * 2 <= 64 * 1024 ? 2 : 1);

@@ -97,6 +97,92 @@ __global__ void k_list_fill(const PassConst* __restrict__ pcp, DevBufs B, const 
   }
 }
 
+// ------------------------------------------------------------------------------ weak list by patch side
+// The weak sweep's NCC-New cost runs the pixel's centre patch at side n_c (6 at radius >= 5, 1 at the
+// radius RANSACToGetFitPlane sets to 0; DPE.cu:1120-1212, 557-690), and a wave runs the sides of its
+// pixels one after the other.  After the fits, each colour's weak list is stably partitioned into
+// side >= 4 then side < 4 pixels (chunks of kPartChunk entries: count, scan, fill), so almost every
+// wave holds one side.  Pixels of a half-sweep are independent, so the order changes no result.
+constexpr int kPartChunk = 1024;
+DEV int weak_side(const PassConst& pc, const DevBufs& B, int center) {
+  const int rad = B.radius[center], inc = MAXo(2, d2i(2.0 * rad / 5.0));
+  return rad >= 0 ? (2 * rad) / inc + 1 : 0;
+}
+DEV int part_key(const PassConst& pc, const DevBufs& B, int center) { return weak_side(pc, B, center) >= 4 ? 1 : 0; }
+DEV int block_sum256(int v, int* s4) {   // sum over a 256-thread block (all threads call it)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if ((threadIdx.x & 63) == 0) s4[threadIdx.x >> 6] = v;
+  __syncthreads();
+  const int t = s4[0] + s4[1] + s4[2] + s4[3];
+  __syncthreads();
+  return t;
+}
+static __global__ void __launch_bounds__(256) k_part_count(const PassConst* __restrict__ pcp, DevBufs B, const int* __restrict__ list,
+                                                    const int* __restrict__ nlist_p, int* __restrict__ chunk_cnt) {
+  const PassConst& pc = *pcp;
+  const int n = *nlist_p, base = blockIdx.x * kPartChunk;
+  if (base >= n) return;   // block-uniform
+  __shared__ int s4[4];
+  int cnt = 0;
+  for (int i = base + (int)threadIdx.x; i < min(n, base + kPartChunk); i += 256) cnt += part_key(pc, B, list[i]);
+  cnt = block_sum256(cnt, s4);
+  if (threadIdx.x == 0) chunk_cnt[blockIdx.x] = cnt;
+}
+// exclusive scan of the chunk counts (one 256-thread block); total side->=4 count into *tot
+static __global__ void __launch_bounds__(256) k_part_scan(const int* __restrict__ nlist_p, int* __restrict__ chunk_cnt,
+                                                   int* __restrict__ tot) {
+  __shared__ int s4[4];
+  const int nch = (*nlist_p + kPartChunk - 1) / kPartChunk;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int acc = 0;
+  for (int k0 = 0; k0 < nch; k0 += 256) {
+    const int k = k0 + (int)threadIdx.x;
+    const int c = k < nch ? chunk_cnt[k] : 0;
+    int incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int t = __shfl_up(incl, o);
+      if (lane >= o) incl += t;
+    }
+    if (lane == 63) s4[wave] = incl;
+    __syncthreads();
+    int before = acc;
+    for (int w = 0; w < wave; ++w) before += s4[w];
+    const int all = s4[0] + s4[1] + s4[2] + s4[3];
+    __syncthreads();
+    if (k < nch) chunk_cnt[k] = before + incl - c;
+    acc += all;
+  }
+  if (threadIdx.x == 0) *tot = acc;
+}
+static __global__ void __launch_bounds__(256) k_part_fill(const PassConst* __restrict__ pcp, DevBufs B, const int* __restrict__ list,
+                                                   const int* __restrict__ nlist_p, const int* __restrict__ chunk_off,
+                                                   const int* __restrict__ tot, int* __restrict__ out) {
+  const PassConst& pc = *pcp;
+  const int n = *nlist_p, base = blockIdx.x * kPartChunk;
+  if (base >= n) return;
+  __shared__ int s4[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int offA = chunk_off[blockIdx.x], offB = *tot + (base - offA);
+  const unsigned long long below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  int runA = 0;   // side->=4 entries of this chunk before the current step
+  for (int i0 = base; i0 < min(n, base + kPartChunk); i0 += 256) {
+    const int i = i0 + (int)threadIdx.x;
+    const int p = i < n ? list[i] : 0;
+    const int k = i < n ? part_key(pc, B, p) : 0;
+    const unsigned long long m = __ballot(k == 1);
+    if (lane == 0) s4[wave] = __popcll(m);
+    __syncthreads();
+    int a = runA + __popcll(m & below);
+    for (int w = 0; w < wave; ++w) a += s4[w];
+    const int all = s4[0] + s4[1] + s4[2] + s4[3];
+    __syncthreads();
+    if (i < n) out[k ? offA + a : offB + (i - base) - a] = p;
+    runA += all;
+  }
+}
+
 // ------------------------------------------------------------------------------ view selection
 // sampling probability of view i before the prior (DPE.cu:1568-1589), costs by candidate j.
 template <class CostF>
