@@ -96,6 +96,7 @@ struct WeakCarveT {
   static constexpr int OSUM = 352;      // [3] Old-NCC patch sums
   static constexpr int CPL = 356;       // [8] float4 candidate planes
   static constexpr int HYP = 388;       // [7] float4 refinement hypotheses; [5] final plane, [6] fit plane
+  static constexpr int RSUM = HYP;      // phases 1-1b: [6][3] row sums of the centre patch (over HYP)
   static constexpr int FC = 416;        // [8] final candidate costs
   static constexpr int MISC = 424;      // [16] ints, slots M_* below
   static constexpr int NBL = 440;       // [9] short2 neighbour pixels

@@ -1038,6 +1038,8 @@ __global__ void __launch_bounds__(256, kTapWaves) k_weak_coop(const PassConst* _
     return t;
   };
   int pcnt[P];
+  // phase 1 by patch rows (the common case: centre side <= 6, 3x3 neighbour patches, C = 16)
+  const bool rows1 = C == 16 && tab_c && tab_n && n_n == 3;
 
   PHASE_BEGIN();
   // ---- phase 1: neighbours, weight tables, Old-NCC patch, candidate rows
@@ -1048,8 +1050,60 @@ __global__ void __launch_bounds__(256, kTapWaves) k_weak_coop(const PassConst* _
       nbl[k] = np;
       nsv[k] = (np.x == -1 || np.y == -1) ? 0u : B.sel[np.x + np.y * W];
     }
-    const int ntc = tab_c ? n_c * n_c : 0, ntn = tab_n ? n_n * n_n : 0;
     const float ss = pc.P.sigma_spatial, sc = pc.P.sigma_color;
+    if (rows1) {
+      // the tables by patch rows with their reference sums (the order of phase 1b's loop): lanes
+      // 0..n_c-1 a centre row each (row sums to RSUM, added in row order in phase 1b), lanes 8..15
+      // a 3x3 neighbour patch each (sums complete); a lane's texel loads are issued together
+      if (c < n_c) {
+        const short2 np = nbg[0];
+        if (!(np.x == -1 || np.y == -1)) {
+          const int i = -rad_c + c * inc_c;
+          float rp[6];
+#pragma unroll
+          for (int b = 0; b < 6; ++b) rp[b] = b < n_c ? ref_texel(B.ref, W, Hh, np.x + i, np.y - rad_c + b * inc_c) : 0.0f;
+          float r_ref = 0, r_rr = 0, r_w = 0;
+#pragma unroll
+          for (int b = 0; b < 6; ++b) {
+            if (b >= n_c) break;
+            const float w = bilateral_weight(i, -rad_c + b * inc_c, rp[b], T.rc, ss, sc);
+            const float wr = w * rp[b];
+            tcp[2 * (c * n_c + b)] = w; tcp[2 * (c * n_c + b) + 1] = wr;
+            r_ref = r_ref + wr;
+            r_rr = __builtin_fmaf(wr, rp[b], r_rr);
+            r_w = r_w + w;
+          }
+          float* rs3 = pb + WC::RSUM + 3 * c;
+          rs3[0] = r_ref; rs3[1] = r_rr; rs3[2] = r_w;
+        }
+      } else if (c >= 8) {
+        const int k = c - 7;
+        const short2 np = nbg[k];
+        if (!(np.x == -1 || np.y == -1)) {
+          float rp[9];
+#pragma unroll
+          for (int t = 0; t < 9; ++t) rp[t] = ref_texel(B.ref, W, Hh, np.x - rad_n + (t / 3) * inc_n, np.y - rad_n + (t % 3) * inc_n);
+          float* tp = tnp + (k - 1) * 18;
+          float a_ref = 0, a_rr = 0, a_w = 0;
+#pragma unroll
+          for (int a = 0; a < 3; ++a) {
+            float r_ref = 0, r_rr = 0, r_w = 0;
+#pragma unroll
+            for (int b = 0; b < 3; ++b) {
+              const float w = bilateral_weight(-rad_n + a * inc_n, -rad_n + b * inc_n, rp[a * 3 + b], T.rc, ss, sc);
+              const float wr = w * rp[a * 3 + b];
+              tp[2 * (a * 3 + b)] = w; tp[2 * (a * 3 + b) + 1] = wr;
+              r_ref = r_ref + wr;
+              r_rr = __builtin_fmaf(wr, rp[a * 3 + b], r_rr);
+              r_w = r_w + w;
+            }
+            a_ref += r_ref; a_rr += r_rr; a_w += r_w;
+          }
+          ncc_pre(a_ref, a_rr, a_w, sums[3 * k], sums[3 * k + 1], sums[3 * k + 2]);
+        }
+      }
+    }
+    const int ntc = tab_c && !rows1 ? n_c * n_c : 0, ntn = tab_n && !rows1 ? n_n * n_n : 0;
     for (int t = c; t < ntc + 8 * ntn; t += C) {
       int k, tt, n, rad, inc;
       if (t < ntc) { k = 0; tt = t; n = n_c; rad = rad_c; inc = inc_c; }
@@ -1094,9 +1148,20 @@ __global__ void __launch_bounds__(256, kTapWaves) k_weak_coop(const PassConst* _
       pb[WC::NBOX_A] = T.nbox[0]; pb[WC::NBOX_A + 1] = T.nbox[1]; pb[WC::NBOX_A + 2] = T.nbox[2]; pb[WC::NBOX_B] = T.nbox[3];
       pb[WC::RC] = T.rc;
     }
+    if (rows1 && c == 0) {   // the centre patch's row sums in row order
+      const short2 np = nbl[0];
+      if (!(np.x == -1 || np.y == -1)) {
+        float a_ref = 0, a_rr = 0, a_w = 0;
+        for (int a = 0; a < n_c; ++a) {
+          const float* rs3 = pb + WC::RSUM + 3 * a;
+          a_ref += rs3[0]; a_rr += rs3[1]; a_w += rs3[2];
+        }
+        ncc_pre(a_ref, a_rr, a_w, sums[0], sums[1], sums[2]);
+      }
+    }
     for (int k = c; k < 9; k += C) {
       const short2 np = nbl[k];
-      if (np.x == -1 || np.y == -1 || !(k == 0 ? tab_c : tab_n)) continue;
+      if (rows1 || np.x == -1 || np.y == -1 || !(k == 0 ? tab_c : tab_n)) continue;
       const int n = k == 0 ? n_c : n_n, rad = k == 0 ? rad_c : rad_n, inc = k == 0 ? inc_c : inc_n;
       const float* tp = k == 0 ? tcp : tnp + (k - 1) * 18;
       float a_ref = 0, a_rr = 0, a_w = 0;
