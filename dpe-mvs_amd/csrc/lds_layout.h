@@ -108,7 +108,7 @@ struct WeakCarveT {
   static constexpr int RND = 472;       // PRE: [12] refinement draws (phase 7), over ALIAS and 4 more floats
   static constexpr int FIXED = PRE ? 484 : 480;
   // misc ints
-  static constexpr int M_NSEL = 0, M_RADC = 1, M_INCC = 2, M_NC = 3, M_WNORM = 4, M_CMASK = 5, M_NB3 = 6, M_FLAGS = 8;
+  static constexpr int M_NSEL = 0, M_RADC = 1, M_INCC = 2, M_NC = 3, M_WNORM = 4, M_CMASK = 5, M_NB3 = 6, M_POOL = 7, M_FLAGS = 8;
   // nv-dependent tail
   LDS_HD static constexpr int cost(int) { return FIXED; }                 // [8][nv]
   LDS_HD static constexpr int sp(int nv) { return FIXED + 8 * nv; }       // [nv]

@@ -974,8 +974,10 @@ __global__ void __launch_bounds__(256, kTapWaves) k_weak_coop(const PassConst* _
   const int ps = lane / C, c = lane % C;
   const int W = pc.W, Hh = pc.H, nv = pc.N - 1;
   const DpeCamera& c0 = pc.cams[0];
-  const int wbase = (xcd_remap(blockIdx.x, gridDim.x, B.xcd_rows * 16) * wpb + wave) * P;
-  if (wbase >= nlist) return;                            // wave-uniform tail
+  const int wgbase = xcd_remap(blockIdx.x, gridDim.x, B.xcd_rows * 16) * wpb * P;
+  const int wbase = wgbase + wave * P;
+  constexpr bool WGP = true;   // workgroup-wide job pools (false: each wave's own 4 pixels)
+  if ((WGP ? wgbase : wbase) >= nlist) return;           // workgroup- (wave-) uniform tail
   const int gi = wbase + ps;
   const bool active = gi < nlist;
   const int center = active ? list[gi] : 0;
@@ -1021,9 +1023,32 @@ __global__ void __launch_bounds__(256, kTapWaves) k_weak_coop(const PassConst* _
   T.rc = active ? ref_texel(B.ref, W, Hh, x, y) : 0.0f;
   T.tc = tcp; T.tn = tnp; T.sums = sums; T.nbl = nbl; T.nsv = nsv;
   const short2* nbg = B.nb + (size_t)center * 9;
-  // pooled phases: the NCCs of all the wave's pixels are dealt round-robin over its 64 lanes (as
-  // in the strong sweep), so a job carries its pixel q; pix(q) = that pixel's LDS block
-  auto pix = [&](int q) -> float* { return (float*)lds4 + (size_t)(wave * P + q) * S; };
+  // pooled phases: the NCCs of all the workgroup's pixels are dealt round-robin over its lanes, so
+  // a job carries its pixel q (0..npx-1, the workgroup's pixels in list order) and pix(q) is that
+  // pixel's LDS block.  A pool's jobs fill whole waves first, so a wave with no job left skips
+  // the round and its SIMD issues other waves (pools over one wave's 4 pixels left 27-46 of 64
+  // lanes idle in the current-plane, refinement and final-cost rounds).  Each pixel's job count
+  // sits in its misc[M_POOL]; a job index is decoded by a scan over the pool's pixels.
+  const int npx = WGP ? wpb * P : P;
+  float* const pool0 = (float*)lds4 + (size_t)(WGP ? 0 : wave * P) * S;
+  const int pbase = WGP ? wgbase : wbase;                // list index of the pool's pixel 0
+  const int pl_lane = WGP ? (int)threadIdx.x : lane, pl_n = WGP ? (int)blockDim.x : 64;
+  auto pool_sync = [&]() { if constexpr (WGP) __syncthreads(); else wave_sync(); };
+  auto pix = [&](int q) -> float* { return pool0 + (size_t)q * S; };
+  auto pool_cnt = [&](int q) -> int { return ((const int*)(pix(q) + WC::MISC))[WC::M_POOL]; };
+  auto pool_total = [&]() -> int { int t = 0; for (int q = 0; q < npx; ++q) t += pool_cnt(q); return t; };
+  auto pool_decode = [&](int j, int& q, int& r) { q = 0; for (int cc; j >= (cc = pool_cnt(q)); ++q) j -= cc; r = j; };
+  auto pool_stat_g = [&](int k, int jobs) {   // DPE_DIAG & 16: jobs, wave rounds with a job, waves
+#if DPE_POOL_STATS
+    if (pl_lane == 0) {
+      atomicAdd(&g_pool[k][0], (unsigned long long)jobs);
+      atomicAdd(&g_pool[k][1], (unsigned long long)((jobs + 63) / 64));
+      atomicAdd(&g_pool[k][2], (unsigned long long)(pl_n / 64));
+    }
+#else
+    (void)k; (void)jobs;
+#endif
+  };
   auto tab_of = [&](int q) -> WeakTab {
     const float* qb = pix(q);
     const int* h = (const int*)(qb + WC::MISC);
@@ -1037,7 +1062,6 @@ __global__ void __launch_bounds__(256, kTapWaves) k_weak_coop(const PassConst* _
     t.nbl = (const short2*)(qb + WC::NBL); t.nsv = (const uint32_t*)(qb + WC::NSV);
     return t;
   };
-  int pcnt[P];
   // phase 1 by patch rows (the common case: centre side <= 6, 3x3 neighbour patches, C = 16)
   const bool rows1 = C == 16 && tab_c && tab_n && n_n == 3;
 
@@ -1200,30 +1224,27 @@ __global__ void __launch_bounds__(256, kTapWaves) k_weak_coop(const PassConst* _
     uint32_t um = 0;
     for (int i = 0; i < 8; ++i) if (misc[WC::M_FLAGS + i] && alias[i] == i) um |= 1u << i;
     misc[WC::M_CMASK] = (int)um;
+    misc[WC::M_POOL] = __builtin_popcount(um);
   }
-  wave_sync();
+  if (!active && c == 0) misc[WC::M_POOL] = 0;
+  pool_sync();
   {
-    int Sj = 0;
-#pragma unroll
-    for (int q = 0; q < P; ++q) {
-      pcnt[q] = wbase + q < nlist ? __builtin_popcount((uint32_t)((const int*)(pix(q) + WC::MISC))[WC::M_CMASK]) : 0;
-      Sj += pcnt[q];
-    }
+    const int Sj = pool_total();
     int q, r;
-    POOL_STAT(2, Sj * nv);
+    pool_stat_g(2, Sj * nv);
     // view-major: the lanes of one round gather from the same source images
-    for (int j = lane; j < Sj * nv; j += 64) {
-      job_decode<P>(pcnt, j % Sj, q, r);
+    for (int j = pl_lane; j < Sj * nv; j += pl_n) {
+      pool_decode(j % Sj, q, r);
       const int v = j / Sj + 1;
       float* qb = pix(q);
       uint32_t m = (uint32_t)((const int*)(qb + WC::MISC))[WC::M_CMASK];
       for (; r > 0; --r) m &= m - 1;
       const int i = __builtin_ctz(m);
-      const int cq = list[wbase + q];
+      const int cq = list[pbase + q];
       (qb + WC::cost(nv))[i * nv + v - 1] = ncc_new_tab<U8>(pc, B, tab_of(q), cq % W, cq / W, v, ((const float4*)(qb + WC::CPL))[i]);
     }
   }
-  wave_sync();
+  pool_sync();
   PHASE(2);
   if (active)
     for (int i = c; i < 8; i += C)
@@ -1257,9 +1278,12 @@ __global__ void __launch_bounds__(256, kTapWaves) k_weak_coop(const PassConst* _
     for (int i = 0; i < nv; ++i) if (vwl[i] > 0) { setBit(tsv, i); wnorm += vwl[i]; sel_list[ns++] = i; }
     misc[WC::M_NSEL] = ns;
     misc[WC::M_WNORM] = __float_as_int(wnorm);
-    hyp[6] = B.fit_plane[center];
+    const float4 f6 = B.fit_plane[center];
+    hyp[6] = f6;
+    misc[WC::M_POOL] = ((f6.x == 0 && f6.y == 0 && f6.z == 0) ? 1 : 2) * ns;   // current (+ fit) plane jobs
   }
-  wave_sync();
+  if (!active && c == 0) misc[WC::M_POOL] = 0;
+  pool_sync();
   PHASE(5);
   const int nsel = active ? misc[WC::M_NSEL] : 0;
   const float wn = active ? __int_as_float(misc[WC::M_WNORM]) : 1.0f;
@@ -1269,27 +1293,22 @@ __global__ void __launch_bounds__(256, kTapWaves) k_weak_coop(const PassConst* _
   // ---- phase 4: current plane and fit plane over the selected views; final candidate costs
   // pixel q's hyp_cost term (DPE.cu:1140-1150) (view v, plane pl) into its hv row
   auto hyp_val_q = [&](int q, int v, const float4& pl) __attribute__((always_inline)) -> float {
-    const int cq = list[wbase + q];
+    const int cq = list[pbase + q];
     const int qx = cq % W, qy = cq / W;
     const float cn = ncc_new_tab<U8>(pc, B, tab_of(q), qx, qy, v, pl);
     return geom ? cn + gf * geom_cost(pc, B, qx, qy, v, pl) : cn;
   };
-  auto nsel_of = [&](int q) -> int { return wbase + q < nlist ? ((const int*)(pix(q) + WC::MISC))[WC::M_NSEL] : 0; };
-  auto fit_of = [&](int q) -> bool {
-    const float4 f = ((const float4*)(pix(q) + WC::HYP))[6];
-    return !(f.x == 0 && f.y == 0 && f.z == 0);
-  };
   {
-#pragma unroll
-    for (int q = 0; q < P; ++q) pcnt[q] = (fit_of(q) ? 2 : 1) * nsel_of(q);
-    POOL_STAT(3, [&] { int t = 0; for (int q = 0; q < P; ++q) t += pcnt[q]; return t; }());
+    const int tot = pool_total();
+    pool_stat_g(3, tot);
     int q, r;
-    for (int j = lane; job_decode<P>(pcnt, j, q, r); j += 64) {
+    for (int j = pl_lane; j < tot; j += pl_n) {
+      pool_decode(j, q, r);
       float* qb = pix(q);
       const int ns = ((const int*)(qb + WC::MISC))[WC::M_NSEL];
       const int h = r / ns, k = r % ns;
       const int v = ((const int*)(qb + WC::sel(nv)))[k] + 1;
-      (qb + WC::hv(nv))[h * nv + k] = hyp_val_q(q, v, h ? ((const float4*)(qb + WC::HYP))[6] : B.planes[list[wbase + q]]);
+      (qb + WC::hv(nv))[h * nv + k] = hyp_val_q(q, v, h ? ((const float4*)(qb + WC::HYP))[6] : B.planes[list[pbase + q]]);
     }
   }
   PHASE(12);   // (phase 6 from here: the final candidate costs)
@@ -1312,7 +1331,7 @@ __global__ void __launch_bounds__(256, kTapWaves) k_weak_coop(const PassConst* _
       fc[i] = f / wn;
     }
   }
-  wave_sync();
+  pool_sync();   // the current / fit-plane values of every pool pixel are in
   PHASE(6);
   // ---- serial: propagation acceptance, fit plane, refinement hypotheses (DPE.cu:1792-1843, 1120-1170)
   float cost_now = 0.0f, cost_written = 0.0f, depth_now = 0.0f;
@@ -1364,15 +1383,16 @@ __global__ void __launch_bounds__(256, kTapWaves) k_weak_coop(const PassConst* _
     h4.w = dist2origin(c0, x, y, depth_perturbed, h4);
     hyp[0] = h0; hyp[1] = h1; hyp[2] = h2; hyp[3] = h3; hyp[4] = h4;
   }
-  wave_sync();
+  if (c == 0) misc[WC::M_POOL] = active && has_fit ? 5 * nsel : 0;
+  pool_sync();
   PHASE(7);
   // ---- phase 5: refinement NCCs, jobs (hypothesis, selected view)
   {
-#pragma unroll
-    for (int q = 0; q < P; ++q) pcnt[q] = fit_of(q) ? 5 * nsel_of(q) : 0;
-    POOL_STAT(4, [&] { int t = 0; for (int q = 0; q < P; ++q) t += pcnt[q]; return t; }());
+    const int tot = pool_total();
+    pool_stat_g(4, tot);
     int q, r;
-    for (int j = lane; job_decode<P>(pcnt, j, q, r); j += 64) {
+    for (int j = pl_lane; j < tot; j += pl_n) {
+      pool_decode(j, q, r);
       float* qb = pix(q);
       const int ns = ((const int*)(qb + WC::MISC))[WC::M_NSEL];
       const int h = r / ns, k = r % ns;
@@ -1380,7 +1400,7 @@ __global__ void __launch_bounds__(256, kTapWaves) k_weak_coop(const PassConst* _
       (qb + WC::hv(nv))[(2 + h) * nv + k] = hyp_val_q(q, v, ((const float4*)(qb + WC::HYP))[h]);
     }
   }
-  wave_sync();
+  pool_sync();
   PHASE(8);
   // ---- serial: sequential acceptance + write-back (DPE.cu:1190-1207, 1831-1843)
   if (active && c == 0) {
@@ -1403,23 +1423,24 @@ __global__ void __launch_bounds__(256, kTapWaves) k_weak_coop(const PassConst* _
     }
     hyp[5] = fin;
   }
-  wave_sync();
+  if (c == 0) misc[WC::M_POOL] = active ? nsel : 0;
+  pool_sync();
   PHASE(9);
   // ---- phase 6: the stored cost is the Old NCC of the final plane (DPE.cu:1845-1861)
   {
-#pragma unroll
-    for (int q = 0; q < P; ++q) pcnt[q] = nsel_of(q);
-    POOL_STAT(5, [&] { int t = 0; for (int q = 0; q < P; ++q) t += pcnt[q]; return t; }());
+    const int tot = pool_total();
+    pool_stat_g(5, tot);
     int q, r;
-    for (int j = lane; job_decode<P>(pcnt, j, q, r); j += 64) {
+    for (int j = pl_lane; j < tot; j += pl_n) {
+      pool_decode(j, q, r);
       float* qb = pix(q);
-      const int cq = list[wbase + q];
+      const int cq = list[pbase + q];
       const int v = ((const int*)(qb + WC::sel(nv)))[r] + 1;
       (qb + WC::hv(nv))[r] = ncc_old_any<U8>(fast_old, qb + WC::PW, qb[WC::OSUM], qb[WC::OSUM + 1], qb[WC::OSUM + 2], cq % W,
                                                    cq / W, pc, B, v, ((const float4*)(qb + WC::HYP))[5]);
     }
   }
-  wave_sync();
+  pool_sync();
   PHASE(10);
   if (active && c == 0) {
     float c2 = 0.0f;
