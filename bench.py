@@ -235,6 +235,7 @@ def pipeline_config4(dist, rank: int, world: int, local_rank: int, n: int = 16, 
     if rank == 0:
         shutil.rmtree(folder, ignore_errors=True)
     passes = [round(p[1], 3) for p in per_rank]
+    rehearsal = bool(dist) and dist.get_backend() != "nccl"
     return {"config": "BASELINE configs[3]: ETH3D-size 2688x1792, 16 reference images, 9 source views each, "
                       "full 3-round schedule, images sharded over the ranks (synthetic scene)",
             "images": n, "width": W, "height": H, "ranks": world, "ranks_in_group": world,
@@ -246,7 +247,10 @@ def pipeline_config4(dist, rank: int, world: int, local_rank: int, n: int = 16, 
             "note": "pipeline wall incl. JPEG decode, EdgeSegment, 12 passes per image, depth all-gathers, .npy outputs; "
                     "passes_s / exchange_s: max over ranks of the pass work and of the depth exchanges "
                     "(dpe_pipeline_last_timings [6] / [5]); passes_s_per_rank shows the load balance" +
-                    ("" if world > 1 else "; one rank: no exchange")}
+                    ("" if world > 1 else "; one rank: no exchange") +
+                    ("; REHEARSAL over gloo (ranks may share one GPU): unmeasured on hardware, the RCCL/xGMI numbers "
+                     "come only from the driver's multi-GPU node" if rehearsal else ""),
+            "measured_on_hardware": not rehearsal}
 
 
 def parity_on_sample(native, local_rank: int, sample) -> dict:
