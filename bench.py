@@ -38,7 +38,7 @@ FLOP_PER_HOMOGRAPHY = 120
 FLOP_PER_GEOM = 60
 MODEL_FLOP_PER_PX = (36 * FLOP_PER_TAP + FLOP_PER_HOMOGRAPHY) * (42 * (NV_ - 1) + 75 * 4)   # 0.86 MFLOP
 # per-dispatch HBM bytes from the committed PMC passes (tools/pmc.sh + tools/prof_summary.py)
-PMC_JSON = next((os.path.join(ROOT, "profiles", f) for f in ("r04f_pmc.json", "r04_pmc.json", "r03s2_pmc.json", "r03_pmc.json", "r02_pmc.json")
+PMC_JSON = next((os.path.join(ROOT, "profiles", f) for f in ("r05_pmc.json", "r04f_pmc.json", "r04_pmc.json", "r03s2_pmc.json", "r03_pmc.json", "r02_pmc.json")
                  if os.path.exists(os.path.join(ROOT, "profiles", f))), os.path.join(ROOT, "profiles", "r04_pmc.json"))
 CLASS_KERNEL = {"strong": "k_strong_coop", "weak": "k_weak_coop", "depth_to_weak": "k_depth_to_weak",
                 "local_refine": "k_local_refine_jobs", "init": "k_random_init", "ransac": "k_ransac_fit",

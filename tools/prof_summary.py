@@ -108,7 +108,7 @@ def main():
              "Per-kernel dispatch durations from `rocprofv3 --kernel-trace --stats` (the work-counting execute dropped).",
              "HBM bytes from separate `--pmc FETCH_SIZE` / `--pmc WRITE_SIZE` passes over one execute, "
              "read = 2 x 1024 x FETCH_SIZE (gfx950 correction), write = 1024 x WRITE_SIZE.", "",
-             "| kernel | dispatches | mean ms | median ms | min ms | ms / execute | VGPR | scratch B | LDS B | HBM MB / dispatch |",
+             "| kernel | dispatches | mean ms | median ms | min ms | ms / execute | trace VGPR field (x2 = VGPRs per lane, tools/ru.py) | scratch B | LDS B | HBM MB / dispatch |",
              "|---|---|---|---|---|---|---|---|---|---|"]
     for k, v in sorted(kt.items(), key=lambda kv: -kv[1]["total_ms"]):
         t = tr.get(k)
