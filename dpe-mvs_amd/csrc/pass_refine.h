@@ -342,7 +342,9 @@ __global__ void __launch_bounds__(64 * kBwD2W, kTapWaves) k_depth_to_weak(const 
       float p_cost = 0.0f;
       for (int si = 1; si < pc.N; ++si) {
         const int vi = si - 1;
-        if (isSet(sel, vi)) {
+        // a selected view whose weight is 0 adds (ncc + gf*geom) * 0 = +0 (both terms are finite
+        // and >= 0), so its NCC is not evaluated (restatement choice 6)
+        if (isSet(sel, vi) && vw[vi] != 0) {
           float tcst = 0.0f;
           const float c = ncc_old_any<U8>(fast, pw, s_ref, s_rr, s_w, x, y, pc, B, si, tp);
           tcst += c;
