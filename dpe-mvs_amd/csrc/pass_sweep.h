@@ -1016,10 +1016,10 @@ __global__ void __launch_bounds__(256, kTapWaves) k_weak_coop(const PassConst* _
   T.n_n = T.rad_n >= 0 ? (2 * T.rad_n) / T.inc_n + 1 : 0;
   T.tab_c = T.n_c >= 1 && T.n_c <= 6;
   T.tab_n = T.n_n >= 1 && T.n_n <= 3;
-  // references: the selects below take field addresses and keep T in scratch (24 B/lane; plain
-  // copies measured 1 ms slower)
-  const int &rad_c = T.rad_c, &inc_c = T.inc_c, &n_c = T.n_c, &rad_n = T.rad_n, &inc_n = T.inc_n, &n_n = T.n_n;
-  const bool &tab_c = T.tab_c, &tab_n = T.tab_n;
+  // plain copies (round 5): references to T's fields under the selects below kept T in scratch
+  // (32 B/lane); with the round-5 phase 1 and workgroup pools the copies are as fast and 0 B
+  const int rad_c = T.rad_c, inc_c = T.inc_c, n_c = T.n_c, rad_n = T.rad_n, inc_n = T.inc_n, n_n = T.n_n;
+  const bool tab_c = T.tab_c, tab_n = T.tab_n;
   T.rc = active ? ref_texel(B.ref, W, Hh, x, y) : 0.0f;
   T.tc = tcp; T.tn = tnp; T.sums = sums; T.nbl = nbl; T.nsv = nsv;
   const short2* nbg = B.nb + (size_t)center * 9;
