@@ -218,6 +218,44 @@ def test_multi_rank_jacobi_matches_one_rank(tmp_path, dense4, world):
         assert a[k].dtype == b[k].dtype and a[k].tobytes() == b[k].tobytes(), k
 
 
+def _timings():
+    ph = (C.c_double * 7)()
+    n = pipeline.lib().dpe_pipeline_last_timings(ph, 7)
+    return n, [float(v) for v in ph]
+
+
+def _rank_timing_main(rank, world, port, folder, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        assert pipeline.run_dpe_pipeline(folder, runner=oracle_runner(), verbose=False, dist=dist) == 0
+        q.put((rank, _timings()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_pipeline_timings_decompose(tmp_path, dense4):
+    """dpe_pipeline_last_timings (bench.py's pipeline_config4 decomposition): 7 entries, the pass work
+    and the exchanges inside the passes' share, the exchanges 0 on one rank and > 0 on each of 2
+    gloo ranks."""
+    import torch.multiprocessing as mp
+    one = _copy(dense4, tmp_path, "t1")
+    assert pipeline.run_dpe_pipeline(one, runner=oracle_runner(), verbose=False) == 0
+    n, t = _timings()
+    assert n == 7 and all(v >= 0.0 for v in t), t
+    assert t[5] == 0.0 and 0.0 < t[6] <= t[3] <= t[0], t
+    two = _copy(dense4, tmp_path, "t2")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    mp.start_processes(_rank_timing_main, args=(2, _free_port(), two, q), nprocs=2, join=True, start_method="spawn")
+    got = dict(q.get(timeout=10) for _ in range(2))
+    for rank, (n, t) in got.items():
+        assert n == 7 and t[5] > 0.0 and 0.0 < t[6] <= t[3] <= t[0], (rank, t)
+        assert t[5] + t[6] <= t[3] * 1.05 + 1e-3, (rank, t)
+
+
 def _rank_fail_main(rank, world, port, folder, mode, q):
     """One rank of a 2-rank run that must fail on every rank without hanging: `mode` "one_problem"
     (world_size > problems) or "rank1_runner" (rank 1's pass runner fails in its third pass)."""
