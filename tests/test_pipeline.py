@@ -256,6 +256,35 @@ def test_pipeline_timings_decompose(tmp_path, dense4):
         assert t[5] + t[6] <= t[3] * 1.05 + 1e-3, (rank, t)
 
 
+def test_failed_collective_aborts_peers(tmp_path, dense4):
+    """A collective that fails on this rank calls DpePipelineOptions.abort_collectives (bin/dpe passes
+    ncclCommAbort) so that peers waiting in theirs fail fast, and the run reports the failure."""
+    d = _copy(dense4, tmp_path, "abort")
+    o = pipeline.DpePipelineOptions()
+    pipeline.lib().dpe_pipeline_default_options(C.byref(o))
+    o.verbose = False
+    o.rank, o.world_size = 0, 2
+    calls = {"allgather": 0, "abort": 0}
+
+    def failing_allgather(_user, send, count, recv):
+        calls["allgather"] += 1
+        return -1
+
+    def abort(_user):
+        calls["abort"] += 1
+        return 0
+    ag = pipeline.ALLGATHER_FN(failing_allgather)
+    ab = C.CFUNCTYPE(C.c_int, C.c_void_p)(abort)
+    o.allgather = ag
+    o.abort_collectives = C.cast(ab, C.c_void_p)
+    runner = oracle_runner()
+    o.runner = C.cast(runner[0], C.c_void_p)
+    o.runner_user = C.cast(runner[1], C.c_void_p) if runner[1] is not None else None
+    rc = pipeline.lib().dpe_run_pipeline(d.encode(), C.byref(o))
+    assert rc != 0 and "all-gather failed" in pipeline.lib().dpe_pipeline_last_error().decode()
+    assert calls["allgather"] >= 1 and calls["abort"] >= 1, calls
+
+
 def _rank_fail_main(rank, world, port, folder, mode, q):
     """One rank of a 2-rank run that must fail on every rank without hanging: `mode` "one_problem"
     (world_size > problems) or "rank1_runner" (rank 1's pass runner fails in its third pass)."""
