@@ -27,4 +27,11 @@ void launch_depth_to_weak(int cls, long L, hipStream_t s, const PassConst* dpc, 
 // LocalRefine (kLrPix pixels per wave), nv source views, over the border pixels the fused
 // DepthToWeak leaves
 void launch_local_refine(int cls, long L, int W, int H, int nv, hipStream_t s, const PassConst* dpc, const DevBufs& B);
+// the f32-texel instantiations of the three (tap_f32.hip, occupancy-first scheduler); the grid,
+// dynamic LDS and arguments are the launchers' above
+void launch_strong_f32(bool edge, unsigned grid, size_t lds, hipStream_t s, const PassConst* dpc, const DevBufs& B,
+                       int it, const int* list, const int* count);
+void launch_depth_to_weak_f32(unsigned grid, hipStream_t s, const PassConst* dpc, const DevBufs& B);
+void launch_local_refine_f32(unsigned grid, size_t lds, int border, hipStream_t s, const PassConst* dpc,
+                             const DevBufs& B);
 }  // namespace dpe

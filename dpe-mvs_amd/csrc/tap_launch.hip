@@ -1,14 +1,15 @@
-// tap_launch.hip — launches of the strong sweep, DepthToWeak and LocalRefine, compiled as their own
-// translation unit with LLVM's occupancy-first iterative scheduler
-// (-mllvm -amdgpu-sched-strategy=iterative-maxocc, see the Makefile).
+// tap_launch.hip — launches of the strong sweep, DepthToWeak and LocalRefine on the 8-bit /
+// quarter-integer texel layouts, their own translation unit; the f32-texel instantiations are in
+// tap_f32.hip.
 //
-// A scheduler is chosen per compilation, so the kernels that gain from it live here.  At the
-// 4 waves/SIMD of __launch_bounds__(256, kTapWaves) the default scheduler hoists the gathers of
-// the unrolled 36-tap loop until it needs more than 128 VGPRs and spills (strong 56, DepthToWeak
-// 68, LocalRefine 36 B/lane of scratch, whose stores reach HBM); the iterative scheduler fits the
-// same code in 106-110 VGPRs with no scratch.  Interleaved A/B on the bench pass (bit-identical
-// outputs): strong -0.4 / -0.6 ms, DepthToWeak -0.6 / -0.6 ms, LocalRefine +0.05 ms.  The weak
-// sweep is slower under it (+1.2 ms, more scratch) and stays in dpe_mvs.hip with the default.
+// A scheduler is chosen per compilation.  Rounds 2-4 compiled these kernels with LLVM's
+// occupancy-first iterative scheduler (-mllvm -amdgpu-sched-strategy=iterative-maxocc): the
+// default one then hoisted the unrolled 36-tap loop's gathers past 128 VGPRs and spilled.  Since
+// round 5's tap reciprocal (no Newton step) and rolled slow-patch loop the default scheduler fits
+// them in 113-124 VGPRs with no scratch, and is faster: strong 26.56 -> 25.99 ms, DepthToWeak
+// 21.81 -> 20.94 ms, wall 67.63 -> 65.73 ms (profiles/r05ad_ab_tapsched.log, bit-identical).  The
+// f32 instantiations still spill under the default (164-244 B/lane) and keep the iterative
+// scheduler in tap_f32.hip.  The weak sweep stays in dpe_mvs.hip with the default.
 #define DPE_TAP_TU 1
 #include "tap_launch.h"
 #include "pass_refine.h"
@@ -24,24 +25,18 @@ void launch_strong(bool edge, int cls, unsigned grid, size_t lds, hipStream_t s,
     if (!once) {
       once = true;
       (void)hipFuncSetAttribute((const void*)k_strong_coop<kTexStrong, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      (void)hipFuncSetAttribute((const void*)k_strong_coop<TEX_F32, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       (void)hipFuncSetAttribute((const void*)k_strong_coop<kTexStrong, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      (void)hipFuncSetAttribute((const void*)k_strong_coop<TEX_F32, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     }
   }
-  if (edge) {
-    if (cls != IMG_F32) k_strong_coop<kTexStrong, true><<<grid, T, lds, s>>>(dpc, B, it, list, count);
-    else k_strong_coop<TEX_F32, true><<<grid, T, lds, s>>>(dpc, B, it, list, count);
-  } else {
-    if (cls != IMG_F32) k_strong_coop<kTexStrong, false><<<grid, T, lds, s>>>(dpc, B, it, list, count);
-    else k_strong_coop<TEX_F32, false><<<grid, T, lds, s>>>(dpc, B, it, list, count);
-  }
+  if (cls == IMG_F32) { launch_strong_f32(edge, grid, lds, s, dpc, B, it, list, count); return; }
+  if (edge) k_strong_coop<kTexStrong, true><<<grid, T, lds, s>>>(dpc, B, it, list, count);
+  else k_strong_coop<kTexStrong, false><<<grid, T, lds, s>>>(dpc, B, it, list, count);
 }
 
 void launch_depth_to_weak(int cls, long L, hipStream_t s, const PassConst* dpc, const DevBufs& B) {
   const unsigned g = (unsigned)((L + kBwD2W - 1) / kBwD2W);
-  if (cls != IMG_F32) k_depth_to_weak<kTexD2W, true><<<g, 64 * kBwD2W, 0, s>>>(dpc, B);
-  else k_depth_to_weak<TEX_F32, true><<<g, 64 * kBwD2W, 0, s>>>(dpc, B);
+  if (cls == IMG_F32) { launch_depth_to_weak_f32(g, s, dpc, B); return; }
+  k_depth_to_weak<kTexD2W, true><<<g, 64 * kBwD2W, 0, s>>>(dpc, B);
 }
 
 void launch_local_refine(int cls, long L, int W, int H, int nv, hipStream_t s, const PassConst* dpc, const DevBufs& B) {
@@ -56,11 +51,10 @@ void launch_local_refine(int cls, long L, int W, int H, int nv, hipStream_t s, c
     if (!once) {
       once = true;
       (void)hipFuncSetAttribute((const void*)k_local_refine_jobs<kTexLR>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      (void)hipFuncSetAttribute((const void*)k_local_refine_jobs<TEX_F32>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     }
   }
-  if (cls != IMG_F32) k_local_refine_jobs<kTexLR><<<g, 64 * kBwLR, lds, s>>>(dpc, B, border);
-  else k_local_refine_jobs<TEX_F32><<<g, 64 * kBwLR, lds, s>>>(dpc, B, border);
+  if (cls == IMG_F32) { launch_local_refine_f32(g, lds, border, s, dpc, B); return; }
+  k_local_refine_jobs<kTexLR><<<g, 64 * kBwLR, lds, s>>>(dpc, B, border);
 }
 
 }  // namespace dpe

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Per-kernel register / scratch / occupancy table of lib/libdpe_mvs.so's two translation units
-(hipcc -Rpass-analysis=kernel-resource-usage; csrc/tap_launch.hip with the Makefile's scheduler).
+"""Per-kernel register / scratch / occupancy table of lib/libdpe_mvs.so's three translation units
+(hipcc -Rpass-analysis=kernel-resource-usage, each with the Makefile's scheduler: the default for
+csrc/dpe_mvs.hip and csrc/tap_launch.hip, iterative-maxocc for csrc/tap_f32.hip).
 Usage: python tools/ru.py [extra hipcc flags...]"""
 import re
 import subprocess
@@ -10,7 +11,9 @@ ROOT = __file__.rsplit("/tools/", 1)[0]
 base = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
         "-Rpass-analysis=kernel-resource-usage", "-c", "-o", "/tmp/dpe_ru.o"]
 out = subprocess.run(base + [ROOT + "/dpe-mvs_amd/csrc/dpe_mvs.hip"] + sys.argv[1:], capture_output=True, text=True).stderr
-out += subprocess.run(base + ["-mllvm", "-amdgpu-sched-strategy=iterative-maxocc", ROOT + "/dpe-mvs_amd/csrc/tap_launch.hip"]
+out += subprocess.run(base + [ROOT + "/dpe-mvs_amd/csrc/tap_launch.hip"] + sys.argv[1:],
+                      capture_output=True, text=True).stderr
+out += subprocess.run(base + ["-mllvm", "-amdgpu-sched-strategy=iterative-maxocc", ROOT + "/dpe-mvs_amd/csrc/tap_f32.hip"]
                       + sys.argv[1:], capture_output=True, text=True).stderr
 rows, cur = [], None
 for line in out.splitlines():
