@@ -2,15 +2,19 @@
 # Build A/B variants of lib/libdpe_mvs.so into dpe-mvs_amd/lib/variants/<name>.so (in parallel).
 # Usage: tools/build_variants.sh "name:-DFLAG=1 -DOTHER=2" "base:" ...
 # The flags apply to all three translation units; TAP_SCHED / F32_SCHED (env) override the
-# schedulers of csrc/tap_launch.hip / csrc/tap_f32.hip (defaults: the Makefile's).
+# schedulers of csrc/tap_launch.hip / csrc/tap_f32.hip (defaults: the Makefile's); flags after a
+# second colon ("name:all flags:main-unit flags") apply to csrc/dpe_mvs.hip only, which always gets
+# the Makefile's MAIN_FLAGS (-fno-slp-vectorize; MAIN_FLAGS in the environment overrides).
 cd "$(dirname "$0")/../dpe-mvs_amd" || exit 1
 mkdir -p lib/variants obj/variants
 TAP_SCHED=${TAP_SCHED-}
 F32_SCHED=${F32_SCHED--mllvm -amdgpu-sched-strategy=iterative-maxocc}
+MAIN_FLAGS=${MAIN_FLAGS--fno-slp-vectorize}
 HF="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -w"
 build() {
-  local name=$1 flags=$2
-  /opt/rocm/bin/hipcc $HF $flags -c -o obj/variants/$name.main.o csrc/dpe_mvs.hip &
+  local name=$1 flags=${2%%:*} mflags=
+  [[ $2 == *:* ]] && mflags=${2#*:}
+  /opt/rocm/bin/hipcc $HF $MAIN_FLAGS $flags $mflags -c -o obj/variants/$name.main.o csrc/dpe_mvs.hip &
   local a=$!
   /opt/rocm/bin/hipcc $HF $flags $TAP_SCHED -c -o obj/variants/$name.tap.o csrc/tap_launch.hip &
   local b=$!

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Per-kernel register / scratch / occupancy table of lib/libdpe_mvs.so's three translation units
-(hipcc -Rpass-analysis=kernel-resource-usage, each with the Makefile's scheduler: the default for
-csrc/dpe_mvs.hip and csrc/tap_launch.hip, iterative-maxocc for csrc/tap_f32.hip).
+(hipcc -Rpass-analysis=kernel-resource-usage, each with the Makefile's flags: the default scheduler
+for csrc/dpe_mvs.hip (SLP vectorizer off) and csrc/tap_launch.hip, iterative-maxocc for
+csrc/tap_f32.hip).
 Usage: python tools/ru.py [extra hipcc flags...]"""
 import re
 import subprocess
@@ -10,7 +11,8 @@ import sys
 ROOT = __file__.rsplit("/tools/", 1)[0]
 base = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
         "-Rpass-analysis=kernel-resource-usage", "-c", "-o", "/tmp/dpe_ru.o"]
-out = subprocess.run(base + [ROOT + "/dpe-mvs_amd/csrc/dpe_mvs.hip"] + sys.argv[1:], capture_output=True, text=True).stderr
+out = subprocess.run(base + ["-fno-slp-vectorize", ROOT + "/dpe-mvs_amd/csrc/dpe_mvs.hip"] + sys.argv[1:],
+                     capture_output=True, text=True).stderr
 out += subprocess.run(base + [ROOT + "/dpe-mvs_amd/csrc/tap_launch.hip"] + sys.argv[1:],
                       capture_output=True, text=True).stderr
 out += subprocess.run(base + ["-mllvm", "-amdgpu-sched-strategy=iterative-maxocc", ROOT + "/dpe-mvs_amd/csrc/tap_f32.hip"]
