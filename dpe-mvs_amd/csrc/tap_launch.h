@@ -1,5 +1,5 @@
 // tap_launch.h — source-image layout per kernel and the launchers of the tap kernels compiled in
-// their own translation unit (tap_launch.hip).
+// their own translation units (tap_launch.hip; the f32-texel instantiations in tap_f32.hip).
 #pragma once
 #include <hip/hip_runtime.h>
 #include "pass_common.h"
