@@ -261,8 +261,9 @@ DEV uint8_t d2w_class(const PassConst& pc, const float* pcs, uint64_t is_peak) {
   return cls;
 }
 
-// grid: one wave per pixel, 4 waves per 256-thread workgroup (DepthToWeak); LocalRefine likewise
-constexpr int kBwD2W = 4, kBwLR = 4;
+// grid: one wave per pixel, one wave per workgroup (DepthToWeak: 19.97 against 20.69 ms at 4 waves,
+// profiles/r05ao_ab_wgsize2.log); LocalRefine 4 waves per 256-thread workgroup
+constexpr int kBwD2W = 1, kBwLR = 4;
 // LocalRefine fused into DepthToWeak's epilogue (LR = true).  For an interior pixel LocalRefine's 11
 // hypotheses (p_disp -5..5, DPE.cu:2809-2831) are DepthToWeak's samples 25..35 (:2663-2686): same
 // plane, depth, selected views and weights, so every per-view NCC and geometric term is the same

@@ -390,7 +390,9 @@ DEV bool job_decode(const int* cnt, int j, int& p, int& r) {
   return false;
 }
 
-constexpr int kBwStrong = 4;   // waves per workgroup
+// waves per workgroup: 2 (4 before round 5's end; 2 fits the first half-sweep beside GenNeighbours
+// better: wall -0.6 ms together with DepthToWeak at 1, profiles/r05ao_ab_wgsize2.log)
+constexpr int kBwStrong = 2;
 template <int U8, bool EDGE>
 __global__ void __launch_bounds__(64 * kBwStrong, kTapWaves) k_strong_coop(const PassConst* __restrict__ pcp, DevBufs B, int iter,
                                                      const int* __restrict__ list, const int* __restrict__ nlist_p) {
