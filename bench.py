@@ -14,7 +14,10 @@ geometric-consistency passes).  Reference images shard one per r
 work is fixed as N grows ("scaling": "weak"); value = all ranks' pixels / max-over-ranks time.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-  N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+  N > 1 either under a launcher (WORLD_SIZE must equal N):
+      python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+  or directly: `python bench.py --gpus N` starts the N ranks itself as a child torch.distributed.run
+  (before anything touches the GPU) and relays rank 0's JSON line and exit code.
 """
 from __future__ import annotations
 
@@ -196,34 +199,52 @@ def coarse_level_pass(native, _abi, synthetic, local_rank: int, sp, W: int, H: i
     return {"mpix_s": round(w * h / dt / 1e6, 4), "ms": round(dt * 1e3, 3), "tex_class": int(cls)}
 
 
-def pipeline_config4(dist, rank: int, world: int, local_rank: int, n: int = 16, W: int = 2688, H: int = 1792) -> dict:
-    """BASELINE configs[3] at the pipeline level: 16 reference images at 2688x1792 (ETH3D high-res
-    size, 9 source views each) through DPE_MVS.run_dpe_pipeline -- decode, EdgeSegment, the full
-    coarse-to-fine schedule of RunDPEPipeline (main.cpp:508-566: 3 resolution rounds x 4 passes,
-    geometric consistency from the second pass on) and the outputs -- with the images sharded in
-    contiguous blocks over the ranks and the depth maps all-gathered between passes (RCCL device
-    hook under "nccl").  Wall time = max over ranks; rate = n * W * H / wall."""
+PIPELINE_CONFIGS = {
+    # BASELINE configs[3]: ETH3D high-res size, 16 reference images, 9 source views each
+    "config4": dict(n=16, W=2688, H=1792, max_src=9, fusion=False,
+                    label="BASELINE configs[3]: ETH3D-size 2688x1792, 16 reference images, 9 source views each, "
+                          "full 3-round schedule, images sharded over the ranks (synthetic scene)"),
+    # BASELINE configs[4]: Tanks&Temples Intermediate size, 32 images, 31 source views each (the most the
+    # 32-bit view masks hold, main.h MAX_IMAGES), edge-guided deformable patches, fusion
+    "config5": dict(n=32, W=1920, H=1080, max_src=31, fusion=True,
+                    label="BASELINE configs[4]: TaT-size 1920x1080, 32 reference images, 31 source views each, "
+                          "edge-guided deformable patches, full 3-round schedule + RunFusion, images sharded "
+                          "over the ranks (synthetic scene)"),
+}
+
+
+def pipeline_config(dist, rank: int, world: int, local_rank: int, name: str) -> dict:
+    """A BASELINE multi-image config at the pipeline level (PIPELINE_CONFIGS[name]) through
+    DPE_MVS.run_dpe_pipeline: decode, EdgeSegment, the full coarse-to-fine schedule of RunDPEPipeline
+    (main.cpp:508-566: 3 resolution rounds x 4 passes, geometric consistency from the second pass on),
+    the outputs and, for config 5, RunFusion on rank 0 (main.cpp:578-580 -> DPE.cpp:1220-1370) -- with
+    the images sharded in contiguous blocks over the ranks and the depth maps all-gathered between
+    passes (RCCL device hook under "nccl").  Wall time = max over ranks; rate = n * W * H / wall."""
     import shutil
     from DPE_MVS import pipeline, synthetic
+    cfg = PIPELINE_CONFIGS[name]
+    n, W, H = cfg["n"], cfg["W"], cfg["H"]
     tag = os.environ.get("TORCHELASTIC_RUN_ID") or os.environ.get("MASTER_PORT") or str(os.getpid())
-    folder = os.path.join("/tmp", f"dpe_cfg4_{tag}")
+    folder = os.path.join("/tmp", f"dpe_{name}_{tag}")
     if rank == 0:
         shutil.rmtree(folder, ignore_errors=True)
         sc = synthetic.make_scene(W, H, n)
-        synthetic.write_dense_folder(folder, W, H, n, max_src=min(9, n - 1), with_edges=False, scene=sc)
+        synthetic.write_dense_folder(folder, W, H, n, max_src=min(cfg["max_src"], n - 1), with_edges=False, scene=sc)
+        del sc
     if dist:
         dist.barrier()
     import torch
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    pipeline.run_dpe_pipeline(folder, gpu_index=local_rank, verbose=False, dist=dist if world > 1 else None)
+    pipeline.run_dpe_pipeline(folder, gpu_index=local_rank, verbose=False, fusion=cfg["fusion"],
+                              dist=dist if world > 1 else None)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     import ctypes
-    ph = (ctypes.c_double * 7)()
-    pipeline.lib().dpe_pipeline_last_timings(ph, 7)
-    # per rank: wall, pass work, depth exchanges (status + export + all-gather + import), EdgeSegment
-    mine = [dt, ph[6], ph[5], ph[2]]
+    ph = (ctypes.c_double * 8)()
+    pipeline.lib().dpe_pipeline_last_timings(ph, 8)
+    # per rank: wall, pass work, depth exchanges (status + export + all-gather + import), EdgeSegment, fusion
+    mine = [dt, ph[6], ph[5], ph[2], ph[7]]
     per_rank = [mine]
     if dist:
         t = torch.tensor(mine, dtype=torch.float64, device="cuda" if dist.get_backend() == "nccl" else "cpu")
@@ -236,21 +257,25 @@ def pipeline_config4(dist, rank: int, world: int, local_rank: int, n: int = 16, 
         shutil.rmtree(folder, ignore_errors=True)
     passes = [round(p[1], 3) for p in per_rank]
     rehearsal = bool(dist) and dist.get_backend() != "nccl"
-    return {"config": "BASELINE configs[3]: ETH3D-size 2688x1792, 16 reference images, 9 source views each, "
-                      "full 3-round schedule, images sharded over the ranks (synthetic scene)",
-            "images": n, "width": W, "height": H, "ranks": world, "ranks_in_group": world,
-            "images_per_rank": [((r + 1) * n) // world - (r * n) // world for r in range(world)],
-            "wall_s": round(dt, 3), "mpix_s": round(n * W * H / dt / 1e6, 4),
-            "passes_s": max(passes), "passes_s_per_rank": passes,
-            "exchange_s": round(max(p[2] for p in per_rank), 3),
-            "edge_segment_s": round(max(p[3] for p in per_rank), 3),
-            "note": "pipeline wall incl. JPEG decode, EdgeSegment, 12 passes per image, depth all-gathers, .npy outputs; "
-                    "passes_s / exchange_s: max over ranks of the pass work and of the depth exchanges "
-                    "(dpe_pipeline_last_timings [6] / [5]); passes_s_per_rank shows the load balance" +
-                    ("" if world > 1 else "; one rank: no exchange") +
-                    ("; REHEARSAL over gloo (ranks may share one GPU): unmeasured on hardware, the RCCL/xGMI numbers "
-                     "come only from the driver's multi-GPU node" if rehearsal else ""),
-            "measured_on_hardware": not rehearsal}
+    out = {"config": cfg["label"], "images": n, "width": W, "height": H, "src_views": min(cfg["max_src"], n - 1),
+           "ranks": world, "ranks_in_group": world,
+           "images_per_rank": [((r + 1) * n) // world - (r * n) // world for r in range(world)],
+           "wall_s": round(dt, 3), "mpix_s": round(n * W * H / dt / 1e6, 4),
+           "passes_s": max(passes), "passes_s_per_rank": passes,
+           "exchange_s": round(max(p[2] for p in per_rank), 3),
+           "edge_segment_s": round(max(p[3] for p in per_rank), 3)}
+    if cfg["fusion"]:
+        out["fusion_s"] = round(per_rank[0][4], 3)
+    out["note"] = ("pipeline wall incl. JPEG decode, EdgeSegment, 12 passes per image, depth all-gathers, .npy outputs" +
+                   ("; fusion_s: RunFusion on rank 0 (dpe_pipeline_last_timings [7], incl. the normal / state "
+                    "gather at N > 1)" if cfg["fusion"] else "") +
+                   "; passes_s / exchange_s: max over ranks of the pass work and of the depth exchanges "
+                   "(dpe_pipeline_last_timings [6] / [5]); passes_s_per_rank shows the load balance" +
+                   ("" if world > 1 else "; one rank: no exchange") +
+                   ("; REHEARSAL over gloo (ranks may share one GPU): unmeasured on hardware, the RCCL/xGMI numbers "
+                    "come only from the driver's multi-GPU node" if rehearsal else ""))
+    out["measured_on_hardware"] = not rehearsal
+    return out
 
 
 def parity_on_sample(native, local_rank: int, sample) -> dict:
@@ -274,6 +299,38 @@ def parity_on_sample(native, local_rank: int, sample) -> dict:
             "bit_exact": bits}
 
 
+def spawn_ranks(n: int) -> int:
+    """`--gpus N` (N > 1) without a launcher: one rank per GPU through a CHILD torch.distributed.run
+    on 127.0.0.1 (never an exec; nothing has initialised the GPU in this process), its stdout (rank
+    0's JSON line) and stderr inherited; returns the child's exit code."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    print(f"bench.py: starting {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.run(cmd, env=dict(os.environ)).returncode
+
+
+def launch_check(world: int, rank: int) -> None:
+    """--launch-check: the rank layout alone (no GPU, gloo), so the --gpus N launch path is testable
+    on CPU: every rank joins one all-reduce, rank 0 prints the line's n_gpus and the ranks seen."""
+    seen = 1
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+        t = torch.ones(1)
+        dist.all_reduce(t)
+        seen = int(t.item())
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "launch_check": True, "n_gpus": world, "ranks_joined": seen}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -284,13 +341,26 @@ def main():
     ap.add_argument("--no-pass-types", action="store_true", help="skip the FIRST_INIT / REFINE_INIT passes (kernel traces)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end dpe_mvs() run")
     ap.add_argument("--e2e-images", type=int, default=10)
-    ap.add_argument("--no-pipeline", action="store_true", help="skip the BASELINE configs[3] pipeline line")
+    ap.add_argument("--no-pipeline", action="store_true", help="skip the BASELINE configs[3] / [4] pipeline lines")
+    ap.add_argument("--no-config5", action="store_true", help="skip the BASELINE configs[4] pipeline line")
+    ap.add_argument("--launch-check", action="store_true", help="only check the rank layout (CPU, gloo)")
     ap.add_argument("--width", type=int, default=W_)
     ap.add_argument("--height", type=int, default=H_)
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus < 1:
+        sys.exit(f"bench.py: --gpus {args.gpus}: need at least 1")
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
+    world = int(world_env or "1")
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU "
+                 f"(--nproc-per-node {args.gpus}) or drop the launcher and let --gpus start the ranks")
     rank = int(os.environ.get("RANK", "0"))
+    if args.launch_check:
+        launch_check(world, rank)
+        return
     import torch
     # one rank per GPU; the modulo only matters for a rehearsal of several ranks on one card
     local_rank = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
@@ -510,7 +580,9 @@ def main():
     if not args.no_pipeline:   # every rank joins (the pipeline all-gathers depth maps between passes)
         ctx.close()
         ctx = None
-        result["pipeline_config4"] = pipeline_config4(dist, rank, world, local_rank)
+        result["pipeline_config4"] = pipeline_config(dist, rank, world, local_rank, "config4")
+        if not args.no_config5:
+            result["pipeline_config5"] = pipeline_config(dist, rank, world, local_rank, "config5")
     if rank == 0 and world == 1 and not args.no_e2e:
         if ctx is not None:
             ctx.close()

@@ -46,9 +46,10 @@ namespace {
 thread_local std::string g_err;
 const char* kOutName = "DPE";
 // wall seconds of the last run's phases: total, decode, GetProblemEdges pre-pass, passes (incl. the
-// exchanges), outputs + fusion, then (multi-rank) the depth exchanges alone and the pass work alone
-constexpr int kNumTimes = 7;
-double g_times[kNumTimes] = {0, 0, 0, 0, 0, 0, 0};
+// exchanges), outputs + fusion, then (multi-rank) the depth exchanges alone, the pass work alone and
+// RunFusion alone (rank 0, incl. the normal/weak exchange that feeds it)
+constexpr int kNumTimes = 8;
+double g_times[kNumTimes] = {0, 0, 0, 0, 0, 0, 0, 0};
 double now_s() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
 
 struct Problem {   // main.h:108-118
@@ -612,9 +613,10 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
           depth_cur[p.ref_image_id] = DepthMap{s.w, s.h, s.depth};
         }
       }
+      // the pass round's GPU work is finished before its clock stops (and, multi-rank, before the
+      // exchange's clock starts): with one rank the passes are otherwise only enqueued here
+      if (resident && !failed && dpe_sync(runner.ctx) != 0) fail(dpe_last_error());
       if (world == 1 && failed) { err = first_err; return 1; }
-      // multi-rank: the pass round's GPU work is finished before the exchange's clock starts
-      if (world > 1 && resident && !failed && dpe_sync(runner.ctx) != 0) fail(dpe_last_error());
       const double tx0 = now_s();
       t_pass += tx0 - tp0;
       if (world > 1 && resident) {   // all-gather of the depth maps from / into the HBM-resident states
@@ -715,6 +717,8 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
   // would leave the others' next collective, or their success, inconsistent with it)
   if (world > 1 && !status_exchange()) return 1;
   if (failed) { err = first_err; return 1; }
+  const double t_fusion0 = now_s();
+  g_times[7] = 0.0;
   if (opt.fusion) {   // RunFusion (main.cpp:578-580)
     std::map<int, ImageState> all;
     for (int pi : blocks[rank]) all[problems[pi].ref_image_id] = states[problems[pi].ref_image_id];
@@ -810,6 +814,7 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
       if (!export_point_cloud((fs::path(dense) / kOutName / "DPE.ply").string(), cloud, err)) return 1;
       if (opt.verbose) std::cout << "Fused " << cloud.size() << " points" << std::endl;
     }
+    g_times[7] = now_s() - t_fusion0;
   }
   if (!opt.keep_intermediate)   // the reference's clean-up (main.cpp:581-595)
     for (int pi : blocks[rank])

@@ -87,7 +87,9 @@ const char* dpe_pipeline_last_error(void);
  * [2] the GetProblemEdges pre-pass (EdgeSegment), [3] the passes (with the depth exchanges),
  * [4] outputs + fusion, [5] the depth exchanges alone (multi-rank: status all-gather, export,
  * all-gather, import, summed over the pass rounds; 0 for one rank), [6] the pass work alone (each
- * pass round up to its GPU work's end).  Returns the number of entries written (<= n, at most 7). */
+ * pass round up to its GPU work's end, on one rank too), [7] RunFusion (part of [4]; with several
+ * ranks it includes the exchange of the final normals / pixel states; 0 without fusion).  Returns
+ * the number of entries written (<= n, at most 8). */
 int dpe_pipeline_last_timings(double* out, int n);
 
 /* Grey-level decode of a JPEG (baseline/extended, luma plane) or binary PGM.  Writes up to `cap`

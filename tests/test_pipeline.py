@@ -218,9 +218,51 @@ def test_multi_rank_jacobi_matches_one_rank(tmp_path, dense4, world):
         assert a[k].dtype == b[k].dtype and a[k].tobytes() == b[k].tobytes(), k
 
 
+def _rank_fusion_main(rank, world, port, folder, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        assert pipeline.run_dpe_pipeline(folder, runner=oracle_runner(), fusion_runner=oracle.fusion_runner(),
+                                         fusion=True, normal=True, weak=True, verbose=False, dist=dist) == 0
+        q.put((rank, _timings()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_eight_ranks_sixteen_images_match_one_rank(tmp_path):
+    """BASELINE configs[3]/[4]'s split at small size: 16 reference images over 8 gloo ranks (blocks of 2
+    per rank, main.cpp:537-558's serial problem loop sharded), the depth maps all-gathered between the
+    passes and the final normals / pixel states gathered for RunFusion on rank 0: every .npy output
+    and the fused PLY byte-identical to a 1-rank Jacobi run, and every rank reporting its exchanges."""
+    import torch.multiprocessing as mp
+    one, many = str(tmp_path / "one"), str(tmp_path / "many")
+    synthetic.write_dense_folder(one, 40, 30, 16, max_src=4)
+    shutil.copytree(one, many)
+    assert pipeline.run_dpe_pipeline(one, runner=oracle_runner(), fusion_runner=oracle.fusion_runner(), fusion=True,
+                                     normal=True, weak=True, schedule="jacobi", verbose=False) == 0
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    mp.start_processes(_rank_fusion_main, args=(8, _free_port(), many, q), nprocs=8, join=True, start_method="spawn")
+    got = dict(q.get(timeout=10) for _ in range(8))
+    assert sorted(got) == list(range(8))
+    for rank, (n, t) in got.items():
+        assert n == 8 and t[5] > 0.0 and 0.0 < t[6] <= t[3], (rank, t)
+        assert t[7] > 0.0, (rank, t)   # rank 0 fuses; every rank joins the normal / state exchange before it
+    outs = ("depth.npy", "normal.npy", "weak.npy")
+    for i in range(16):
+        for f in outs:
+            a = np.load(os.path.join(one, "DPE", f"{i:08d}", f))
+            b = np.load(os.path.join(many, "DPE", f"{i:08d}", f))
+            assert a.dtype == b.dtype and a.tobytes() == b.tobytes(), (i, f)
+    pa = open(os.path.join(one, "DPE", "DPE.ply"), "rb").read()
+    assert len(pa) > 200 and pa == open(os.path.join(many, "DPE", "DPE.ply"), "rb").read()
+
+
 def _timings():
-    ph = (C.c_double * 7)()
-    n = pipeline.lib().dpe_pipeline_last_timings(ph, 7)
+    ph = (C.c_double * 8)()
+    n = pipeline.lib().dpe_pipeline_last_timings(ph, 8)
     return n, [float(v) for v in ph]
 
 
@@ -237,22 +279,22 @@ def _rank_timing_main(rank, world, port, folder, q):
 
 
 def test_pipeline_timings_decompose(tmp_path, dense4):
-    """dpe_pipeline_last_timings (bench.py's pipeline_config4 decomposition): 7 entries, the pass work
-    and the exchanges inside the passes' share, the exchanges 0 on one rank and > 0 on each of 2
-    gloo ranks."""
+    """dpe_pipeline_last_timings (bench.py's pipeline_config4/5 decomposition): 8 entries, the pass
+    work and the exchanges inside the passes' share, the exchanges 0 on one rank and > 0 on each of 2
+    gloo ranks, the fusion time 0 without fusion and inside the outputs phase with it."""
     import torch.multiprocessing as mp
     one = _copy(dense4, tmp_path, "t1")
     assert pipeline.run_dpe_pipeline(one, runner=oracle_runner(), verbose=False) == 0
     n, t = _timings()
-    assert n == 7 and all(v >= 0.0 for v in t), t
-    assert t[5] == 0.0 and 0.0 < t[6] <= t[3] <= t[0], t
+    assert n == 8 and all(v >= 0.0 for v in t), t
+    assert t[5] == 0.0 and 0.0 < t[6] <= t[3] <= t[0] and t[7] == 0.0, t
     two = _copy(dense4, tmp_path, "t2")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     mp.start_processes(_rank_timing_main, args=(2, _free_port(), two, q), nprocs=2, join=True, start_method="spawn")
     got = dict(q.get(timeout=10) for _ in range(2))
     for rank, (n, t) in got.items():
-        assert n == 7 and t[5] > 0.0 and 0.0 < t[6] <= t[3] <= t[0], (rank, t)
+        assert n == 8 and t[5] > 0.0 and 0.0 < t[6] <= t[3] <= t[0], (rank, t)
         assert t[5] + t[6] <= t[3] * 1.05 + 1e-3, (rank, t)
 
 

@@ -1,4 +1,4 @@
-"""Timeline of one overlapped pass from a rocprofv3 --kernel-trace CSV (tools/gpu_r4_b.sh): every
+"""Timeline of one overlapped pass from a rocprofv3 --kernel-trace CSV (tools/gpu_run.sh TAG timeline): every
 dispatch of the last pass with its start offset, duration and queue, then the busy time of each
 queue and the span of the setup chain on the aux stream.
 
