@@ -67,6 +67,8 @@ struct DevBufs {
 //   4  weak-sweep path statistics (tools/weak_stats.py)
 //   8  GenNeighbours per-pixel clocks and counts (tools/gn_times.py)
 //  16  job-pool statistics of the cooperative kernels (tools/pool_stats.py)
+//  32  TIMING ONLY, results wrong: the fast taps' texel loads replaced by values made from their
+//      address bits (the gather path's share of a tap kernel, interleaved A/B with AB_NOCHECK=1)
 #ifndef DPE_DIAG
 #define DPE_DIAG 0
 #endif
@@ -75,6 +77,7 @@ struct DevBufs {
 #define DPE_LINE_STATS (((DPE_DIAG) >> 1) & 1)
 #define DPE_WEAK_STATS (((DPE_DIAG) >> 2) & 1)
 #define DPE_GN_TIMES (((DPE_DIAG) >> 3) & 1)
+#define DPE_FAKE_GATHER (((DPE_DIAG) >> 5) & 1)
 // Phase profiling (DPE_DIAG & 1): shader-clock cycles of each phase of a cooperative kernel,
 // summed over waves into B.phase[k].
 #if DPE_PHASE_PROF
@@ -325,8 +328,10 @@ DEV float2 project_h(const Homog& H, float x, float y) {   // ComputeCorrespondi
 }
 
 // True when every tap (x, y) of the rectangle [x0, x1] x [y0, y1] computes its projective
-// denominator qz = fma(h7, y, fma(h6, x, h8)) with a biased exponent in [1, 252], so the 3-op
-// d_rcp_fast(qz) is bit-identical to 1.0f / qz.  qz is affine in (x, y): its exact values over the
+// denominator qz = fma(h7, y, fma(h6, x, h8)) with a biased exponent in [1, 252]: there the bare
+// v_rcp_f32 (rcp_tap<true>) is the tap reciprocal of restatement choice 8 (the rcp_model / oracle
+// o_rcp_tap table value) with no per-tap range test, and project_h_fast's d_rcp_fast is
+// bit-identical to 1.0f / z.  qz is affine in (x, y): its exact values over the
 // rectangle lie between the four corner values (evaluated here with the taps' own formula), and
 // a tap's computed value is within 2^-22 * max(|bz|, |qz|) of the exact one.  Same sign at the
 // corners, a minimum magnitude well above that error and above 2^-100, and magnitudes below 2^100
@@ -355,7 +360,9 @@ DEV float ref_texel(const float* ref, int W, int H, int x, int y) {
 // addressing, DPE.cpp:927-933), restated (round 3; oracle OracleSampleQ):
 // a tap whose homography rows give (qx, qy, qz) reads the padded quad texel (Ux >> 8, Uy >> 8) with
 // weights (Ux & 255) / 256, (Uy & 255) / 256, where
-//     U = clamp(RN_even(Q * iz + 256), 0, 256 * lim + 256),   Q = 256 q (exact),  iz = RN(1 / qz)
+//     U = clamp(RN_even(Q * iz + 256), 0, 256 * lim + 256),   Q = 256 q (exact),  iz = rcp_tap(qz)
+// (round 5, restatement choice 8: iz is gfx950's v_rcp_f32 of qz, within 1 ulp of 1/qz and not
+// correctly rounded, for biased exponents 1..252; IEEE 1/qz outside; rounds 3-4 used RN(1 / qz))
 // i.e. the coordinate s + 1 = q / qz + 1 in 1/256 units rounded to nearest ONCE.  The rows are
 // pre-scaled by 256 (power of two: exact), and t = fma(Q, iz, 1.5·2^23 + 256) lands on the unit grid
 // of [2^23, 2^24), so t's encoding minus that of 1.5·2^23 is U: one FMA per coordinate (round 2 used
@@ -429,10 +436,21 @@ template <int T> DEV uint32_t tex_view(const DevBufs& B) {
 template <int T> constexpr uint32_t tex_bytes() { return T == TEX_F16 ? 8u : 4u; }
 template <int T> DEV uint32_t tex_stride(int W) { return (uint32_t)(W + (T == TEX_P16 ? 3 : 2)); }
 // the two row interpolations (r0 at y0, r1 at y1) of the texel at `p` for the x weight ax = fx / 256
+// texel load of the fast taps (DPE_FAKE_GATHER: f16 values in [128, 256) / bytes from the address bits)
+template <class V, bool A4 = false> DEV V ld_texel(const uint8_t* p) {
+#if DPE_FAKE_GATHER
+  const uint32_t a = (uint32_t)(uintptr_t)p;
+  if constexpr (sizeof(V) == 8) { V v; v.x = 0x58005800u | (a & 0x03FF03FFu); v.y = 0x58005800u | ((a >> 3) & 0x03FF03FFu); return v; }
+  else return (V)(a & 0x7F7F7F7Fu);
+#else
+  if constexpr (A4) return *(const uint2_a4*)p;
+  else return *(const V*)p;
+#endif
+}
 template <int T>
 DEV void texel_rows(const uint8_t* p, float ax, float& r0, float& r1) {
   if constexpr (T == TEX_P16) {
-    const uint2 t = *(const uint2_a4*)p;                 // (a, c), (b, d)
+    const uint2 t = ld_texel<uint2, true>(p);            // (a, c), (b, d)
     const h2v df = __builtin_bit_cast(h2v, t.y) - __builtin_bit_cast(h2v, t.x);
     const uint32_t d = __builtin_bit_cast(uint32_t, df);
     asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(r0) : "v"(ax), "v"(d), "v"(t.x));
@@ -440,11 +458,11 @@ DEV void texel_rows(const uint8_t* p, float ax, float& r0, float& r1) {
   } else if constexpr (T == TEX_F16) {
     // v_fma_mix_f32 is fma(ax, (float)half, (float)half) with one rounding; the compiler only forms
     // it under f32 denormal flushing, which cannot matter here (|ax*d| >= 2^-8 or 0, a integer)
-    const uint2 t = *(const uint2*)p;
+    const uint2 t = ld_texel<uint2>(p);
     asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(r0) : "v"(ax), "v"(t.y), "v"(t.x));
     asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[0,1,1] op_sel_hi:[0,1,1]" : "=v"(r1) : "v"(ax), "v"(t.y), "v"(t.x));
   } else {
-    const uint32_t t = *(const uint32_t*)p;
+    const uint32_t t = ld_texel<uint32_t>(p);
     const float t00 = (float)(t & 255u), t10 = (float)((t >> 8) & 255u);
     const float t01 = (float)((t >> 16) & 255u), t11 = (float)(t >> 24);
     r0 = __builtin_fmaf(ax, t10 - t00, t00);
@@ -525,8 +543,9 @@ DEV float tex_t_fast(float t, float tmax) { return __builtin_amdgcn_fmed3f(t, kT
 
 // One bilinear tap of the 8-bit quad image (layout T) at the view offset `vadj` (tex_vadj), from
 // the homography h with scaled column coefficients (scale_cols) and its row terms
-// bxy = 256 (h0 x + h2, h3 x + h5), bz = h6 x + h8; column yf.  Bit-identical to sample_quad8
-// when the tap's qz is in d_rcp_fast's exact range (rcp_range_ok).
+// bxy = 256 (h0 x + h2, h3 x + h5), bz = h6 x + h8; column yf.  Bit-identical to sample_quad8 with
+// rcp_model's reciprocal when the tap's qz has a biased exponent in [1, 252] (rcp_range_ok), where
+// the bare v_rcp_f32 is restatement choice 8's tap reciprocal.
 template <int T>
 DEV float tap_u8_fast(const DevBufs& B, uint32_t vadj, uint32_t stride, f2v tmax, const float* h, f2v bxy, float bz,
                       float yf) {
@@ -543,7 +562,7 @@ DEV float tap_u8_fast(const DevBufs& B, uint32_t vadj, uint32_t stride, f2v tmax
     texel_rows<T>(p, tex_frac(ctx, ux), r0, r1);
     return __builtin_fmaf(ay, r1 - r0, r0);
   } else {
-    const uint32_t tt = *(const uint32_t*)p;
+    const uint32_t tt = ld_texel<uint32_t>(p);
     const float ax = tex_frac(ctx, ux);
     const f2v lo = (f2v){(float)(tt & 255u), (float)((tt >> 16) & 255u)};
     const f2v hi = (f2v){(float)((tt >> 8) & 255u), (float)(tt >> 24)};

@@ -42,3 +42,18 @@ void launch_local_refine_f32(unsigned grid, size_t lds, int border, hipStream_t 
 }
 
 }  // namespace dpe
+
+// this unit's own copies of the DPE_DIAG counters (static __device__ in pass_common.h), summed by
+// tools/pool_stats.py and tools/line_stats.py with the other two units'
+#if DPE_POOL_STATS
+extern "C" void dpe_dbg_pool_stats_f32(unsigned long long out[24], int reset) {
+  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(dpe::g_pool), sizeof(dpe::g_pool));
+  if (reset) { unsigned long long z[24] = {}; (void)hipMemcpyToSymbol(HIP_SYMBOL(dpe::g_pool), z, sizeof(z)); }
+}
+#endif
+#if DPE_LINE_STATS
+extern "C" void dpe_dbg_line_stats_f32(unsigned long long out[16], int reset) {
+  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(dpe::g_lstat), sizeof(dpe::g_lstat));
+  if (reset) { unsigned long long z[16] = {}; (void)hipMemcpyToSymbol(HIP_SYMBOL(dpe::g_lstat), z, sizeof(z)); }
+}
+#endif

@@ -104,6 +104,18 @@ def literal_lib(mode: int):
     return _literal[mode]
 
 
+_rcp_ieee = None
+
+
+def rcp_ieee_lib():
+    """The ORACLE_RCP_IEEE build: restatement choice 8 off (the tap reciprocal IEEE 1.0f / z instead
+    of the gfx950 v_rcp_f32 table), every other choice as in lib()."""
+    global _rcp_ieee
+    if _rcp_ieee is None:
+        _rcp_ieee = _load(os.path.join(HERE, "build", "liboracle_dpe_rcp_ieee.so"))
+    return _rcp_ieee
+
+
 def host_threads() -> int:
     """Host threads this process may use: OMP_NUM_THREADS when set (the GPU box sets it to its CPU
     share), else the affinity mask."""

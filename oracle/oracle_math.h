@@ -125,10 +125,20 @@ static inline float o_rcp_hw(float z) {   // v_rcp_f32(z) for a biased exponent 
   r = (uint32_t)((int64_t)r + (int64_t)(127 - (int)e) * (1 << 23));   // scaled by 2^(127 - e)
   return bits_to_f(r | (u & 0x80000000u));
 }
+// ORACLE_RCP_IEEE (build/liboracle_dpe_rcp_ieee.so, tests/test_rcp_choice.py only): choice 8 off,
+// the tap reciprocal the IEEE 1.0f / z of rounds 3-4, every other restatement choice kept -- so that
+// the parity claims resting on the device-derived table are measured, not assumed
+#ifndef ORACLE_RCP_IEEE
+#define ORACLE_RCP_IEEE 0
+#endif
 static inline float o_rcp_tap(float z) {
+#if ORACLE_RCP_IEEE
+  return 1.0f / z;
+#else
   uint32_t u; std::memcpy(&u, &z, 4);
   const uint32_t e = (u >> 23) & 0xFFu;
   return e - 1u < 252u ? o_rcp_hw(z) : 1.0f / z;
+#endif
 }
 
 // float -> int truncation with CUDA cvt.rzi.s32 semantics (saturating, NaN -> 0).

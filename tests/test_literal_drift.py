@@ -1,4 +1,4 @@
-"""What the oracle's restatement choices cost: the restated oracle against its ORACLE_LITERAL builds
+"""What the oracle's restatement choices cost: the restated oracle against its ORACLE_LITERAL builds and the ORACLE_RCP_IEEE build (choice 8 off)
 (oracle/dpe_oracle.cpp: ComputeHomography / ComputeCorrespondingPoint / tex2D(pt + 0.5f) evaluated as
 DPE.cu:453-522, 734-736 write them; literal 1 with IEEE division, literal 2 with a * (1 / b) as a
 model of --use_fast_math), same inputs and Philox seeds, through one pass and through the 8-pass
@@ -29,7 +29,7 @@ def threads():
 def test_single_pass_drift(threads):
     # one REFINE_ITER + geom pass: ~93 % of the depths bit-identical, ~0.5 % beyond 1e-3 relative
     r = literal_drift.single_pass(160, 120, 3, threads)
-    for m in ("literal_ieee", "literal_fastdiv"):
+    for m in literal_drift.COMPARED:
         d = r[m]
         assert d["frac_bit_identical"] > 0.85, (m, d)
         assert d["frac_rel_gt_1e-3"] < 0.01, (m, d)
@@ -43,7 +43,7 @@ def test_schedule_drift_within_patchmatch_spread(threads):
     # ground truth is the same
     r = literal_drift.schedule(160, 120, 3, threads)
     ctl = r["restated_seed+1"]
-    for m in ("literal_ieee", "literal_fastdiv"):
+    for m in literal_drift.COMPARED:
         d = r[m]
         assert d["frac_rel_gt_1e-3"] <= 1.1 * ctl["frac_rel_gt_1e-3"], (m, d, ctl)
         assert d["rel_median"] <= 1.1 * ctl["rel_median"], (m, d, ctl)
@@ -51,6 +51,6 @@ def test_schedule_drift_within_patchmatch_spread(threads):
         assert d["weak_agreement"] >= ctl["weak_agreement"] - 0.005, (m, d, ctl)
     gt = r["vs_ground_truth"]
     base = gt["restated"]
-    for m in ("literal_ieee", "literal_fastdiv"):
+    for m in literal_drift.COMPARED:
         assert abs(gt[m]["frac_within_1pct"] - base["frac_within_1pct"]) < 0.01, (m, gt)
         assert abs(gt[m]["rel_median"] - base["rel_median"]) < 0.05 * base["rel_median"], (m, gt)

@@ -24,13 +24,13 @@ bufs = _abi.PassBuffers(inp, st)
 assert lib.dpe_pm_stage(ctx, C.byref(bufs.inp), C.byref(bufs.st)) == 0
 lib.dpe_set_timing(ctx, 1)
 buf = (C.c_ulonglong * 16)()
-for fn in ("dpe_dbg_line_stats_main", "dpe_dbg_line_stats_tap"):
+for fn in ("dpe_dbg_line_stats_main", "dpe_dbg_line_stats_tap", "dpe_dbg_line_stats_f32"):
     getattr(lib, fn)(buf, 1)
 rc = lib.dpe_pm_execute(ctx, None)
 assert rc == 0, (rc, lib.dpe_last_error())
 assert lib.dpe_pm_fetch(ctx, C.byref(bufs.st)) == 0, lib.dpe_last_error()
 tot = [0] * 16
-for fn in ("dpe_dbg_line_stats_main", "dpe_dbg_line_stats_tap"):
+for fn in ("dpe_dbg_line_stats_main", "dpe_dbg_line_stats_tap", "dpe_dbg_line_stats_f32"):
     getattr(lib, fn)(buf, 1)
     if buf[1]:   # row 0: the clamp-free choice of ELIDE builds, per translation unit
         print(f"{fn}: clamp-free choice: wave calls {buf[1]:.3e}, all lanes inside {buf[0] / buf[1]:.3f}, "

@@ -1,8 +1,10 @@
-"""How far the oracle's restatement choices 3 and 7 (oracle/dpe_oracle.cpp header) move whole passes
-and the whole 8-pass schedule, measured on the CPU against the ORACLE_LITERAL builds, which evaluate
-ComputeHomography / ComputeCorrespondingPoint (DPE.cu:453-522) and tex2D(pt + 0.5f) (DPE.cu:734-736,
-DPE.cpp:927-933) as the reference writes them (literal 1: IEEE division; literal 2: a * (1 / b), a
-model of --use_fast_math's approximate division).  Same inputs, same Philox seeds.
+"""How far the oracle's restatement choices 3, 7 and 8 (oracle/dpe_oracle.cpp header) move whole
+passes and the whole 8-pass schedule, measured on the CPU against the ORACLE_LITERAL builds, which
+evaluate ComputeHomography / ComputeCorrespondingPoint (DPE.cu:453-522) and tex2D(pt + 0.5f)
+(DPE.cu:734-736, DPE.cpp:927-933) as the reference writes them (literal 1: IEEE division; literal 2:
+a * (1 / b), a model of --use_fast_math's approximate division; both with choices 3, 7 and 8 off),
+and against the ORACLE_RCP_IEEE build (choice 8 alone off: the tap reciprocal IEEE 1.0f / z instead of
+the gfx950 v_rcp_f32 table).  Same inputs, same Philox seeds.
 
 TEST INFRASTRUCTURE (uses the oracle only).  Usage:
     python tools/literal_drift.py [--threads T] [--out profiles/r04_literal_drift.json] [--sizes 160x120x3,320x240x5]
@@ -26,12 +28,15 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 import oracle  # noqa: E402
 from DPE_MVS import _abi, pipeline, synthetic  # noqa: E402
 
-MODES = {"restated": None, "literal_ieee": 1, "literal_fastdiv": 2}
+MODES = {"restated": None, "literal_ieee": 1, "literal_fastdiv": 2, "rcp_ieee": "rcp"}
+COMPARED = ("literal_ieee", "literal_fastdiv", "rcp_ieee")
 SEED = 0x5EED   # run_dpe_pipeline's default base_seed
 
 
 def _lib(mode):
-    return oracle.lib() if MODES[mode] is None else oracle.literal_lib(MODES[mode])
+    if MODES[mode] is None:
+        return oracle.lib()
+    return oracle.rcp_ieee_lib() if MODES[mode] == "rcp" else oracle.literal_lib(MODES[mode])
 
 
 def compare(depth_a, depth_b, normal_a=None, normal_b=None, weak_a=None, weak_b=None) -> dict:
@@ -70,7 +75,7 @@ def single_pass(W: int, H: int, n: int, threads: int) -> dict:
     inp = synthetic.pass_input(sc, p, depths=synthetic.src_depths(sc), seed=W * 7 + n)
     out = {m: oracle.run_pass(inp, st, threads, library=_lib(m)) for m in MODES}
     res = {}
-    for m in ("literal_ieee", "literal_fastdiv"):
+    for m in COMPARED:
         a, b = out["restated"], out[m]
         # depth along the pixel ray is what the plane's w holds after the pass (GetDepthandNormal)
         res[m] = compare(a["planes"][..., 3], b["planes"][..., 3], a["planes"][..., :3], b["planes"][..., :3],
@@ -99,7 +104,7 @@ def schedule(W: int, H: int, n: int, threads: int) -> dict:
                           for i in range(n)}
         cat = lambda o, f: np.concatenate([o[i][f].reshape(-1, *o[i][f].shape[2:]) for i in range(n)])  # noqa: E731
         res = {}
-        for m in ("literal_ieee", "literal_fastdiv", "restated_seed+1"):
+        for m in COMPARED + ("restated_seed+1",):
             a = outs["restated"]; b = outs[m]
             res[m] = compare(cat(a, "depth"), cat(b, "depth"), cat(a, "normal"), cat(b, "normal"), cat(a, "weak"),
                              cat(b, "weak"))
@@ -124,7 +129,8 @@ def main():
     ap.add_argument("--sizes", default="160x120x3,320x240x5")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
-    report = {"what": "restated oracle vs ORACLE_LITERAL builds (restatement choices 3 and 7 off)", "cases": []}
+    report = {"what": "restated oracle vs the ORACLE_LITERAL builds (restatement choices 3, 7 and 8 off) and the "
+                      "ORACLE_RCP_IEEE build (choice 8 alone off: IEEE tap reciprocal)", "cases": []}
     for spec in a.sizes.split(","):
         W, H, n = (int(v) for v in spec.split("x"))
         t0 = time.time()

@@ -26,12 +26,12 @@ bufs = _abi.PassBuffers(inp, st)
 assert lib.dpe_pm_stage(ctx, C.byref(bufs.inp), C.byref(bufs.st)) == 0
 lib.dpe_set_timing(ctx, 1)
 buf = (C.c_ulonglong * 24)()
-for fn in ("dpe_dbg_pool_stats_main", "dpe_dbg_pool_stats_tap"):
+for fn in ("dpe_dbg_pool_stats_main", "dpe_dbg_pool_stats_tap", "dpe_dbg_pool_stats_f32"):
     getattr(lib, fn)(buf, 1)
 assert lib.dpe_pm_execute(ctx, None) == 0, lib.dpe_last_error()
 assert lib.dpe_pm_fetch(ctx, C.byref(bufs.st)) == 0, lib.dpe_last_error()
 tot = [0] * 24
-for fn in ("dpe_dbg_pool_stats_main", "dpe_dbg_pool_stats_tap"):
+for fn in ("dpe_dbg_pool_stats_main", "dpe_dbg_pool_stats_tap", "dpe_dbg_pool_stats_f32"):
     getattr(lib, fn)(buf, 1)
     for k in range(24):
         tot[k] += buf[k]
