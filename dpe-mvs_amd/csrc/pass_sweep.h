@@ -967,7 +967,7 @@ DEV float ncc_new_tab(const PassConst& pc, const DevBufs& B, const WeakTab& T, i
   if (nfast) WSTAT(14);
   static_assert(DPE_NEIGHBOUR_NUM == 9, "neighbour pairs 1..8");
 #ifndef DPE_WEAK_PAIR
-#define DPE_WEAK_PAIR 1
+#define DPE_WEAK_PAIR 0
 #endif
 #pragma unroll 1
   for (int k = 1; k < DPE_NEIGHBOUR_NUM; k += 2) {
