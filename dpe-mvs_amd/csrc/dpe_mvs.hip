@@ -117,6 +117,7 @@ struct DpeContext {
   hipEvent_t ev_done = nullptr;      // end of the last dpe_pm_execute's work on its stream
   bool pending = false;              // ev_done recorded and not yet waited for
   bool staged = false;
+  bool gn_done_for_stage = false;    // DPE_DBG_GN_ONCE (timing experiments): GenNeighbours' outputs kept
   bool timing = false;
   bool counting = false;
   int gn_slots = 0;                  // DPE_OPT_GN_SLOTS (0 = by rotate_time)
@@ -151,7 +152,8 @@ struct DpeContext {
   DevArr<short2> nb, nearest, edge_neigh, lab_bound;
   DevArr<int> radius;
   DevArr<int> tab_right, tab_down;   // FindNearestStrongPoint tables
-  DevArr<int> gn_ovf;                // GenNeighbours pixels left to the scratch kernel (k_gen_neighbours_lds)
+  DevArr<int> gn_ovf;
+  DevArr<float> gn_complex;          // DPE_DBG_GN_ONCE: complex_ after GenNeighbours                // GenNeighbours pixels left to the scratch kernel (k_gen_neighbours_lds)
   DevArr<float> gn_tab;              // normalised image coordinates per column / row (k_gn_tables)
   DevArr<int> lists, row_counts, list_totals;   // per-colour pixel lists for the sweeps
   DevArr<int> part_cnt;                          // per colour: chunk counts / offsets of the weak-list partition
@@ -282,7 +284,7 @@ void dpe_destroy(DpeContext* c) {
   c->e_rows.release(); c->e_mag.release(); c->e_itab.release(); c->e_dx.release(); c->e_dy.release();
   c->e_ftab.release(); c->e_stab.release();
   c->cnt.release();
-  c->tab_right.release(); c->tab_down.release(); c->gn_ovf.release(); c->gn_tab.release();
+  c->tab_right.release(); c->tab_down.release(); c->gn_ovf.release(); c->gn_tab.release(); c->gn_complex.release();
   c->lists.release(); c->row_counts.release(); c->list_totals.release(); c->part_cnt.release();
   (void)hipStreamSynchronize(c->aux);
   (void)hipEventDestroy(c->ev_fork); (void)hipEventDestroy(c->ev_join); (void)hipEventDestroy(c->ev_ei);
@@ -656,6 +658,7 @@ static int stage_impl(DpeContext* c, const DpePassInput* in, const StageSrc& src
   B.radius = c->radius.p;
   HIPC(hipStreamSynchronize(c->stream));
   c->staged = true;
+  c->gn_done_for_stage = false;
   return DPE_OK;
 }
 
@@ -717,6 +720,12 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   };
 
   if (timing) (void)hipEventRecord(c->ev_start, s);
+  // DPE_DBG_GN_ONCE=1 (timing experiments only): GenNeighbours runs in the first execute after a stage
+  // and its outputs (nb, weak_rel and complex_, which GenEdgeInform rewrites: restored after it) are kept for the next executes of the same staged state,
+  // which then skip it -- the same results (GenNeighbours depends only on the staged state), and the
+  // pass time without GenNeighbours on the critical path
+  static const bool gn_once = [] { const char* e = getenv("DPE_DBG_GN_ONCE"); return e && atoi(e) == 1; }();
+  const bool gn_skip = gn_once && c->gn_done_for_stage;
   // initial state (the reference uploads it in CudaSpaceInitialization, DPE.cpp:964-1015)
   HIPC(hipMemcpyAsync(B.planes, c->planes0.p, L * sizeof(float4), hipMemcpyDeviceToDevice, s));
   HIPC(hipMemcpyAsync(B.weak, c->weak0.p, L, hipMemcpyDeviceToDevice, s));
@@ -724,9 +733,9 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   HIPC(hipMemsetAsync(B.costs, 0, L * sizeof(float), s));
   HIPC(hipMemsetAsync(B.fit_plane, 0, L * sizeof(float4), s));
   HIPC(hipMemsetAsync(B.complex_, 0, L * sizeof(float), s));
-  HIPC(hipMemsetAsync(B.weak_rel, 0xFF, L, s));   // GenNeighbours writes 0 / 1 for every WEAK pixel
+  if (!gn_skip) HIPC(hipMemsetAsync(B.weak_rel, 0xFF, L, s));   // GenNeighbours writes 0 / 1 for every WEAK pixel
   HIPC(hipMemsetAsync(B.vw, 0, L * DPE_MAX_IMAGES, s));
-  HIPC(hipMemsetAsync(B.nb, 0xFF, L * 9 * sizeof(short2), s));
+  if (!gn_skip) HIPC(hipMemsetAsync(B.nb, 0xFF, L * 9 * sizeof(short2), s));
   HIPC(hipMemsetAsync(B.nearest, 0xFF, L * sizeof(short2), s));
   HIPC(hipMemsetAsync(B.edge_neigh, 0xFF, L * 8 * sizeof(short2), s));
   HIPC(hipMemsetAsync(B.lab_bound, 0xFF, L * 8 * sizeof(short2), s));
@@ -772,6 +781,7 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   }
   k_gen_edge_inform<<<fg, fb, 0, a>>>(dpc, Bc);
   if (pc.P.use_edge) k_edge_rays<<<(unsigned)(3 * (W + H) - 2), 64, 0, a>>>(dpc, Bc);
+  if (gn_skip) HIPC(hipMemcpyAsync(B.complex_, c->gn_complex.p, L * sizeof(float), hipMemcpyDeviceToDevice, a));
   if (overlap) HIPC(hipEventRecord(c->ev_ei, a));
   k_strong_tables_scan<<<(unsigned)(W + H), 64, 0, a>>>(dpc, Bc, c->tab_right.p, c->tab_down.p);
   k_find_nearest_strong<<<fg, fb, 0, a>>>(dpc, Bc, c->tab_right.p, c->tab_down.p);
@@ -779,7 +789,8 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   k_list_count<1><<<(H + 3) / 4, 256, 0, a>>>(dpc, Bc, c->row_counts.p + 2 * (size_t)H + 2);
   k_list_scan<1><<<1, 64, 0, a>>>(dpc, c->row_counts.p + 2 * (size_t)H + 2, c->list_totals.p + 4);
   k_list_fill<1><<<(H + 3) / 4, 256, 0, a>>>(dpc, Bc, c->row_counts.p + 2 * (size_t)H + 2, weak_list, (long)L);
-  if (pc.P.rotate_time <= 4) {
+  if (gn_skip) {
+  } else if (pc.P.rotate_time <= 4) {
     // the scratch-free kernel; pixels with more support points than its LDS slots (none at the
     // BASELINE workloads) or a NaN go to the scratch kernel, a small persistent grid that loops over
     // that overflow list (list_totals slot 6)
@@ -796,6 +807,11 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
     k_gen_neighbours<<<kGnOvfBlocks, 256, 0, a>>>(dpc, Bc, c->gn_ovf.p, c->list_totals.p + 6);
   } else {
     k_gen_neighbours<<<kGnOvfBlocks, 256, 0, a>>>(dpc, Bc, weak_list, c->list_totals.p + 4);
+  }
+  if (gn_once && !gn_skip) {
+    HIPC(c->gn_complex.ensure(L));
+    HIPC(hipMemcpyAsync(c->gn_complex.p, B.complex_, L * sizeof(float), hipMemcpyDeviceToDevice, a));
+    c->gn_done_for_stage = true;
   }
   k_neighbour_update<<<fg, fb, 0, a>>>(dpc, Bc);
   if (overlap) {

@@ -436,21 +436,26 @@ template <int T> DEV uint32_t tex_view(const DevBufs& B) {
 template <int T> constexpr uint32_t tex_bytes() { return T == TEX_F16 ? 8u : 4u; }
 template <int T> DEV uint32_t tex_stride(int W) { return (uint32_t)(W + (T == TEX_P16 ? 3 : 2)); }
 // the two row interpolations (r0 at y0, r1 at y1) of the texel at `p` for the x weight ax = fx / 256
-// texel load of the fast taps (DPE_FAKE_GATHER: f16 values in [128, 256) / bytes from the address bits)
-template <class V, bool A4 = false> DEV V ld_texel(const uint8_t* p) {
+// texel loads of the fast taps; DPE_FAKE_GATHER (timing only): f16 values in [128, 256) / bytes made
+// from the address bits instead of memory
 #if DPE_FAKE_GATHER
+DEV uint2 fake_texel2(const uint8_t* p) {
   const uint32_t a = (uint32_t)(uintptr_t)p;
-  if constexpr (sizeof(V) == 8) { V v; v.x = 0x58005800u | (a & 0x03FF03FFu); v.y = 0x58005800u | ((a >> 3) & 0x03FF03FFu); return v; }
-  else return (V)(a & 0x7F7F7F7Fu);
-#else
-  if constexpr (A4) return *(const uint2_a4*)p;
-  else return *(const V*)p;
-#endif
+  uint2 v; v.x = 0x58005800u | (a & 0x03FF03FFu); v.y = 0x58005800u | ((a >> 3) & 0x03FF03FFu);
+  return v;
 }
+#define LD_TEXEL_P16(p) fake_texel2(p)
+#define LD_TEXEL_F16(p) fake_texel2(p)
+#define LD_TEXEL_U8(p) ((uint32_t)(uintptr_t)(p) & 0x7F7F7F7Fu)
+#else
+#define LD_TEXEL_P16(p) (*(const uint2_a4*)(p))
+#define LD_TEXEL_F16(p) (*(const uint2*)(p))
+#define LD_TEXEL_U8(p) (*(const uint32_t*)(p))
+#endif
 template <int T>
 DEV void texel_rows(const uint8_t* p, float ax, float& r0, float& r1) {
   if constexpr (T == TEX_P16) {
-    const uint2 t = ld_texel<uint2, true>(p);            // (a, c), (b, d)
+    const uint2 t = LD_TEXEL_P16(p);                     // (a, c), (b, d)
     const h2v df = __builtin_bit_cast(h2v, t.y) - __builtin_bit_cast(h2v, t.x);
     const uint32_t d = __builtin_bit_cast(uint32_t, df);
     asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(r0) : "v"(ax), "v"(d), "v"(t.x));
@@ -458,11 +463,11 @@ DEV void texel_rows(const uint8_t* p, float ax, float& r0, float& r1) {
   } else if constexpr (T == TEX_F16) {
     // v_fma_mix_f32 is fma(ax, (float)half, (float)half) with one rounding; the compiler only forms
     // it under f32 denormal flushing, which cannot matter here (|ax*d| >= 2^-8 or 0, a integer)
-    const uint2 t = ld_texel<uint2>(p);
+    const uint2 t = LD_TEXEL_F16(p);
     asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(r0) : "v"(ax), "v"(t.y), "v"(t.x));
     asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[0,1,1] op_sel_hi:[0,1,1]" : "=v"(r1) : "v"(ax), "v"(t.y), "v"(t.x));
   } else {
-    const uint32_t t = ld_texel<uint32_t>(p);
+    const uint32_t t = LD_TEXEL_U8(p);
     const float t00 = (float)(t & 255u), t10 = (float)((t >> 8) & 255u);
     const float t01 = (float)((t >> 16) & 255u), t11 = (float)(t >> 24);
     r0 = __builtin_fmaf(ax, t10 - t00, t00);
@@ -562,7 +567,7 @@ DEV float tap_u8_fast(const DevBufs& B, uint32_t vadj, uint32_t stride, f2v tmax
     texel_rows<T>(p, tex_frac(ctx, ux), r0, r1);
     return __builtin_fmaf(ay, r1 - r0, r0);
   } else {
-    const uint32_t tt = ld_texel<uint32_t>(p);
+    const uint32_t tt = LD_TEXEL_U8(p);
     const float ax = tex_frac(ctx, ux);
     const f2v lo = (f2v){(float)(tt & 255u), (float)((tt >> 16) & 255u)};
     const f2v hi = (f2v){(float)((tt >> 8) & 255u), (float)(tt >> 24)};

@@ -867,46 +867,6 @@ DEV float patch_ncc_tab(const PassConst& pc, const DevBufs& B, int v, const Homo
   return ncc_finalize_pre(sm[0], sm[1], sm[2], a[0], a[1], a[2]);
 }
 
-// Two fast 3x3 patches of one homography (the weak sweep's neighbour patches k, k + 1): per patch the
-// operations of tab_taps<U8, true, 3>, interleaved so that all 18 gathers are in flight together.
-template <int U8>
-DEV void tab_taps3_pair(const PassConst& pc, const DevBufs& B, int v, const Homog& H0, int cx0, int cy0, int cx1, int cy1,
-                        int rad, int inc, const float* __restrict__ tw0, const float* __restrict__ tw1, float* acc0,
-                        float* acc1) {
-  const int W = pc.W, Hh = pc.H;
-  const Homog H = scale_cols(H0);
-  const f2v* wp0 = (const f2v*)tw0;
-  const f2v* wp1 = (const f2v*)tw1;
-  const uint32_t stride = tex_stride<U8>(W), vadj = tex_vadj<U8>((uint32_t)v * tex_view<U8>(B), stride);
-  const f2v tmax = tex_tmax2(W, Hh);
-  f2v s_sr0 = f2s(0.0f), s_sr1 = f2s(0.0f);
-  float s_ss0 = 0, s_ss1 = 0;
-#pragma unroll
-  for (int a = 0; a < 3; ++a) {
-    const float xf0 = (float)(cx0 - rad + a * inc), xf1 = (float)(cx1 - rad + a * inc);
-    const f2v bxy0 = fma2((f2v){H.h[0], H.h[3]}, f2s(xf0), (f2v){H.h[2], H.h[5]}) * f2s(kTexUnit);
-    const f2v bxy1 = fma2((f2v){H.h[0], H.h[3]}, f2s(xf1), (f2v){H.h[2], H.h[5]}) * f2s(kTexUnit);
-    const float bz0 = __builtin_fmaf(H.h[6], xf0, H.h[8]), bz1 = __builtin_fmaf(H.h[6], xf1, H.h[8]);
-    f2v r_sr0 = f2s(0.0f), r_sr1 = f2s(0.0f);
-    float r_ss0 = 0, r_ss1 = 0;
-#pragma unroll
-    for (int b = 0; b < 3; ++b) {
-      const float sp0 = tap_u8_fast<U8>(B, vadj, stride, tmax, H.h, bxy0, bz0, (float)(cy0 - rad + b * inc));
-      const float sp1 = tap_u8_fast<U8>(B, vadj, stride, tmax, H.h, bxy1, bz1, (float)(cy1 - rad + b * inc));
-      const f2v w0 = wp0[a * 3 + b], w1 = wp1[a * 3 + b];
-      r_sr0 = fma2(w0, f2s(sp0), r_sr0);
-      r_sr1 = fma2(w1, f2s(sp1), r_sr1);
-      const float ws0 = w0.x * sp0, ws1 = w1.x * sp1;
-      r_ss0 = __builtin_fmaf(ws0, sp0, r_ss0);
-      r_ss1 = __builtin_fmaf(ws1, sp1, r_ss1);
-    }
-    s_sr0 += r_sr0; s_ss0 += r_ss0;
-    s_sr1 += r_sr1; s_ss1 += r_ss1;
-  }
-  acc0[0] = s_sr0.x; acc0[1] = s_ss0; acc0[2] = s_sr0.y;
-  acc1[0] = s_sr1.x; acc1[1] = s_ss1; acc1[2] = s_sr1.y;
-}
-
 // Weak-sweep path statistics (DPE_DIAG & 4; tools/weak_stats.py): per NCC-New,
 // the centre patch side and path, the neighbour-patch paths, and per wave the number of distinct
 // centre-patch variants its lanes execute one after another.  Off in the product.
@@ -960,66 +920,33 @@ DEV float ncc_new_tab(const PassConst& pc, const DevBufs& B, const WeakTab& T, i
     }
   }
   // k = 1..8; one range check over the union of the 3x3 neighbour patches selects the fast
-  // reciprocal for all of them (it is exact on every tap inside that box).  The neighbours go in
-  // pairs (1, 2), (3, 4), ...: two fast 3x3 patches of a pair have their 18 gathers in flight
-  // together (tab_taps3_pair), and the pair's terms are then added in k order as before.
+  // reciprocal for all of them (it is exact on every tap inside that box)
   const bool nfast = T.nb3 && rcp_range_ok(H, T.nbox[0], T.nbox[1], T.nbox[2], T.nbox[3]);
   if (nfast) WSTAT(14);
-  static_assert(DPE_NEIGHBOUR_NUM == 9, "neighbour pairs 1..8");
-#ifndef DPE_WEAK_PAIR
-#define DPE_WEAK_PAIR 0
-#endif
 #pragma unroll 1
-  for (int k = 1; k < DPE_NEIGHBOUR_NUM; k += 2) {
-    int st[2];                                   // 0: no term, 1: +2 (outside, view selected), 2: patch
-    short2 npk[2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const short2 np = T.nbl[k + j];
-      npk[j] = np;
-      st[j] = 0;
-      if (np.x == -1 || np.y == -1) continue;
-      const float2 nsp = nfast ? project_h_fast(H, (float)np.x, (float)np.y) : project_h(H, (float)np.x, (float)np.y);
-      if (nsp.x < 0 || nsp.y < 0 || nsp.x >= (float)W || nsp.y >= (float)Hh) st[j] = isSet(T.nsv[k + j], v - 1) ? 1 : 0;
-      else st[j] = 2;
+  for (int k = 1; k < DPE_NEIGHBOUR_NUM; ++k) {
+    const short2 np = T.nbl[k];
+    if (np.x == -1 || np.y == -1) continue;
+    const float2 nsp = nfast ? project_h_fast(H, (float)np.x, (float)np.y) : project_h(H, (float)np.x, (float)np.y);
+    if (nsp.x < 0 || nsp.y < 0 || nsp.x >= (float)W || nsp.y >= (float)Hh) {
+      if (isSet(T.nsv[k], v - 1)) { strong_cost += 2.0f; strong_count++; }
+      continue;
     }
-    float tc[2] = {0.0f, 0.0f};
-    if (DPE_WEAK_PAIR && nfast && st[0] == 2 && st[1] == 2) {
-      WSTAT(15, 2);
-      float a0[3], a1[3];
-      tab_taps3_pair<U8>(pc, B, v, H, npk[0].x, npk[0].y, npk[1].x, npk[1].y, T.rad_n, T.inc_n, T.tn + (k - 1) * 18,
-                         T.tn + k * 18, a0, a1);
-      count_work(B, 0, 18ull);
-      const float* s0 = T.sums + 3 * k;
-      const float* s1 = T.sums + 3 * (k + 1);
-      tc[0] = ncc_finalize_pre(s0[0], s0[1], s0[2], a0[0], a0[1], a0[2]);
-      tc[1] = ncc_finalize_pre(s1[0], s1[1], s1[2], a1[0], a1[1], a1[2]);
+    float tc;
+    WSTAT(15);
+    if (!nfast && !T.tab_n) WSTAT(16);
+    if (nfast) {
+      float a[3];
+      tab_taps<U8, true, 3>(pc, B, v, H, np.x, np.y, T.rad_n, T.inc_n, 3, T.tn + (k - 1) * 18, a);
+      count_work(B, 0, 9ull);
+      const float* sm = T.sums + 3 * k;
+      tc = ncc_finalize_pre(sm[0], sm[1], sm[2], a[0], a[1], a[2]);
     } else {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        if (st[j] != 2) continue;
-        const int kk = k + j;
-        const short2 np = npk[j];
-        WSTAT(15);
-        if (!nfast && !T.tab_n) WSTAT(16);
-        if (nfast) {
-          float a[3];
-          tab_taps<U8, true, 3>(pc, B, v, H, np.x, np.y, T.rad_n, T.inc_n, 3, T.tn + (kk - 1) * 18, a);
-          count_work(B, 0, 9ull);
-          const float* sm = T.sums + 3 * kk;
-          tc[j] = ncc_finalize_pre(sm[0], sm[1], sm[2], a[0], a[1], a[2]);
-        } else {
-          tc[j] = T.tab_n ? patch_ncc_tab<U8, 6>(pc, B, v, H, np.x, np.y, T.rad_n, T.inc_n, T.n_n, T.tn + (kk - 1) * 18,
-                                                 T.sums + 3 * kk)
-                          : patch_ncc_generic<U8>(pc, B, v, H, np.x, np.y, T.rc, T.rad_n, T.inc_n);
-        }
-      }
+      tc = T.tab_n ? patch_ncc_tab<U8, 6>(pc, B, v, H, np.x, np.y, T.rad_n, T.inc_n, T.n_n, T.tn + (k - 1) * 18,
+                                       T.sums + 3 * k)
+                   : patch_ncc_generic<U8>(pc, B, v, H, np.x, np.y, T.rc, T.rad_n, T.inc_n);
     }
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      if (st[j] == 1) { strong_cost += 2.0f; strong_count++; }
-      else if (st[j] == 2) { strong_cost += tc[j]; strong_count++; }
-    }
+    strong_cost += tc; strong_count++;
   }
   if (strong_count == 0) return center_cost;
   strong_cost /= (float)strong_count;
@@ -1036,11 +963,8 @@ __host__ __device__ inline int weak_lds_per_pixel(int nv) { return WC::per_pixel
 
 // CheckerboardPropagationWeak (DPE.cu:1668-1862) + PlaneHypothesisRefinementWeak (:1120-1212).
 // C lanes per pixel, 64/C pixels per wave, blockDim.x/64 waves per workgroup.
-#ifndef DPE_WEAK_WAVES
-#define DPE_WEAK_WAVES kTapWaves
-#endif
 template <int U8, int C>
-__global__ void __launch_bounds__(256, DPE_WEAK_WAVES) k_weak_coop(const PassConst* __restrict__ pcp, DevBufs B, int iter,
+__global__ void __launch_bounds__(256, kTapWaves) k_weak_coop(const PassConst* __restrict__ pcp, DevBufs B, int iter,
                                                    const int* __restrict__ list, const int* __restrict__ nlist_p) {
   extern __shared__ float4 lds4[];
   static_assert(C == 16 || C == 32, "the per-pixel phases give lanes 0..8 the patch sums and lanes 8..15 the alias rows");

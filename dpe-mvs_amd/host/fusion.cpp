@@ -18,11 +18,34 @@
 #include <cmath>
 #include <cstring>
 #include <fstream>
+#include <algorithm>
+#include <cstdlib>
+#include <memory>
+#include <thread>
 #include <unordered_map>
 
 namespace dpe_host {
 
 // RunFusion's serial part (DPE.cpp:1286-1367) over the candidates of `fn`.
+//
+// Round 6, three changes that keep every result (tests/test_fusion.py: the PLY bit for bit):
+//  * the next image's candidates are fetched on a worker thread while this image is fused (double
+//    buffer; only one `fn` call runs at a time, and the fusion itself makes no `fn` call);
+//  * the candidate buffers are allocated once, uninitialised (`fn` writes every index, and every
+//    value the walk reads);
+//  * what in the reference's loop does not depend on the masks -- the angle test (acos) and the
+//    consistency weight (exp) of every candidate -- is evaluated first on host threads, with the
+//    same float expressions, into a per-pixel bit set of the candidates that pass and their weights;
+//    the serial walk then visits only those, in ascending view order, and adds the same weights in
+//    the same order (the masks it tests and sets are exactly the reference's).
+namespace {
+int fusion_threads() {
+  unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  if (const char* e = getenv("OMP_NUM_THREADS")) { const int v = atoi(e); if (v > 0) hw = std::min(hw, (unsigned)v); }
+  return (int)std::min(16u, hw);
+}
+}  // namespace
+
 bool run_fusion(std::vector<FusionView>& views, dpe_fusion_fn fn, void* user, std::vector<FusedPoint>& cloud,
                 std::string& err) {
   const int n = (int)views.size();
@@ -34,22 +57,75 @@ bool run_fusion(std::vector<FusionView>& views, dpe_fusion_fn fn, void* user, st
     dv[i] = views[i].view;
     views[i].mask.assign((size_t)views[i].view.width * views[i].view.height, 0);
   }
-  std::vector<int32_t> cidx;
-  std::vector<float> cval;
+  std::vector<std::vector<int>> srcs(n);
+  std::vector<int> refs(n);
+  size_t cap = 1;
   for (int i = 0; i < n; ++i) {
-    const int ref = idx_of(views[i].image_id);
-    FusionView& R = views[ref];
-    const int cols = R.view.width, rows = R.view.height;
-    std::vector<int> src;
-    for (int id : views[i].src_ids) src.push_back(idx_of(id));
-    const int ns = (int)src.size();
-    cidx.assign((size_t)cols * rows * ns, -1);
-    cval.assign((size_t)cols * rows * ns * 3, 0.0f);
-    if (ns > 0) {
-      const int rc = fn(user, dv.data(), n, ref, src.data(), ns, cidx.data(), cval.data());
-      if (rc != 0) { err = "fusion candidates failed (" + std::to_string(rc) + ")"; return false; }
+    refs[i] = idx_of(views[i].image_id);
+    for (int id : views[i].src_ids) srcs[i].push_back(idx_of(id));
+    if (srcs[i].size() > 32) { err = "fusion: more than 32 source views"; return false; }
+    const DpeFusionView& R = views[refs[i]].view;
+    cap = std::max(cap, (size_t)R.width * R.height * srcs[i].size());
+  }
+  struct Cand {
+    std::unique_ptr<int32_t[]> idx;
+    std::unique_ptr<float[]> val;
+    int rc = 0;
+  };
+  Cand buf[2];
+  for (Cand& b : buf) { b.idx.reset(new int32_t[cap]); b.val.reset(new float[cap * 3]); }
+  auto fetch = [&](int i, Cand* b) {
+    const int ns = (int)srcs[i].size();
+    b->rc = ns > 0 ? fn(user, dv.data(), n, refs[i], srcs[i].data(), ns, b->idx.get(), b->val.get()) : 0;
+  };
+  const int nt = fusion_threads();
+  std::vector<uint32_t> pass;     // per pixel: the candidates (views j) whose angle test passes
+  std::vector<float> wgt;         // their exp(-tmp_index), at p * ns + j
+  std::thread worker;
+  fetch(0, &buf[0]);
+  for (int i = 0; i < n; ++i) {
+    if (worker.joinable()) worker.join();
+    if (i + 1 < n) worker = std::thread(fetch, i + 1, &buf[(i + 1) & 1]);
+    const Cand& b = buf[i & 1];
+    if (b.rc != 0) {
+      if (worker.joinable()) worker.join();
+      err = "fusion candidates failed (" + std::to_string(b.rc) + ")";
+      return false;
     }
-    std::vector<int> used(ns);
+    FusionView& R = views[refs[i]];
+    const int cols = R.view.width, rows = R.view.height;
+    const std::vector<int>& src = srcs[i];
+    const int ns = (int)src.size();   // <= DPE_MAX_IMAGES - 1: one bit per view
+    const size_t L = (size_t)cols * rows;
+    const int32_t* cidx = b.idx.get();
+    const float* cval = b.val.get();
+    pass.assign(L, 0u);
+    wgt.resize(L * (size_t)std::max(ns, 1));
+    if (ns > 0) {   // mask-independent part of DPE.cpp:1318-1343, on host threads
+      std::vector<std::thread> pool;
+      for (int t = 0; t < nt; ++t)
+        pool.emplace_back([&, t]() {
+          const size_t lo = L * t / nt, hi = L * (t + 1) / nt;
+          for (size_t p = lo; p < hi; ++p) {
+            if (!(R.view.depth[p] > 0.0f)) continue;
+            uint32_t m = 0;
+            for (int j = 0; j < ns; ++j) {
+              if (cidx[p * ns + j] < 0) continue;
+              const float* v = cval + (p * ns + j) * 3;
+              float angle = std::acos(v[2]);                 // GetAngle (DPE.cpp:1208-1217)
+              if (angle != angle) angle = 0.0f;
+              if (angle < 0.174533f) {                       // reproj < 2, rel < 0.01 tested by the candidates
+                const float tmp_index = v[0] + 200 * v[1] + angle * 10;
+                wgt[p * ns + j] = std::exp(-tmp_index);
+                m |= 1u << j;
+              }
+            }
+            pass[p] = m;
+          }
+        });
+      for (auto& th : pool) th.join();
+    }
+    int used[32];
     for (int r = 0; r < rows; ++r)
       for (int c = 0; c < cols; ++c) {
         const size_t p = (size_t)r * cols + c;
@@ -57,33 +133,27 @@ bool run_fusion(std::vector<FusionView>& views, dpe_fusion_fn fn, void* user, st
         if (R.mask[p] == 1) continue;
         const float ref_depth = R.view.depth[p];
         if (ref_depth <= 0.0) continue;
-        int num_consistent = 0;
+        int num_consistent = 0, nused = 0;
         float dyn = 0.0f;
-        for (int j = 0; j < ns; ++j) {
-          used[j] = -1;
+        for (uint32_t m = pass[p]; m; m &= m - 1) {
+          const int j = __builtin_ctz(m);
           const int32_t sp = cidx[p * ns + j];
-          if (sp < 0) continue;
           if (views[src[j]].mask[sp] == 1) continue;
-          const float* v = cval.data() + (p * ns + j) * 3;
-          float angle = std::acos(v[2]);                     // GetAngle (DPE.cpp:1208-1217)
-          if (angle != angle) angle = 0.0f;
-          if (angle < 0.174533f) {                           // reproj < 2, rel < 0.01 tested by the candidates
-            used[j] = sp;
-            const float tmp_index = v[0] + 200 * v[1] + angle * 10;
-            dyn += std::exp(-tmp_index);
-            num_consistent++;
-          }
+          used[nused++] = j;
+          dyn += wgt[p * ns + j];
+          num_consistent++;
         }
         const float factor = R.weak[p] == DPE_WEAK ? 0.45f : 0.3f;
         if (num_consistent >= 1 && dyn > factor * num_consistent) {
           float col[3] = {(float)R.bgr[3 * p], (float)R.bgr[3 * p + 1], (float)R.bgr[3 * p + 2]};
-          for (int j = 0; j < ns; ++j) {
-            if (used[j] < 0) continue;
+          for (int k = 0; k < nused; ++k) {
+            const int j = used[k];
+            const size_t sp = (size_t)cidx[p * ns + j];
             FusionView& S = views[src[j]];
-            S.mask[used[j]] = 1;
-            col[0] += S.bgr[3 * (size_t)used[j]];
-            col[1] += S.bgr[3 * (size_t)used[j] + 1];
-            col[2] += S.bgr[3 * (size_t)used[j] + 2];
+            S.mask[sp] = 1;
+            col[0] += S.bgr[3 * sp];
+            col[1] += S.bgr[3 * sp + 1];
+            col[2] += S.bgr[3 * sp + 2];
           }
           for (float& x : col) x /= (num_consistent + 1);
           const FusedPoint pt = fusion_point(c, r, ref_depth, R.view.cam, col);
@@ -91,6 +161,7 @@ bool run_fusion(std::vector<FusionView>& views, dpe_fusion_fn fn, void* user, st
         }
       }
   }
+  if (worker.joinable()) worker.join();
   return true;
 }
 

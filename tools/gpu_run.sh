@@ -9,12 +9,14 @@
 #   timeline     overlapped kernel trace (tools/timeline.py) pmc          PMC traffic + bottleneck passes
 #   rehearsal    `bench.py --gpus 2` over gloo on one GPU    ab:<a.so,b.so,...>  interleaved A/B (tools/ab_libs.py)
 #   phase:<so>   phase profile of a DPE_DIAG build
+#   run:<cmd>    any command (quote the step: "run:DPE_DBG_GN_ONCE=1 python -u tools/gn_ceiling.py 10")
 cd "$GRAFT_REPO_ROOT" || exit 1
 export PYTHONUNBUFFERED=1
 mkdir -p gpurun_out
 R=$GRAFT_REPO_ROOT
 tag=$1; shift
 [ -n "$tag" ] || { echo "usage: gpu_run.sh TAG STEP..."; exit 2; }
+nrun=0
 PT="python -u -m pytest -p no:cacheprovider --timeout 900 --timeout-method thread"
 for step in "$@"; do
   name=${step%%:*}; arg=${step#*:}; [ "$arg" = "$step" ] && arg=
@@ -38,6 +40,8 @@ for step in "$@"; do
                --no-pass-types --no-config5 > "$log" 2>&1) ;;
     ab)     (cd "$R" && AB_ROUNDS=${AB_ROUNDS:-5} timeout -k 10 600 python -u tools/ab_libs.py ${arg//,/ } > "$log" 2>&1) ;;
     phase)  (cd "$R" && timeout -k 10 200 python -u tools/phase_prof.py "$arg" > "$log" 2>&1) ;;
+    run)    log=$R/gpurun_out/${tag}_run$((++nrun)).log
+            (cd "$R" && timeout -k 10 400 env $arg > "$log" 2>&1) ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
   rc=$?
