@@ -1332,6 +1332,15 @@ extern "C" void dpe_state_clear(DpeContext* c) {
   c->snap_mode = false;
 }
 
+extern "C" int dpe_host_pin(void* ptr, size_t bytes) {
+  if (!ptr || bytes == 0) return DPE_ERR_ARG;
+  return hipHostRegister(ptr, bytes, hipHostRegisterDefault) == hipSuccess ? DPE_OK : DPE_ERR_HIP;
+}
+extern "C" int dpe_host_unpin(void* ptr) {
+  if (!ptr) return DPE_ERR_ARG;
+  return hipHostUnregister(ptr) == hipSuccess ? DPE_OK : DPE_ERR_HIP;
+}
+
 extern "C" int dpe_fusion_stage(DpeContext* c, const DpeFusionView* views, int n) {
   g_err.clear();
   if (!c || !views || n < 1) { g_err = "dpe_fusion_stage: bad argument"; return DPE_ERR_ARG; }

@@ -19,6 +19,8 @@
 #include <cstring>
 #include <fstream>
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <memory>
 #include <thread>
@@ -73,7 +75,22 @@ bool run_fusion(std::vector<FusionView>& views, dpe_fusion_fn fn, void* user, st
     int rc = 0;
   };
   Cand buf[2];
-  for (Cand& b : buf) { b.idx.reset(new int32_t[cap]); b.val.reset(new float[cap * 3]); }
+  // page-locked when the runtime allows (the candidate copies are ~16 B per (pixel, source view))
+  struct Pin {
+    void* p = nullptr;
+    void pin(void* q, size_t n) { if (dpe_host_pin(q, n) == DPE_OK) p = q; }
+    ~Pin() { if (p) dpe_host_unpin(p); }
+  } pins[4];
+  for (int k = 0; k < 2; ++k) {
+    buf[k].idx.reset(new int32_t[cap]);
+    buf[k].val.reset(new float[cap * 3]);
+    pins[2 * k].pin(buf[k].idx.get(), cap * sizeof(int32_t));
+    pins[2 * k + 1].pin(buf[k].val.get(), cap * 3 * sizeof(float));
+  }
+  // DPE_FUSION_PROFILE=1: seconds waiting for candidates, in the parallel terms, in the serial walk
+  static const bool prof = [] { const char* e = getenv("DPE_FUSION_PROFILE"); return e && atoi(e) != 0; }();
+  double t_wait = 0, t_terms = 0, t_walk = 0;
+  auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
   auto fetch = [&](int i, Cand* b) {
     const int ns = (int)srcs[i].size();
     b->rc = ns > 0 ? fn(user, dv.data(), n, refs[i], srcs[i].data(), ns, b->idx.get(), b->val.get()) : 0;
@@ -84,7 +101,9 @@ bool run_fusion(std::vector<FusionView>& views, dpe_fusion_fn fn, void* user, st
   std::thread worker;
   fetch(0, &buf[0]);
   for (int i = 0; i < n; ++i) {
+    double t0 = now();
     if (worker.joinable()) worker.join();
+    t_wait += now() - t0;
     if (i + 1 < n) worker = std::thread(fetch, i + 1, &buf[(i + 1) & 1]);
     const Cand& b = buf[i & 1];
     if (b.rc != 0) {
@@ -101,6 +120,7 @@ bool run_fusion(std::vector<FusionView>& views, dpe_fusion_fn fn, void* user, st
     const float* cval = b.val.get();
     pass.assign(L, 0u);
     wgt.resize(L * (size_t)std::max(ns, 1));
+    t0 = now();
     if (ns > 0) {   // mask-independent part of DPE.cpp:1318-1343, on host threads
       std::vector<std::thread> pool;
       for (int t = 0; t < nt; ++t)
@@ -125,6 +145,8 @@ bool run_fusion(std::vector<FusionView>& views, dpe_fusion_fn fn, void* user, st
         });
       for (auto& th : pool) th.join();
     }
+    t_terms += now() - t0;
+    t0 = now();
     int used[32];
     for (int r = 0; r < rows; ++r)
       for (int c = 0; c < cols; ++c) {
@@ -160,8 +182,12 @@ bool run_fusion(std::vector<FusionView>& views, dpe_fusion_fn fn, void* user, st
           cloud.push_back(pt);
         }
       }
+    t_walk += now() - t0;
   }
   if (worker.joinable()) worker.join();
+  if (prof)
+    fprintf(stderr, "fusion: %d images, wait for candidates %.3f s, angle/weight terms %.3f s, serial walk %.3f s, "
+            "%zu points\n", n, t_wait, t_terms, t_walk, cloud.size());
   return true;
 }
 

@@ -758,16 +758,20 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
     if (rank == 0) {
       std::vector<FusionView> views(problems.size());
       const bool use_block = fs::exists(fs::path(dense) / "blocks");
-      for (size_t i = 0; i < problems.size(); ++i) {
+      // each view's camera, colour image (decode + RescaleImageAndCamera) and block mask on its own
+      // host thread (independent files, independent outputs)
+      std::vector<std::string> verr(problems.size());
+      auto load_view = [&](size_t i) -> bool {
+        std::string& err = verr[i];
         const Problem& p = problems[i];
         FusionView& v = views[i];
         const ImageState& st = all.at(p.ref_image_id);
         v.image_id = p.ref_image_id;
         v.src_ids = p.src_image_ids;
         DpeCamera cam;
-        if (!read_camera((fs::path(dense) / "cams" / (fmt_index(p.ref_image_id) + "_cam.txt")).string(), cam, err)) return 1;
+        if (!read_camera((fs::path(dense) / "cams" / (fmt_index(p.ref_image_id) + "_cam.txt")).string(), cam, err)) return false;
         ColorImage img;
-        if (!read_bgr((fs::path(dense) / "images" / (fmt_index(p.ref_image_id) + ".jpg")).string(), img, err)) return 1;
+        if (!read_bgr((fs::path(dense) / "images" / (fmt_index(p.ref_image_id) + ".jpg")).string(), img, err)) return false;
         if (img.w != st.w || img.h != st.h) {   // RescaleImageAndCamera (DPE.cpp:1123-1144), per channel
           const float sx = st.w / (float)img.w, sy = st.h / (float)img.h;
           std::vector<uint8_t> ch((size_t)img.w * img.h), och((size_t)st.w * st.h);
@@ -784,8 +788,8 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
         cam.width = st.w; cam.height = st.h;
         if (use_block) {
           GrayImage b;
-          if (!read_gray((fs::path(dense) / "blocks" / ("mask_" + std::to_string(p.ref_image_id) + ".jpg")).string(), b, err)) return 1;
-          if (b.w != st.w || b.h != st.h) { err = "block mask size differs from the depth map"; return 1; }
+          if (!read_gray((fs::path(dense) / "blocks" / ("mask_" + std::to_string(p.ref_image_id) + ".jpg")).string(), b, err)) return false;
+          if (b.w != st.w || b.h != st.h) { err = "block mask size differs from the depth map"; return false; }
           v.block = std::move(b.px);
         }
         v.view.width = st.w; v.view.height = st.h;
@@ -793,6 +797,19 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
         v.view.depth = st.depth.data();
         v.view.normal = st.normal.data();
         v.weak = st.weak.data();
+        return true;
+      };
+      {
+        const size_t nv = problems.size();
+        const int nt = (int)std::min<size_t>(nv, std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency())));
+        std::vector<std::thread> pool;
+        for (int t = 0; t < nt; ++t)
+          pool.emplace_back([&, t]() {
+            for (size_t i = t; i < nv; i += nt)
+              if (!load_view(i) && verr[i].empty()) verr[i] = "fusion view load failed";
+          });
+        for (auto& th : pool) th.join();
+        for (auto& e : verr) if (!e.empty()) { err = e; return 1; }
       }
       NativeFusion nf;
       dpe_fusion_fn ffn = opt.fusion_runner;

@@ -311,6 +311,12 @@ int dpe_fusion_stage(DpeContext* ctx, const DpeFusionView* views, int n_views);
  * HOST output buffers of W*H*ns int32 / W*H*ns*3 floats.  Synchronous. */
 int dpe_fusion_candidates(DpeContext* ctx, int ref, const int* src, int ns, int32_t* idx, float* val);
 
+/* Page-locks (pins) / releases a caller's host buffer so that device -> host copies into it run at
+ * full PCIe rate (hipHostRegister; the host fusion pins its candidate buffers).  Nonzero when the
+ * runtime refuses (no device, limits): the buffer then stays pageable and every call still works. */
+int dpe_host_pin(void* ptr, size_t bytes);
+int dpe_host_unpin(void* ptr);
+
 #ifdef __cplusplus
 }
 #endif
