@@ -41,7 +41,7 @@ FLOP_PER_HOMOGRAPHY = 120
 FLOP_PER_GEOM = 60
 MODEL_FLOP_PER_PX = (36 * FLOP_PER_TAP + FLOP_PER_HOMOGRAPHY) * (42 * (NV_ - 1) + 75 * 4)   # 0.86 MFLOP
 # per-dispatch HBM bytes from the committed PMC passes (tools/pmc.sh + tools/prof_summary.py)
-PMC_JSON = next((os.path.join(ROOT, "profiles", f) for f in ("r05_pmc.json", "r04f_pmc.json", "r04_pmc.json", "r03s2_pmc.json", "r03_pmc.json", "r02_pmc.json")
+PMC_JSON = next((os.path.join(ROOT, "profiles", f) for f in ("r06_pmc.json", "r05_pmc.json", "r04f_pmc.json", "r04_pmc.json", "r03s2_pmc.json", "r03_pmc.json", "r02_pmc.json")
                  if os.path.exists(os.path.join(ROOT, "profiles", f))), os.path.join(ROOT, "profiles", "r04_pmc.json"))
 CLASS_KERNEL = {"strong": "k_strong_coop", "weak": "k_weak_coop", "depth_to_weak": "k_depth_to_weak",
                 "local_refine": "k_local_refine_jobs", "init": "k_random_init", "ransac": "k_ransac_fit",
@@ -543,10 +543,11 @@ def main():
             "frac": round(achieved_tflops / FP32_PEAK_TFLOPS, 4),
             "traffic": pmc_traffic(dom),
             "traffic_source": os.path.relpath(PMC_JSON, ROOT) + " (FETCH_SIZE x2 x1024 + WRITE_SIZE x1024, per launch)",
-            "note": "no MFMA-shaped work: priced against the f32 vector peak; neither VALU issue nor the texture-"
-                    "address path bounds the tap loops alone (each 55-75 % busy; removing the gathers or two "
-                    "clamps per tap moves the strong sweep <= 3 %, shortening the per-tap dependency chain 4 %: "
-                    "DESIGN.md s3, s8). achieved = "
+            "note": "no MFMA-shaped work: priced against the f32 vector peak.  The tap loops keep the VALU "
+                    "occupied ~100 % of the time (~70 % in throughput terms, the rest dependency stalls); making "
+                    "every texel gather free moves the strong sweep by nothing and DepthToWeak by 5.7 % "
+                    "(profiles/r06a_ab_fake_gather.log, DESIGN.md s3), so HBM / gather bandwidth does not bound "
+                    "them. achieved = "
                     "algorithmic FLOP per launch (120/homography + 32/bilinear tap + 60/geom term, counted on "
                     "device) / avg launch time (hipEvents on the pass stream)",
             "avg_launch_ms": round(avg_launch_ms, 3),

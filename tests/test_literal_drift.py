@@ -1,9 +1,9 @@
-"""What the oracle's restatement choices cost: the restated oracle against its ORACLE_LITERAL builds and the ORACLE_RCP_IEEE build (choice 8 off)
+"""What the oracle's restatement choices cost: the restated oracle against its ORACLE_LITERAL builds
 (oracle/dpe_oracle.cpp: ComputeHomography / ComputeCorrespondingPoint / tex2D(pt + 0.5f) evaluated as
 DPE.cu:453-522, 734-736 write them; literal 1 with IEEE division, literal 2 with a * (1 / b) as a
-model of --use_fast_math), same inputs and Philox seeds, through one pass and through the 8-pass
-coarse-to-fine schedule (tools/literal_drift.py, numbers in DESIGN.md §4 and
-profiles/r04_literal_drift.json).
+model of --use_fast_math; choices 3, 7 and 8 off) and against the ORACLE_RCP_IEEE build (choice 8
+alone off), same inputs and Philox seeds, through one pass and through the 8-pass coarse-to-fine
+schedule (tools/literal_drift.py, numbers in DESIGN.md §4 and profiles/r06_rcp_choice8_drift.json).
 
 Parity stays unpinned (no reference vectors): this measures the distance between the restatement
 and the reference's literal float32 semantics, and sets it beside PatchMatch's own spread (the
