@@ -43,6 +43,23 @@ def test_library_loads_without_gpu():
         assert getattr(p, name) == pytest.approx(getattr(ref, name)), name
 
 
+def test_host_pin_refuses_gracefully_without_gpu():
+    """dpe_host_pin / dpe_host_unpin (the host fusion's pinned candidate buffers): an argument error
+    for a null buffer, and a runtime refusal -- not a crash -- where no device is present (here);
+    callers then keep the buffer pageable."""
+    import numpy as np
+    lib = C.CDLL(LIB)
+    lib.dpe_host_pin.argtypes = [C.c_void_p, C.c_size_t]
+    lib.dpe_host_unpin.argtypes = [C.c_void_p]
+    assert lib.dpe_host_pin(None, 16) == -1          # DPE_ERR_ARG
+    a = np.zeros(1 << 16, np.uint8)
+    rc = lib.dpe_host_pin(a.ctypes.data, a.nbytes)
+    if rc == 0:                      # a GPU is present: pinning works and is undone
+        assert lib.dpe_host_unpin(a.ctypes.data) == 0
+    else:
+        assert rc < 0
+
+
 def test_struct_layouts():
     assert C.sizeof(_abi.DpeCamera) == 112
     offs = {n: getattr(_abi.DpePatchMatchParams, n).offset for n, _ in _abi.DpePatchMatchParams._fields_}

@@ -208,3 +208,41 @@ def test_gpu_pipeline_fusion_ply_matches_cpu(tmp_path, fused):
     from DPE_MVS import dpe_mvs
     assert dpe_mvs(a, 0, False, True, False, True, False, False, False) == 0       # HIP pass + HIP fusion tests
     assert open(os.path.join(a, "DPE", "DPE.ply"), "rb").read() == open(os.path.join(fused, "DPE", "DPE.ply"), "rb").read()
+
+
+@pytest.mark.gpu
+def test_gpu_candidates_into_pinned_buffers(fused):
+    """The host fusion pins its candidate buffers (dpe_host_pin): the copies into page-locked memory
+    give the same candidates as into pageable memory, and unpinning succeeds."""
+    from DPE_MVS import native
+    lib = native.load_library()
+    lib.dpe_host_pin.argtypes = [C.c_void_p, C.c_size_t]
+    lib.dpe_host_unpin.argtypes = [C.c_void_p]
+    views = _final_views(fused, 4)
+    keep = []
+    arr = (_abi.DpeFusionView * 4)()
+    for k, v in enumerate(views):
+        d, n = np.ascontiguousarray(v["depth"], np.float32), np.ascontiguousarray(v["normal"], np.float32)
+        keep += [d, n]
+        arr[k] = _abi.DpeFusionView(d.shape[1], d.shape[0], v["cam"], d.ctypes.data, n.ctypes.data)
+    ctx = lib.dpe_create(0)
+    try:
+        lib.dpe_fusion_stage.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+        lib.dpe_fusion_candidates.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+        assert lib.dpe_fusion_stage(ctx, arr, 4) == 0
+        src = np.array(views[0]["src_ids"], np.int32)
+        L = views[0]["depth"].size
+        gi, gv = np.empty(L * len(src), np.int32), np.empty(L * len(src) * 3, np.float32)
+        pi, pv = np.empty_like(gi), np.empty_like(gv)
+        assert lib.dpe_host_pin(pi.ctypes.data, pi.nbytes) == 0 and lib.dpe_host_pin(pv.ctypes.data, pv.nbytes) == 0
+        try:
+            assert lib.dpe_fusion_candidates(ctx, 0, src.ctypes.data, len(src), gi.ctypes.data, gv.ctypes.data) == 0
+            assert lib.dpe_fusion_candidates(ctx, 0, src.ctypes.data, len(src), pi.ctypes.data, pv.ctypes.data) == 0
+            assert np.array_equal(gi, pi)
+            m = np.repeat(gi >= 0, 3)
+            assert np.array_equal(gv[m].view(np.uint32), pv[m].view(np.uint32))
+        finally:
+            assert lib.dpe_host_unpin(pi.ctypes.data) == 0 and lib.dpe_host_unpin(pv.ctypes.data) == 0
+    finally:
+        lib.dpe_destroy(ctx)
+
