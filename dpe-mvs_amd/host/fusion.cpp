@@ -148,9 +148,14 @@ bool run_fusion(std::vector<FusionView>& views, dpe_fusion_fn fn, void* user, st
     t_terms += now() - t0;
     t0 = now();
     int used[32];
+    uint8_t* smask[32];
+    for (int j = 0; j < ns; ++j) smask[j] = views[src[j]].mask.data();
     for (int r = 0; r < rows; ++r)
       for (int c = 0; c < cols; ++c) {
         const size_t p = (size_t)r * cols + c;
+        // no candidate passes the angle test: the reference's loop finds num_consistent = 0 and
+        // keeps nothing, whatever the masks say
+        if (!pass[p]) continue;
         if (!R.block.empty() && R.block[p] < 128) continue;
         if (R.mask[p] == 1) continue;
         const float ref_depth = R.view.depth[p];
@@ -160,7 +165,7 @@ bool run_fusion(std::vector<FusionView>& views, dpe_fusion_fn fn, void* user, st
         for (uint32_t m = pass[p]; m; m &= m - 1) {
           const int j = __builtin_ctz(m);
           const int32_t sp = cidx[p * ns + j];
-          if (views[src[j]].mask[sp] == 1) continue;
+          if (smask[j][sp] == 1) continue;
           used[nused++] = j;
           dyn += wgt[p * ns + j];
           num_consistent++;
@@ -172,7 +177,7 @@ bool run_fusion(std::vector<FusionView>& views, dpe_fusion_fn fn, void* user, st
             const int j = used[k];
             const size_t sp = (size_t)cidx[p * ns + j];
             FusionView& S = views[src[j]];
-            S.mask[sp] = 1;
+            smask[j][sp] = 1;
             col[0] += S.bgr[3 * sp];
             col[1] += S.bgr[3 * sp + 1];
             col[2] += S.bgr[3 * sp + 2];
