@@ -219,6 +219,8 @@ struct NativeFusion {
   DpeContext* ctx = nullptr;
   bool own = false;
   const DpeFusionView* staged = nullptr;
+  std::string err;   // the library's message of a failed call (run_fusion calls from a worker thread,
+                     // and dpe_last_error() is per thread)
   ~NativeFusion() { if (own && ctx) dpe_destroy(ctx); }
 };
 int native_fusion(void* user, const DpeFusionView* views, int n, int ref, const int* src, int ns, int32_t* idx,
@@ -226,10 +228,12 @@ int native_fusion(void* user, const DpeFusionView* views, int n, int ref, const 
   NativeFusion* f = static_cast<NativeFusion*>(user);
   if (f->staged != views) {
     const int r = dpe_fusion_stage(f->ctx, views, n);
-    if (r != DPE_OK) return r;
+    if (r != DPE_OK) { f->err = dpe_last_error(); return r; }
     f->staged = views;
   }
-  return dpe_fusion_candidates(f->ctx, ref, src, ns, idx, val);
+  const int r = dpe_fusion_candidates(f->ctx, ref, src, ns, idx, val);
+  if (r != DPE_OK) f->err = dpe_last_error();
+  return r;
 }
 
 // the per-pass intermediate maps of the reference (main.cpp:439-446)
@@ -825,7 +829,7 @@ int run(const char* dense_folder, const DpePipelineOptions& opt) {
       }
       std::vector<FusedPoint> cloud;
       if (!run_fusion(views, ffn, fuser, cloud, err)) {
-        if (!opt.fusion_runner) err += std::string(": ") + dpe_last_error();
+        if (!opt.fusion_runner) err += std::string(": ") + (nf.err.empty() ? std::string(dpe_last_error()) : nf.err);
         return 1;
       }
       if (!export_point_cloud((fs::path(dense) / kOutName / "DPE.ply").string(), cloud, err)) return 1;
