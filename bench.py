@@ -236,15 +236,20 @@ def pipeline_config(dist, rank: int, world: int, local_rank: int, name: str) -> 
     import torch
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    pipeline.run_dpe_pipeline(folder, gpu_index=local_rank, verbose=False, fusion=cfg["fusion"],
-                              dist=dist if world > 1 else None)
+    error = None
+    try:   # a failed run is reported in the line (the pipeline fails every rank at the same exchange);
+        # every rank still joins the timing all-gather below, so the ranks stay in step
+        pipeline.run_dpe_pipeline(folder, gpu_index=local_rank, verbose=False, fusion=cfg["fusion"],
+                                  dist=dist if world > 1 else None)
+    except Exception as e:  # noqa: BLE001
+        error = f"{type(e).__name__}: {e}"[:400]
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     import ctypes
     ph = (ctypes.c_double * 8)()
     pipeline.lib().dpe_pipeline_last_timings(ph, 8)
     # per rank: wall, pass work, depth exchanges (status + export + all-gather + import), EdgeSegment, fusion
-    mine = [dt, ph[6], ph[5], ph[2], ph[7]]
+    mine = [float("nan") if error else dt, ph[6], ph[5], ph[2], ph[7]]
     per_rank = [mine]
     if dist:
         t = torch.tensor(mine, dtype=torch.float64, device="cuda" if dist.get_backend() == "nccl" else "cpu")
@@ -252,9 +257,12 @@ def pipeline_config(dist, rank: int, world: int, local_rank: int, name: str) -> 
         dist.all_gather(allr, t)
         per_rank = [[float(v) for v in a.tolist()] for a in allr]
         dist.barrier()
-    dt = max(p[0] for p in per_rank)
     if rank == 0:
         shutil.rmtree(folder, ignore_errors=True)
+    if error or any(p[0] != p[0] for p in per_rank):
+        return {"config": cfg["label"], "ranks": world, "error": error or "failed on another rank",
+                "measured_on_hardware": False}
+    dt = max(p[0] for p in per_rank)
     passes = [round(p[1], 3) for p in per_rank]
     rehearsal = bool(dist) and dist.get_backend() != "nccl"
     out = {"config": cfg["label"], "images": n, "width": W, "height": H, "src_views": min(cfg["max_src"], n - 1),

@@ -12,6 +12,7 @@ import os
 import shutil
 import socket
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -442,3 +443,17 @@ def test_cli_runs_on_gpu(tmp_path, dense4):
     assert "All done" in r.stdout
     for f in OUTS:
         assert os.path.exists(os.path.join(a, "DPE", "00000003", f))
+
+
+@pytest.mark.gpu
+def test_gpu_torch_nccl_hooks_single_rank():
+    """The torch "nccl" (RCCL) all-gather hooks that bench.py's multi-GPU pipeline lines and
+    dpe_mvs(dist=...) hand the C++ pipeline: the device hook on the library's own HBM buffers and the
+    host hook, called as the pipeline calls them, through a real RCCL communicator (one rank: the
+    box has one GPU; the multi-rank transport is the driver's 8-GPU run)."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "torch_hooks_probe.py")], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "HOOKS_OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
