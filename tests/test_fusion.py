@@ -246,3 +246,30 @@ def test_gpu_candidates_into_pinned_buffers(fused):
     finally:
         lib.dpe_destroy(ctx)
 
+
+
+def test_fusion_with_block_masks_matches_serial_runfusion(tmp_path):
+    """dense_folder/blocks/mask_<id>.jpg (DPE.cpp:1252-1262, 1290-1292): reference pixels whose block
+    mask is < 128 are skipped.  The round-6 fusion (parallel terms, sparse serial walk) gives the
+    serial restatement's points bit for bit with the masks present, and fewer points than without."""
+    from PIL import Image
+    d = str(tmp_path / "blk")
+    synthetic.write_dense_folder(d, 64, 48, 4)
+    os.makedirs(os.path.join(d, "blocks"))
+    for i in range(4):
+        m = np.zeros((48, 64), np.uint8)
+        m[:, 16 + 6 * i:] = 255
+        Image.fromarray(m, mode="L").save(os.path.join(d, "blocks", f"mask_{i}.jpg"), quality=95)
+    assert pipeline.run_dpe_pipeline(d, runner=oracle_runner(), fusion_runner=oracle.fusion_runner(), fusion=True,
+                                     verbose=False, keep_intermediate=True) == 0
+    xyz, bgr = read_ply(os.path.join(d, "DPE", "DPE.ply"))
+    views = _final_views(d, 4)
+    for i, v in enumerate(views):
+        v["block"] = pipeline.read_gray(os.path.join(d, "blocks", f"mask_{i}.jpg"))
+    ref = oracle.run_fusion(views)
+    assert ref.shape[0] == xyz.shape[0] > 0
+    assert np.array_equal(ref[:, :3].view(np.uint32), xyz.view(np.uint32))
+    assert np.array_equal(ref[:, 3:].astype(np.uint8), bgr)
+    for v in views:
+        v["block"] = None
+    assert oracle.run_fusion(views).shape[0] > xyz.shape[0]
