@@ -89,110 +89,156 @@ bool run_fusion(std::vector<FusionView>& views, dpe_fusion_fn fn, void* user, st
   }
   // DPE_FUSION_PROFILE=1: seconds waiting for candidates, in the parallel terms, in the serial walk
   static const bool prof = [] { const char* e = getenv("DPE_FUSION_PROFILE"); return e && atoi(e) != 0; }();
-  double t_wait = 0, t_terms = 0, t_walk = 0;
+  double t_wait = 0, t_terms = 0, t_walk = 0, t_points = 0;
   auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
   auto fetch = [&](int i, Cand* b) {
     const int ns = (int)srcs[i].size();
     b->rc = ns > 0 ? fn(user, dv.data(), n, refs[i], srcs[i].data(), ns, b->idx.get(), b->val.get()) : 0;
   };
   const int nt = fusion_threads();
-  std::vector<uint32_t> pass;     // per pixel: the candidates (views j) whose angle test passes
-  std::vector<float> wgt;         // their exp(-tmp_index), at p * ns + j
+  // per image: the candidates whose angle test passes (bit j of pass[p]) and their weights
+  struct Terms {
+    std::vector<uint32_t> pass;
+    std::vector<float> wgt;
+  };
+  Terms terms[2];
+  auto make_terms = [&](int i, const Cand* b, Terms* tm, int threads) {   // DPE.cpp:1318-1343 without the masks
+    const FusionView& R = views[refs[i]];
+    const int ns = (int)srcs[i].size();
+    const size_t L = (size_t)R.view.width * R.view.height;
+    tm->pass.assign(L, 0u);
+    tm->wgt.resize(L * (size_t)std::max(ns, 1));
+    if (ns == 0) return;
+    const int32_t* cidx = b->idx.get();
+    const float* cval = b->val.get();
+    uint32_t* pass = tm->pass.data();
+    float* wgt = tm->wgt.data();
+    std::vector<std::thread> pool;
+    for (int t = 0; t < threads; ++t)
+      pool.emplace_back([&, t]() {
+        const size_t lo = L * t / threads, hi = L * (t + 1) / threads;
+        for (size_t p = lo; p < hi; ++p) {
+          if (!(R.view.depth[p] > 0.0f)) continue;
+          if (!R.block.empty() && R.block[p] < 128) continue;     // skipped by the walk in any case
+          uint32_t m = 0;
+          for (int j = 0; j < ns; ++j) {
+            if (cidx[p * ns + j] < 0) continue;
+            const float* v = cval + (p * ns + j) * 3;
+            float angle = std::acos(v[2]);                 // GetAngle (DPE.cpp:1208-1217)
+            if (angle != angle) angle = 0.0f;
+            if (angle < 0.174533f) {                       // reproj < 2, rel < 0.01 tested by the candidates
+              const float tmp_index = v[0] + 200 * v[1] + angle * 10;
+              wgt[p * ns + j] = std::exp(-tmp_index);
+              m |= 1u << j;
+            }
+          }
+          pass[p] = m;
+        }
+      });
+    for (auto& th : pool) th.join();
+  };
+  // the fused pixels of one image in walk order: pixel, depth, the candidates it used (bit j)
+  struct Fused {
+    uint32_t p, used;
+    float depth;
+  };
+  std::vector<Fused> fused;
   std::thread worker;
+  double t0 = now();
   fetch(0, &buf[0]);
+  if (buf[0].rc == 0) make_terms(0, &buf[0], &terms[0], nt);
+  t_terms += now() - t0;
   for (int i = 0; i < n; ++i) {
-    double t0 = now();
+    t0 = now();
     if (worker.joinable()) worker.join();
     t_wait += now() - t0;
-    if (i + 1 < n) worker = std::thread(fetch, i + 1, &buf[(i + 1) & 1]);
     const Cand& b = buf[i & 1];
     if (b.rc != 0) {
-      if (worker.joinable()) worker.join();
       err = "fusion candidates failed (" + std::to_string(b.rc) + ")";
       return false;
     }
+    // the next image's candidates and terms on the worker (its own threads) while this one is walked
+    if (i + 1 < n)
+      worker = std::thread([&, i]() {
+        Cand* nb = &buf[(i + 1) & 1];
+        fetch(i + 1, nb);
+        if (nb->rc == 0) make_terms(i + 1, nb, &terms[(i + 1) & 1], std::max(1, nt - 1));
+      });
     FusionView& R = views[refs[i]];
     const int cols = R.view.width, rows = R.view.height;
     const std::vector<int>& src = srcs[i];
     const int ns = (int)src.size();   // <= DPE_MAX_IMAGES - 1: one bit per view
-    const size_t L = (size_t)cols * rows;
     const int32_t* cidx = b.idx.get();
-    const float* cval = b.val.get();
-    pass.assign(L, 0u);
-    wgt.resize(L * (size_t)std::max(ns, 1));
+    const uint32_t* pass = terms[i & 1].pass.data();
+    const float* wgt = terms[i & 1].wgt.data();
     t0 = now();
-    if (ns > 0) {   // mask-independent part of DPE.cpp:1318-1343, on host threads
-      std::vector<std::thread> pool;
-      for (int t = 0; t < nt; ++t)
-        pool.emplace_back([&, t]() {
-          const size_t lo = L * t / nt, hi = L * (t + 1) / nt;
-          for (size_t p = lo; p < hi; ++p) {
-            if (!(R.view.depth[p] > 0.0f)) continue;
-            uint32_t m = 0;
-            for (int j = 0; j < ns; ++j) {
-              if (cidx[p * ns + j] < 0) continue;
-              const float* v = cval + (p * ns + j) * 3;
-              float angle = std::acos(v[2]);                 // GetAngle (DPE.cpp:1208-1217)
-              if (angle != angle) angle = 0.0f;
-              if (angle < 0.174533f) {                       // reproj < 2, rel < 0.01 tested by the candidates
-                const float tmp_index = v[0] + 200 * v[1] + angle * 10;
-                wgt[p * ns + j] = std::exp(-tmp_index);
-                m |= 1u << j;
-              }
-            }
-            pass[p] = m;
-          }
-        });
-      for (auto& th : pool) th.join();
-    }
-    t_terms += now() - t0;
-    t0 = now();
-    int used[32];
     uint8_t* smask[32];
     for (int j = 0; j < ns; ++j) smask[j] = views[src[j]].mask.data();
+    fused.clear();
     for (int r = 0; r < rows; ++r)
       for (int c = 0; c < cols; ++c) {
         const size_t p = (size_t)r * cols + c;
-        // no candidate passes the angle test: the reference's loop finds num_consistent = 0 and
-        // keeps nothing, whatever the masks say
+        // no candidate passes the angle test (or the pixel is blocked / has no depth): the
+        // reference's loop finds num_consistent = 0 and keeps nothing, whatever the masks say
         if (!pass[p]) continue;
-        if (!R.block.empty() && R.block[p] < 128) continue;
         if (R.mask[p] == 1) continue;
         const float ref_depth = R.view.depth[p];
-        if (ref_depth <= 0.0) continue;
-        int num_consistent = 0, nused = 0;
+        int num_consistent = 0;
+        uint32_t used = 0;
         float dyn = 0.0f;
         for (uint32_t m = pass[p]; m; m &= m - 1) {
           const int j = __builtin_ctz(m);
           const int32_t sp = cidx[p * ns + j];
           if (smask[j][sp] == 1) continue;
-          used[nused++] = j;
+          used |= 1u << j;
           dyn += wgt[p * ns + j];
           num_consistent++;
         }
         const float factor = R.weak[p] == DPE_WEAK ? 0.45f : 0.3f;
         if (num_consistent >= 1 && dyn > factor * num_consistent) {
-          float col[3] = {(float)R.bgr[3 * p], (float)R.bgr[3 * p + 1], (float)R.bgr[3 * p + 2]};
-          for (int k = 0; k < nused; ++k) {
-            const int j = used[k];
-            const size_t sp = (size_t)cidx[p * ns + j];
-            FusionView& S = views[src[j]];
-            smask[j][sp] = 1;
-            col[0] += S.bgr[3 * sp];
-            col[1] += S.bgr[3 * sp + 1];
-            col[2] += S.bgr[3 * sp + 2];
+          for (uint32_t m = used; m; m &= m - 1) {
+            const int j = __builtin_ctz(m);
+            smask[j][cidx[p * ns + j]] = 1;
           }
-          for (float& x : col) x /= (num_consistent + 1);
-          const FusedPoint pt = fusion_point(c, r, ref_depth, R.view.cam, col);
-          cloud.push_back(pt);
+          fused.push_back(Fused{(uint32_t)p, used, ref_depth});
         }
       }
     t_walk += now() - t0;
+    // colours and 3-D points of the fused pixels (DPE.cpp:1345-1366): they read only the images'
+    // colours, which nothing writes, so they run on host threads, each point at its walk position
+    t0 = now();
+    const size_t base = cloud.size(), nf = fused.size();
+    cloud.resize(base + nf);
+    {
+      std::vector<std::thread> pool;
+      const int th = (int)std::min<size_t>((size_t)nt, std::max<size_t>(1, nf / 4096));
+      for (int t = 0; t < th; ++t)
+        pool.emplace_back([&, t]() {
+          for (size_t k = nf * t / th; k < nf * (t + 1) / th; ++k) {
+            const Fused& f = fused[k];
+            const size_t p = f.p;
+            float col[3] = {(float)R.bgr[3 * p], (float)R.bgr[3 * p + 1], (float)R.bgr[3 * p + 2]};
+            for (uint32_t m = f.used; m; m &= m - 1) {
+              const int j = __builtin_ctz(m);
+              const size_t sp = (size_t)cidx[p * ns + j];
+              const FusionView& S = views[src[j]];
+              col[0] += S.bgr[3 * sp];
+              col[1] += S.bgr[3 * sp + 1];
+              col[2] += S.bgr[3 * sp + 2];
+            }
+            const int num_consistent = __builtin_popcount(f.used);
+            for (float& x : col) x /= (num_consistent + 1);
+            cloud[base + k] = fusion_point((int)(p % cols), (int)(p / cols), f.depth, R.view.cam, col);
+          }
+        });
+      for (auto& th2 : pool) th2.join();
+    }
+    t_points += now() - t0;
   }
   if (worker.joinable()) worker.join();
   if (prof)
-    fprintf(stderr, "fusion: %d images, wait for candidates %.3f s, angle/weight terms %.3f s, serial walk %.3f s, "
-            "%zu points\n", n, t_wait, t_terms, t_walk, cloud.size());
+    fprintf(stderr, "fusion: %d images, wait for candidates + terms %.3f s, first image's terms %.3f s, serial walk "
+            "%.3f s, points %.3f s, %zu points\n", n, t_wait, t_terms, t_walk, t_points, cloud.size());
   return true;
 }
 
