@@ -81,16 +81,24 @@ bool run_fusion(std::vector<FusionView>& views, dpe_fusion_fn fn, void* user, st
     void pin(void* q, size_t n) { if (dpe_host_pin(q, n) == DPE_OK) p = q; }
     ~Pin() { if (p) dpe_host_unpin(p); }
   } pins[4];
-  for (int k = 0; k < 2; ++k) {
-    buf[k].idx.reset(new int32_t[cap]);
-    buf[k].val.reset(new float[cap * 3]);
-    pins[2 * k].pin(buf[k].idx.get(), cap * sizeof(int32_t));
-    pins[2 * k + 1].pin(buf[k].val.get(), cap * 3 * sizeof(float));
-  }
-  // DPE_FUSION_PROFILE=1: seconds waiting for candidates, in the parallel terms, in the serial walk
+  // DPE_FUSION_PROFILE=1: seconds pinning, waiting for candidates, in the terms, the walk, the points
   static const bool prof = [] { const char* e = getenv("DPE_FUSION_PROFILE"); return e && atoi(e) != 0; }();
-  double t_wait = 0, t_terms = 0, t_walk = 0, t_points = 0;
+  // DPE_FUSION_PIN=0: pageable candidate buffers (A/B of the pinning)
+  static const bool pin = [] { const char* e = getenv("DPE_FUSION_PIN"); return !(e && atoi(e) == 0); }();
+  double t_wait = 0, t_terms = 0, t_walk = 0, t_points = 0, t_pin = 0;
   auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+  {
+    const double tp = now();
+    for (int k = 0; k < 2; ++k) {
+      buf[k].idx.reset(new int32_t[cap]);
+      buf[k].val.reset(new float[cap * 3]);
+      if (pin) {
+        pins[2 * k].pin(buf[k].idx.get(), cap * sizeof(int32_t));
+        pins[2 * k + 1].pin(buf[k].val.get(), cap * 3 * sizeof(float));
+      }
+    }
+    t_pin = now() - tp;
+  }
   auto fetch = [&](int i, Cand* b) {
     const int ns = (int)srcs[i].size();
     b->rc = ns > 0 ? fn(user, dv.data(), n, refs[i], srcs[i].data(), ns, b->idx.get(), b->val.get()) : 0;
@@ -237,8 +245,9 @@ bool run_fusion(std::vector<FusionView>& views, dpe_fusion_fn fn, void* user, st
   }
   if (worker.joinable()) worker.join();
   if (prof)
-    fprintf(stderr, "fusion: %d images, wait for candidates + terms %.3f s, first image's terms %.3f s, serial walk "
-            "%.3f s, points %.3f s, %zu points\n", n, t_wait, t_terms, t_walk, t_points, cloud.size());
+    fprintf(stderr, "fusion: %d images, buffers + pinning %.3f s, wait for candidates + terms %.3f s, first image "
+            "%.3f s, serial walk %.3f s, points %.3f s, %zu points\n", n, t_pin, t_wait, t_terms, t_walk, t_points,
+            cloud.size());
   return true;
 }
 
