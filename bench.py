@@ -43,6 +43,13 @@ MODEL_FLOP_PER_PX = (36 * FLOP_PER_TAP + FLOP_PER_HOMOGRAPHY) * (42 * (NV_ - 1) 
 # per-dispatch HBM bytes from the committed PMC passes (tools/pmc.sh + tools/prof_summary.py)
 PMC_JSON = next((os.path.join(ROOT, "profiles", f) for f in ("r06_pmc.json", "r05_pmc.json", "r04f_pmc.json", "r04_pmc.json", "r03s2_pmc.json", "r03_pmc.json", "r02_pmc.json")
                  if os.path.exists(os.path.join(ROOT, "profiles", f))), os.path.join(ROOT, "profiles", "r04_pmc.json"))
+# secondary roof (the on-chip gather rate): a 64-lane texel gather costs the texture
+# path at least one CU-cycle per lane quad = 16 CU-cycles (profiles/r03_td_probe2.md), so at the
+# ~2.4 GHz the chip holds a CU serves at most 64 taps per 16 cycles; bytes per tap of each class's layout
+GATHER_CU = 256
+GATHER_GHZ = 2.4
+GATHER_CYCLES_PER_WAVE = 16
+TAP_BYTES = {"strong": 8, "depth_to_weak": 8, "local_refine": 8, "init": 8, "weak": 4}   # P16 / F16 / U8 texels
 CLASS_KERNEL = {"strong": "k_strong_coop", "weak": "k_weak_coop", "depth_to_weak": "k_depth_to_weak",
                 "local_refine": "k_local_refine_jobs", "init": "k_random_init", "ransac": "k_ransac_fit",
                 "setup": "k_gen_neighbours_lds"}
@@ -574,6 +581,18 @@ def main():
                                         "LocalRefine, the refinement and final-cost NCCs exceed the model's count; "
                                         "bitwise-identical candidate planes sharing one NCC lowers it)"},
         },
+        "gather_roof": {
+            "kernel": f"k_{dom}",
+            "achieved_taps_per_s": round(cnt[dom]["taps"] / launches / (avg_launch_ms * 1e-3), -6),
+            "peak_taps_per_s": GATHER_CU * GATHER_GHZ * 1e9 * 64 / GATHER_CYCLES_PER_WAVE,
+            "frac": round(cnt[dom]["taps"] / launches / (avg_launch_ms * 1e-3)
+                          / (GATHER_CU * GATHER_GHZ * 1e9 * 64 / GATHER_CYCLES_PER_WAVE), 4),
+            "achieved_GBps": round(cnt[dom]["taps"] / launches / (avg_launch_ms * 1e-3) * TAP_BYTES.get(dom, 8) / 1e9, 1),
+            "bytes_per_tap": TAP_BYTES.get(dom, 8),
+            "note": "SURVEY.md §8d's secondary roof: device-counted bilinear taps per launch / avg launch time against "
+                    "the texture path's best case of 16 CU-cycles per 64-lane gather (one 128-B line per lane quad, "
+                    "profiles/r03_td_probe2.md); making every gather free does not speed the strong sweep "
+                    "(profiles/r06a_ab_fake_gather.log), so this roof is not the bound either"},
         "hbm": {"pass_algorithmic_bytes": pass_bytes,
                 "achieved_GBps": round(pass_bytes / (ms_per_step * 1e-3) / 1e9, 2), "peak_GBps": HBM_PEAK_GBS},
         "pass_tflops": round(pass_flops / (ms_per_step * 1e-3) / 1e12, 3),
