@@ -152,8 +152,8 @@ struct DpeContext {
   DevArr<short2> nb, nearest, edge_neigh, lab_bound;
   DevArr<int> radius;
   DevArr<int> tab_right, tab_down;   // FindNearestStrongPoint tables
-  DevArr<int> gn_ovf;
-  DevArr<float> gn_complex;          // DPE_DBG_GN_ONCE: complex_ after GenNeighbours                // GenNeighbours pixels left to the scratch kernel (k_gen_neighbours_lds)
+  DevArr<int> gn_ovf;                // GenNeighbours pixels left to the scratch kernel (k_gen_neighbours_lds)
+  DevArr<float> gn_complex;          // DPE_DBG_GN_ONCE: complex_ after GenNeighbours
   DevArr<float> gn_tab;              // normalised image coordinates per column / row (k_gn_tables)
   DevArr<int> lists, row_counts, list_totals;   // per-colour pixel lists for the sweeps
   DevArr<int> part_cnt;                          // per colour: chunk counts / offsets of the weak-list partition
