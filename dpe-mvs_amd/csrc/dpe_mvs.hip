@@ -906,12 +906,28 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   k_depth_normal<<<fg, fb, 0, s>>>(dpc, Bc);
   for (int colour = 0; colour < 2; ++colour) k_filter<<<hg, hb, 0, s>>>(dpc, Bc, colour);   // hb: 32 x 4 = kFilterThreads
   end();
+  // LocalRefine on the 6-px border (which DepthToWeak leaves to it) reads and writes only its own
+  // pixel's plane besides the images and source depths (DPE.cu:2749-2835), and DepthToWeak writes
+  // only interior pixels: the two are independent, so the border kernel runs on the aux stream
+  // beside DepthToWeak (launched first: it is small and would otherwise wait for DepthToWeak's slots)
+  if (overlap) {
+    HIPC(hipEventRecord(c->ev_fork, s));
+    HIPC(hipStreamWaitEvent(a, c->ev_fork, 0));
+    Bc = begin(DPE_CLASS_LOCAL_REFINE);
+    launch_local_refine(c->img_cls, (long)L, W, H, nv, a, dpc, Bc);
+    end();
+    HIPC(hipEventRecord(c->ev_join, a));
+  }
   Bc = begin(DPE_CLASS_DEPTH_TO_WEAK);
   launch_depth_to_weak(c->img_cls, (long)L, s, dpc, Bc);
   end();
-  Bc = begin(DPE_CLASS_LOCAL_REFINE);
-  launch_local_refine(c->img_cls, (long)L, W, H, nv, s, dpc, Bc);
-  end();
+  if (overlap) {
+    HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
+  } else {
+    Bc = begin(DPE_CLASS_LOCAL_REFINE);
+    launch_local_refine(c->img_cls, (long)L, W, H, nv, s, dpc, Bc);
+    end();
+  }
   HIPC(hipGetLastError());
   if (slot_overflow) {   // per-class times would silently miss launches
     HIPC(hipStreamSynchronize(s));
