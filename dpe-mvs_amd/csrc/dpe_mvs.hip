@@ -731,15 +731,20 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   HIPC(hipMemcpyAsync(B.weak, c->weak0.p, L, hipMemcpyDeviceToDevice, s));
   HIPC(hipMemcpyAsync(B.sel, c->sel0.p, L * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
   HIPC(hipMemsetAsync(B.costs, 0, L * sizeof(float), s));
-  HIPC(hipMemsetAsync(B.fit_plane, 0, L * sizeof(float4), s));
-  HIPC(hipMemsetAsync(B.complex_, 0, L * sizeof(float), s));
-  if (!gn_skip) HIPC(hipMemsetAsync(B.weak_rel, 0xFF, L, s));   // GenNeighbours writes 0 / 1 for every WEAK pixel
   HIPC(hipMemsetAsync(B.vw, 0, L * DPE_MAX_IMAGES, s));
-  if (!gn_skip) HIPC(hipMemsetAsync(B.nb, 0xFF, L * 9 * sizeof(short2), s));
-  HIPC(hipMemsetAsync(B.nearest, 0xFF, L * sizeof(short2), s));
-  HIPC(hipMemsetAsync(B.edge_neigh, 0xFF, L * 8 * sizeof(short2), s));
-  HIPC(hipMemsetAsync(B.lab_bound, 0xFF, L * 8 * sizeof(short2), s));
-  HIPC(hipMemsetAsync(B.radius, 0, L * sizeof(int), s));
+  // the rest of the initial state is first read by the setup chain (or, after it joins the pass
+  // stream, by RANSACToGetFitPlane and the weak sweeps): it is cleared on the setup chain's stream
+  auto clear_setup_state = [&](hipStream_t q) -> int {
+    HIPC(hipMemsetAsync(B.fit_plane, 0, L * sizeof(float4), q));
+    HIPC(hipMemsetAsync(B.complex_, 0, L * sizeof(float), q));
+    if (!gn_skip) HIPC(hipMemsetAsync(B.weak_rel, 0xFF, L, q));   // GenNeighbours writes 0 / 1 for every WEAK pixel
+    if (!gn_skip) HIPC(hipMemsetAsync(B.nb, 0xFF, L * 9 * sizeof(short2), q));
+    HIPC(hipMemsetAsync(B.nearest, 0xFF, L * sizeof(short2), q));
+    HIPC(hipMemsetAsync(B.edge_neigh, 0xFF, L * 8 * sizeof(short2), q));
+    HIPC(hipMemsetAsync(B.lab_bound, 0xFF, L * 8 * sizeof(short2), q));
+    HIPC(hipMemsetAsync(B.radius, 0, L * sizeof(int), q));
+    return DPE_OK;
+  };
 
   const dim3 fb(16, 16), fg((W + 15) / 16, (H + 15) / 16);
   const dim3 rb(16, kRansacThreads / 16), rg((W + 15) / 16, (H + rb.y - 1) / rb.y);
@@ -779,6 +784,7 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
     HIPC(hipEventRecord(c->ev_fork, s));
     HIPC(hipStreamWaitEvent(a, c->ev_fork, 0));
   }
+  if (const int rc = clear_setup_state(a); rc != DPE_OK) return rc;
   k_gen_edge_inform<<<fg, fb, 0, a>>>(dpc, Bc);
   if (pc.P.use_edge) k_edge_rays<<<(unsigned)(3 * (W + H) - 2), 64, 0, a>>>(dpc, Bc);
   if (gn_skip) HIPC(hipMemcpyAsync(B.complex_, c->gn_complex.p, L * sizeof(float), hipMemcpyDeviceToDevice, a));
