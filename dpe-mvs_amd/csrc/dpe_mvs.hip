@@ -662,6 +662,18 @@ static int stage_impl(DpeContext* c, const DpePassInput* in, const StageSrc& src
   return DPE_OK;
 }
 
+// the state a strong half-sweep reads its neighbours from (planes, costs, selected views before the
+// sweep: the red/black same-colour semantics), the three copies in one launch
+__global__ void __launch_bounds__(256) k_snapshot(const uint4* __restrict__ planes, const uint32_t* __restrict__ costs,
+                                                  const uint32_t* __restrict__ sel, uint4* __restrict__ planes_s,
+                                                  uint32_t* __restrict__ costs_s, uint32_t* __restrict__ sel_s, size_t L) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= L) return;
+  planes_s[i] = planes[i];
+  costs_s[i] = costs[i];
+  sel_s[i] = sel[i];
+}
+
 extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   g_err.clear();
   if (!c) { g_err = "dpe_pm_execute: null context"; return DPE_ERR_ARG; }
@@ -843,9 +855,8 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   };
   for (int it = 0; it < pc.P.max_iterations; ++it) {
     for (int colour = 0; colour < 2; ++colour) {
-      HIPC(hipMemcpyAsync(B.planes_snap, B.planes, L * sizeof(float4), hipMemcpyDeviceToDevice, s));
-      HIPC(hipMemcpyAsync(B.costs_snap, B.costs, L * sizeof(float), hipMemcpyDeviceToDevice, s));
-      HIPC(hipMemcpyAsync(B.sel_snap, B.sel, L * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+      k_snapshot<<<(unsigned)((L + 255) / 256), 256, 0, s>>>((const uint4*)B.planes, (const uint32_t*)B.costs, B.sel,
+                                                          (uint4*)B.planes_snap, (uint32_t*)B.costs_snap, B.sel_snap, L);
       Bc = begin(DPE_CLASS_STRONG);
       strong_sweep(Bc, it, c->lists.p + (colour * 2 + 0) * list_stride, c->list_totals.p + colour * 2 + 0);
       if (overlap && it == 0 && colour == 0) {
