@@ -662,6 +662,24 @@ static int stage_impl(DpeContext* c, const DpePassInput* in, const StageSrc& src
   return DPE_OK;
 }
 
+// the pass's initial state in one launch: planes, weak_info and selected views from the staged
+// copies, costs and view weights cleared
+static_assert(DPE_MAX_IMAGES == 32, "k_pass_init clears 32 view-weight bytes per pixel");
+__global__ void __launch_bounds__(256) k_pass_init(const uint4* __restrict__ planes0, const uint8_t* __restrict__ weak0,
+                                                   const uint32_t* __restrict__ sel0, uint4* __restrict__ planes,
+                                                   uint8_t* __restrict__ weak, uint32_t* __restrict__ sel,
+                                                   uint32_t* __restrict__ costs, uint4* __restrict__ vw, size_t L) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= L) return;
+  planes[i] = planes0[i];
+  weak[i] = weak0[i];
+  sel[i] = sel0[i];
+  costs[i] = 0u;
+  const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+  vw[2 * i] = z;
+  vw[2 * i + 1] = z;
+}
+
 // the state a strong half-sweep reads its neighbours from (planes, costs, selected views before the
 // sweep: the red/black same-colour semantics), the three copies in one launch
 __global__ void __launch_bounds__(256) k_snapshot(const uint4* __restrict__ planes, const uint32_t* __restrict__ costs,
@@ -739,11 +757,8 @@ extern "C" int dpe_pm_execute(DpeContext* c, void* stream_) {
   static const bool gn_once = [] { const char* e = getenv("DPE_DBG_GN_ONCE"); return e && atoi(e) == 1; }();
   const bool gn_skip = gn_once && c->gn_done_for_stage;
   // initial state (the reference uploads it in CudaSpaceInitialization, DPE.cpp:964-1015)
-  HIPC(hipMemcpyAsync(B.planes, c->planes0.p, L * sizeof(float4), hipMemcpyDeviceToDevice, s));
-  HIPC(hipMemcpyAsync(B.weak, c->weak0.p, L, hipMemcpyDeviceToDevice, s));
-  HIPC(hipMemcpyAsync(B.sel, c->sel0.p, L * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
-  HIPC(hipMemsetAsync(B.costs, 0, L * sizeof(float), s));
-  HIPC(hipMemsetAsync(B.vw, 0, L * DPE_MAX_IMAGES, s));
+  k_pass_init<<<(unsigned)((L + 255) / 256), 256, 0, s>>>((const uint4*)c->planes0.p, c->weak0.p, c->sel0.p, (uint4*)B.planes,
+                                                          B.weak, B.sel, (uint32_t*)B.costs, (uint4*)B.vw, L);
   // the rest of the initial state is first read by the setup chain (or, after it joins the pass
   // stream, by RANSACToGetFitPlane and the weak sweeps): it is cleared on the setup chain's stream
   auto clear_setup_state = [&](hipStream_t q) -> int {
