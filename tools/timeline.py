@@ -23,11 +23,11 @@ def main():
     ks = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]),
            r.get("Queue_Id") or r.get("Stream_Id") or "?") for r in rows]
     ks.sort()
-    # a pass starts with the first list kernel of the setup (k_list_count<0>) after the memcpys; split
-    # at the k_random_init dispatches: pass i = [init_i - (setup before it), next pass)
-    starts = [i for i, k in enumerate(ks) if k[2].startswith("k_list_count<0>")]
-    # the first k_list_count<0> of a pass precedes k_gen_edge_inform
-    pass_starts = [i for i in starts if i + 3 < len(ks) and any(ks[j][2].startswith("k_gen_edge_inform") for j in range(i, min(i + 6, len(ks))))]
+        # (since round 6 a pass begins with k_pass_init, the initial state in one launch)
+    pass_starts = [i for i, k in enumerate(ks) if k[2].startswith("k_pass_init")]
+    if not pass_starts:   # older builds: the first k_list_count<0> of a pass precedes k_gen_edge_inform
+        starts = [i for i, k in enumerate(ks) if k[2].startswith("k_list_count<0>")]
+        pass_starts = [i for i in starts if i + 3 < len(ks) and any(ks[j][2].startswith("k_gen_edge_inform") for j in range(i, min(i + 6, len(ks))))]
     if len(pass_starts) < back:
         print("passes found:", len(pass_starts))
         return
