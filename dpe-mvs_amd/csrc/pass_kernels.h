@@ -923,7 +923,7 @@ __global__ void __launch_bounds__(256) k_random_init(const PassConst* __restrict
 }
 
 // ------------------------------------------------------------------------------ RANSACToGetFitPlane
-constexpr int kRansacThreads = 128;   // 1-D workgroups: 28 KB of LDS each
+constexpr int kRansacThreads = 128;   // 1-D workgroups: 16 KB of LDS each
 // One thread per entry of a weak list (the sweep's list of one colour), instead of the reference's
 // full-grid launch with ~80 % of the threads returning at once.  Only the colour's own weak update
 // reads a fit plane or radius, so the rows past the red/black grid (half_rows) need none.
@@ -948,12 +948,18 @@ __global__ void __launch_bounds__(kRansacThreads) k_ransac_fit(const PassConst* 
     }
   }
   // support points in LDS (thread index fastest): the random draws index them, which a register
-  // array cannot do without scratch memory
+  // array cannot do without scratch memory.  Their normals are re-read from the planes when a try
+  // needs them (nothing writes a plane during the fits): 128 B of LDS per thread instead of 224, so
+  // 5 waves per SIMD instead of 3 and both colours' fits resident at once
   __shared__ short2 s_sp[8][kRansacThreads];
-  __shared__ float3 s_sp3[8][kRansacThreads], s_spn[8][kRansacThreads];
+  __shared__ float3 s_sp3[8][kRansacThreads];
   const int tid = threadIdx.x;
   struct Col2 { short2* p; DEV short2& operator[](int i) const { return p[i * kRansacThreads]; } } sp{&s_sp[0][tid]};
-  struct Col3 { float3* p; DEV float3& operator[](int i) const { return p[i * kRansacThreads]; } } sp3{&s_sp3[0][tid]}, spn{&s_spn[0][tid]};
+  struct Col3 { float3* p; DEV float3& operator[](int i) const { return p[i * kRansacThreads]; } } sp3{&s_sp3[0][tid]};
+  auto spn = [&](int i) -> float3 {
+    const float4 pl = B.planes[sp[i].x + sp[i].y * W];
+    return make_float3(pl.x, pl.y, pl.z);
+  };
   int sc = 0;
   float X[3];
   const short2* nb = B.nb + (size_t)center * 9;
@@ -965,7 +971,6 @@ __global__ void __launch_bounds__(kRansacThreads) k_ransac_fit(const PassConst* 
     const float depth = depth_from_plane(camera, pl, tp.x, tp.y);
     get3d(camera, tp.x, tp.y, depth, X);
     sp3[sc] = make_float3(X[0], X[1], X[2]);
-    spn[sc] = make_float3(pl.x, pl.y, pl.z);
     sc++;
   }
   if (sc < 3) { B.fit_plane[center] = B.planes[center]; return; }
@@ -992,7 +997,7 @@ __global__ void __launch_bounds__(kRansacThreads) k_ransac_fit(const PassConst* 
     if (a == b || b == c || a == c) continue;
     bool is_strong_plane = false;
     if (pc.P.geom_consistency && edge_limit) {
-      const float3 AN = spn[a], BN = spn[b], CN = spn[c];
+      const float3 AN = spn(a), BN = spn(b), CN = spn(c);
       is_strong_plane = true;
       if ((double)(AN.x * BN.x + AN.y * BN.y + AN.z * BN.z) < 0.8660254 ||
           (double)(AN.x * CN.x + AN.y * CN.y + AN.z * CN.z) < 0.8660254 ||
