@@ -14,7 +14,7 @@ groups=(
 i=0
 for g in "${groups[@]}"; do
   if [ -n "$PMC_GROUPS" ] && [[ " $PMC_GROUPS " != *" $i "* ]]; then i=$((i+1)); continue; fi
-  DPE_OVERLAP=0 timeout -k 10 300 rocprofv3 --pmc $g --output-format csv -d $OUT/g$i -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-instrument --no-e2e --no-pass-types > $OUT/g$i.log 2>&1 || { echo "pass $i failed"; exit 1; }
+  DPE_OVERLAP=0 timeout -k 10 300 rocprofv3 --pmc $g --output-format csv -d $OUT/g$i -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-instrument --no-e2e --no-pass-types --no-pipeline > $OUT/g$i.log 2>&1 || { echo "pass $i failed"; exit 1; }
   i=$((i+1))
 done
 echo PMC_DONE

@@ -11,7 +11,7 @@ groups=(
 )
 i=0
 for g in "${groups[@]}"; do
-  DPE_OVERLAP=0 timeout -s KILL 240 rocprofv3 --pmc $g --output-format csv -d $OUT/g$i -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-instrument > $OUT/g$i.log 2>&1 || { echo "pass $i failed"; exit 1; }
+  DPE_OVERLAP=0 timeout -s KILL 240 rocprofv3 --pmc $g --output-format csv -d $OUT/g$i -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-instrument --no-e2e --no-pass-types --no-pipeline > $OUT/g$i.log 2>&1 || { echo "pass $i failed"; exit 1; }
   i=$((i+1))
 done
 echo PMC_DONE
