@@ -349,6 +349,50 @@ DEV bool rcp_range_ok(const Homog& H, float x0, float x1, float y0, float y1) {
          amax < 1.2676506002282294e+30f;
 }
 
+// Round 6: true when, besides rcp_range_ok, every tap (x, y) of the box [x0, x1] x [y0, y1] has its
+// computed t = fma(Qx, iz, kTexMagic + 1) strictly inside the clamp range (kTexMagic, kTexMagic + W + 1)
+// (and the same for y with H), so tex_t_fast's med3 returns t itself and the taps can skip it: the
+// same bits.  Why it suffices (s = Qx / qz, the tap's exact coordinate; the clamp range is s in
+// [-1, W]):
+//  * qz, Qx, Qy are affine in (x, y) and qz keeps one sign over the box (rcp_range_ok), so each tap's
+//    exact s lies between the exact corner values;
+//  * each corner is tested with the taps' own FMAs: Qx >= 0 and fma(W - 1, qz, -Qx) >= 0 (times the
+//    sign of qz), i.e. s in [0, W - 1] up to the rounding of those values, below 0.01 texel under
+//    the two magnitude conditions below;
+//  * a tap's computed t differs from s + kTexMagic + 1 by at most 0.1 texel: qz is one FMA of
+//    (h7 y) and b = fma(h6, x, h8), so its relative error is <= 2^-24 (1 + |b| / |qz|) <= 2^-17 when
+//    min |qz| >= 2^-6 max |b, qz| (condition 1); v_rcp_f32 adds 2^-22; Qx's absolute error is
+//    <= 2^-24 (|Qx| + |bx|) and |bx| <= 2^16 min |qz| (condition 2) makes it <= 2^-8 texel after the
+//    division; |s| < 2^14 (images narrower than 16383 px) gives |s| 2^-16.9 < 0.13 -- the corner
+//    margin of one texel on each side covers all of it.
+DEV bool taps_unclamped(const Homog& H, float x0, float x1, float y0, float y1, float wm1, float hm1) {
+  const float b0 = __builtin_fmaf(H.h[6], x0, H.h[8]), b1 = __builtin_fmaf(H.h[6], x1, H.h[8]);
+  const float q00 = __builtin_fmaf(H.h[7], y0, b0), q01 = __builtin_fmaf(H.h[7], y1, b0);
+  const float q10 = __builtin_fmaf(H.h[7], y0, b1), q11 = __builtin_fmaf(H.h[7], y1, b1);
+  const float mn = __builtin_fminf(__builtin_fminf(q00, q01), __builtin_fminf(q10, q11));
+  const float mx = __builtin_fmaxf(__builtin_fmaxf(q00, q01), __builtin_fmaxf(q10, q11));
+  const float amax = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(b0), __builtin_fabsf(b1)),
+                                     __builtin_fmaxf(__builtin_fabsf(mn), __builtin_fabsf(mx)));
+  const float sg = mn > 0.0f ? 1.0f : -1.0f;
+  const float lo = mn > 0.0f ? mn : -mx;
+  const float bx0 = __builtin_fmaf(H.h[0], x0, H.h[2]), bx1 = __builtin_fmaf(H.h[0], x1, H.h[2]);
+  const float by0 = __builtin_fmaf(H.h[3], x0, H.h[5]), by1 = __builtin_fmaf(H.h[3], x1, H.h[5]);
+  const float bmax = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(bx0), __builtin_fabsf(bx1)),
+                                     __builtin_fmaxf(__builtin_fabsf(by0), __builtin_fabsf(by1)));
+  bool ok = lo >= amax * 0.015625f && bmax <= lo * 65536.0f;
+  const float bxs[2] = {bx0, bx1}, bys[2] = {by0, by1}, qs[4] = {q00, q01, q10, q11}, ys[2] = {y0, y1};
+  float m = 3.40282347e+38f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float qz = qs[k] * sg;
+    const float X = __builtin_fmaf(H.h[1], ys[k & 1], bxs[k >> 1]) * sg;
+    const float Y = __builtin_fmaf(H.h[4], ys[k & 1], bys[k >> 1]) * sg;
+    m = __builtin_fminf(m, __builtin_fminf(__builtin_fminf(X, Y),
+                                           __builtin_fminf(__builtin_fmaf(wm1, qz, -X), __builtin_fmaf(hm1, qz, -Y))));
+  }
+  return ok && m >= 0.0f;
+}
+
 // ------------------------------------------------------------------------------ sampling
 DEV float ref_texel(const float* ref, int W, int H, int x, int y) {
   x = x < 0 ? 0 : (x > W - 1 ? W - 1 : x);
@@ -580,15 +624,17 @@ DEV float tap_u8_fast(const DevBufs& B, uint32_t vadj, uint32_t stride, f2v tmax
 // the coordinate FMAs packed across the two taps; per element the same operations as tap_u8_fast,
 // so each result is bit-identical to it.
 // `base` is the texel array the byte offsets index (tex_base of the layout; vadj selects the view).
-template <int T>
+template <int T, bool CLAMP = true>
 DEV f2v tap2_at(const uint8_t* base, uint32_t vadj, uint32_t stride, f2v tmax, const float* h, f2v bxy, float bz, f2v yf) {
   const f2v qx = fma2(f2s(h[1]), yf, f2s(bxy.x));
   const f2v qy = fma2(f2s(h[4]), yf, f2s(bxy.y));
   const f2v qz = fma2(f2s(h[7]), yf, f2s(bz));
   const f2v iz = (f2v){rcp_tap<true>(qz.x), rcp_tap<true>(qz.y)};
   const f2v tx = fma2(qx, iz, f2s(kTexMagic + kTexUnit)), ty = fma2(qy, iz, f2s(kTexMagic + kTexUnit));
-  const float cx0 = tex_t_fast(tx.x, tmax.x), cx1 = tex_t_fast(tx.y, tmax.x);
-  const float cy0 = tex_t_fast(ty.x, tmax.y), cy1 = tex_t_fast(ty.y, tmax.y);
+  // CLAMP = false: the caller proved every tap inside the clamp range (taps_unclamped), where the
+  // clamp returns t itself
+  const float cx0 = CLAMP ? tex_t_fast(tx.x, tmax.x) : tx.x, cx1 = CLAMP ? tex_t_fast(tx.y, tmax.x) : tx.y;
+  const float cy0 = CLAMP ? tex_t_fast(ty.x, tmax.y) : ty.x, cy1 = CLAMP ? tex_t_fast(ty.y, tmax.y) : ty.y;
   const uint32_t ux0 = __float_as_uint(cx0), ux1 = __float_as_uint(cx1);
   const uint32_t uy0 = __float_as_uint(cy0), uy1 = __float_as_uint(cy1);
   const uint8_t* p0 = base + (vadj + (__umul24(uy0 >> 8, stride) + (ux0 >> 8)) * tex_bytes<T>());

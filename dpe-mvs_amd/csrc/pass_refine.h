@@ -65,7 +65,7 @@ DEV void patch_lds_pre(const float* pw, float& p_inv, float& p_mref, float& p_va
 // base + vofs + (ty * stride + tx) * texel bytes, 32-bit arithmetic).
 // Packed form: (r_src, r_rs) accumulate as one pair; weights are (w, w*grey) pairs in LDS; the two
 // taps of a row pair share each packed op (tap2_at).
-template <int U8>
+template <int U8, bool CLAMP = true>
 DEV void taps36_at(const float* pw, int px, int py, f2v tmax, const uint8_t* base, uint32_t vofs, uint32_t stride,
                    const Homog& H0, float* acc) {
     const Homog H = scale_cols(H0);
@@ -83,7 +83,7 @@ DEV void taps36_at(const float* pw, int px, int py, f2v tmax, const uint8_t* bas
       float r_ss = 0;
 #pragma unroll
       for (int b = 0; b < 6; b += 2) {
-        const f2v sp = tap2_at<U8>(base, vadj, stride, tmax, H.h, bxy, bz,
+        const f2v sp = tap2_at<U8, CLAMP>(base, vadj, stride, tmax, H.h, bxy, bz,
                                    (f2v){(float)(py - 5 + 2 * b), (float)(py - 3 + 2 * b)});
         const f2v w0 = wp[a * 6 + b], w1 = wp[a * 6 + b + 1];
         const float ws0 = w0.x * sp.x, ws1 = w1.x * sp.y;   // two plain multiplies: no operand packing
@@ -101,13 +101,13 @@ DEV void taps36_at(const float* pw, int px, int py, f2v tmax, const uint8_t* bas
 // 1.3e9 on the bench workload, profiles/r05d_pool_stats.log) goes through the rolled generic loop,
 // which sums the same weights (bilateral_weight of the same texels) in the same order, so the same
 // bits, and keeps an unrolled per-tap-tested loop out of every caller's register budget.
-template <int U8, bool FAST>
+template <int U8, bool FAST, bool CLAMP = true>
 DEV void lds_taps(const float* pw, int px, int py, const PassConst& pc, const DevBufs& B, int v, const Homog& H0,
                   float* acc) {
   const int W = pc.W, Hh = pc.H;
   if constexpr (U8 != TEX_F32 && FAST) {
-    taps36_at<U8>(pw, px, py, tex_tmax2(W, Hh), tex_base<U8>(B), (uint32_t)v * tex_view<U8>(B),
-                      tex_stride<U8>(W), H0, acc);
+    taps36_at<U8, CLAMP>(pw, px, py, tex_tmax2(W, Hh), tex_base<U8>(B), (uint32_t)v * tex_view<U8>(B),
+                         tex_stride<U8>(W), H0, acc);
   } else if constexpr (!FAST) {
     float g[6];
     generic_taps<U8, false>(pc, B, v, H0, px, py, ref_texel(B.ref, W, Hh, px, py), pc.P.strong_radius,
@@ -201,7 +201,16 @@ DEV float ncc_old_lds(const float* pw, float s_ref, float s_rr, float s_w, int p
   const bool ok = rcp_range_ok(H, (float)(px - 5), (float)(px + 5), (float)(py - 5), (float)(py + 5));
   PATCH_STAT(ok);
   if (ok) {
-    lds_taps<U8, true>(pw, px, py, pc, B, v, H, a);
+#ifndef DPE_UNCLAMPED
+#define DPE_UNCLAMPED 1
+#endif
+    // the clamp-free taps when every active lane's patch is inside the image with a texel to spare
+    if (DPE_UNCLAMPED && U8 != TEX_F32 &&
+        __all(taps_unclamped(H, (float)(px - 5), (float)(px + 5), (float)(py - 5), (float)(py + 5), (float)(pc.W - 1),
+                             (float)(pc.H - 1))))
+      lds_taps<U8, true, false>(pw, px, py, pc, B, v, H, a);
+    else
+      lds_taps<U8, true>(pw, px, py, pc, B, v, H, a);
   } else
     lds_taps<U8, false>(pw, px, py, pc, B, v, H, a);
   return ncc_finalize_pre(s_ref, s_rr, s_w, a[0], a[1], a[2]);   // (inv, mref, var_ref) of patch_lds_pre
