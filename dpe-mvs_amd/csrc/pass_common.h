@@ -359,12 +359,12 @@ DEV bool rcp_range_ok(const Homog& H, float x0, float x1, float y0, float y1) {
 //  * each corner is tested with the taps' own FMAs: Qx >= 0 and fma(W - 1, qz, -Qx) >= 0 (times the
 //    sign of qz), i.e. s in [0, W - 1] up to the rounding of those values, below 0.01 texel under
 //    the two magnitude conditions below;
-//  * a tap's computed t differs from s + kTexMagic + 1 by at most 0.1 texel: qz is one FMA of
+//  * a tap's computed t differs from s + kTexMagic + 1 by at most 0.15 texel: qz is one FMA of
 //    (h7 y) and b = fma(h6, x, h8), so its relative error is <= 2^-24 (1 + |b| / |qz|) <= 2^-17 when
 //    min |qz| >= 2^-6 max |b, qz| (condition 1); v_rcp_f32 adds 2^-22; Qx's absolute error is
-//    <= 2^-24 (|Qx| + |bx|) and |bx| <= 2^16 min |qz| (condition 2) makes it <= 2^-8 texel after the
-//    division; |s| < 2^14 (images narrower than 16383 px) gives |s| 2^-16.9 < 0.13 -- the corner
-//    margin of one texel on each side covers all of it.
+//    <= 2^-24 (|Qx| + 2 |bx|) and |bx| <= 2^16 min |qz| (condition 2) makes it <= 2^-6.8 texel after
+//    the division; |s| < 2^14 (images narrower than 16383 px) gives |s| 2^-16.9 < 0.14; the final
+//    rounding of t adds 2^-9 -- the corner margin of one texel on each side covers all of it.
 DEV bool taps_unclamped(const Homog& H, float x0, float x1, float y0, float y1, float wm1, float hm1) {
   const float b0 = __builtin_fmaf(H.h[6], x0, H.h[8]), b1 = __builtin_fmaf(H.h[6], x1, H.h[8]);
   const float q00 = __builtin_fmaf(H.h[7], y0, b0), q01 = __builtin_fmaf(H.h[7], y1, b0);
