@@ -72,6 +72,10 @@ struct DevBufs {
 #ifndef DPE_DIAG
 #define DPE_DIAG 0
 #endif
+// DPE_UNCLAMPED=0 (A/B only): every fast Old-NCC patch keeps its tap clamps (taps_unclamped unused)
+#ifndef DPE_UNCLAMPED
+#define DPE_UNCLAMPED 1
+#endif
 #define DPE_POOL_STATS (((DPE_DIAG) >> 4) & 1)
 #define DPE_PHASE_PROF ((DPE_DIAG) & 1)
 #define DPE_LINE_STATS (((DPE_DIAG) >> 1) & 1)

@@ -201,9 +201,6 @@ DEV float ncc_old_lds(const float* pw, float s_ref, float s_rr, float s_w, int p
   const bool ok = rcp_range_ok(H, (float)(px - 5), (float)(px + 5), (float)(py - 5), (float)(py + 5));
   PATCH_STAT(ok);
   if (ok) {
-#ifndef DPE_UNCLAMPED
-#define DPE_UNCLAMPED 1
-#endif
     // the clamp-free taps when every active lane's patch is inside the image with a texel to spare
     if (DPE_UNCLAMPED && U8 != TEX_F32 &&
         __all(taps_unclamped(H, (float)(px - 5), (float)(px + 5), (float)(py - 5), (float)(py + 5), (float)(pc.W - 1),
