@@ -202,11 +202,18 @@ DEV float ncc_old_lds(const float* pw, float s_ref, float s_rr, float s_w, int p
   PATCH_STAT(ok);
   if (ok) {
     // the clamp-free taps when every active lane's patch is inside the image with a texel to spare
-    if (DPE_UNCLAMPED && U8 != TEX_F32 &&
-        __all(taps_unclamped(H, (float)(px - 5), (float)(px + 5), (float)(py - 5), (float)(py + 5), (float)(pc.W - 1),
-                             (float)(pc.H - 1))))
+    const bool ncl = taps_unclamped(H, (float)(px - 5), (float)(px + 5), (float)(py - 5), (float)(py + 5), (float)(pc.W - 1),
+                                    (float)(pc.H - 1));
+#if DPE_POOL_STATS   // tools/pool_stats.py: lanes failing the test, lanes tested, lanes on the clamp-free path
+    atomicAdd(&g_pool[6][2], ncl ? 0ull : 1ull);
+    atomicAdd(&g_pool[7][0], 1ull);
+#endif
+    if (DPE_UNCLAMPED && U8 != TEX_F32 && __all(ncl)) {
+#if DPE_POOL_STATS
+      atomicAdd(&g_pool[7][1], 1ull);
+#endif
       lds_taps<U8, true, false>(pw, px, py, pc, B, v, H, a);
-    else
+    } else
       lds_taps<U8, true>(pw, px, py, pc, B, v, H, a);
   } else
     lds_taps<U8, false>(pw, px, py, pc, B, v, H, a);

@@ -37,6 +37,8 @@ for fn in ("dpe_dbg_pool_stats_main", "dpe_dbg_pool_stats_tap", "dpe_dbg_pool_st
         tot[k] += buf[k]
 print(f"Old NCC patches from LDS {tot[18]:12d}  slow (reciprocal range check failed) {tot[19]:12d} "
       f"= {100.0 * tot[19] / max(tot[18], 1):.2f}%", flush=True)
+print(f"fast Old NCC lanes {tot[21]:12d}  failing taps_unclamped {tot[20]:12d} = {100.0 * tot[20] / max(tot[21], 1):.2f}%  "
+      f"on the clamp-free path {tot[22]:12d} = {100.0 * tot[22] / max(tot[21], 1):.2f}%", flush=True)
 for k in range(6):
     jobs, rounds, waves = tot[3 * k: 3 * k + 3]
     if waves:
