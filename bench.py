@@ -41,7 +41,7 @@ FLOP_PER_HOMOGRAPHY = 120
 FLOP_PER_GEOM = 60
 MODEL_FLOP_PER_PX = (36 * FLOP_PER_TAP + FLOP_PER_HOMOGRAPHY) * (42 * (NV_ - 1) + 75 * 4)   # 0.86 MFLOP
 # per-dispatch HBM bytes from the committed PMC passes (tools/pmc.sh + tools/prof_summary.py)
-PMC_JSON = next((os.path.join(ROOT, "profiles", f) for f in ("r06f_pmc.json", "r06_pmc.json", "r05_pmc.json", "r04f_pmc.json", "r04_pmc.json", "r03s2_pmc.json", "r03_pmc.json", "r02_pmc.json")
+PMC_JSON = next((os.path.join(ROOT, "profiles", f) for f in ("r06g_pmc.json", "r06f_pmc.json", "r06_pmc.json", "r05_pmc.json", "r04f_pmc.json", "r04_pmc.json", "r03s2_pmc.json", "r03_pmc.json", "r02_pmc.json")
                  if os.path.exists(os.path.join(ROOT, "profiles", f))), os.path.join(ROOT, "profiles", "r04_pmc.json"))
 # secondary roof (the on-chip gather rate): a 64-lane texel gather costs the texture
 # path at least one CU-cycle per lane quad = 16 CU-cycles (profiles/r03_td_probe2.md), so at the
