@@ -94,8 +94,9 @@ __global__ void __launch_bounds__(64) k_edge_rays(const PassConst* __restrict__ 
 __global__ void __launch_bounds__(256) k_gen_edge_inform(const PassConst* __restrict__ pcp, DevBufs B) {   // DPE.cu:2483-2591
   const PassConst& pc = *pcp;
   __shared__ uint8_t s_tile[kEiTile * kEiTile];
+  __shared__ uint32_t s_hs[kEiTile][16];   // round 6: row sums of the packed flags over 2r + 1 columns
   const int radius = pc.P.strong_radius;
-  const bool tiled = pc.P.use_edge && radius >= 0 && radius <= kEiTileR;
+  const bool tiled = pc.P.use_edge && radius >= 0 && radius <= kEiTileR && blockDim.x == 16;
   if (tiled) {   // block-uniform; every thread of the block helps before any returns
     const int lb0 = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y, B.xcd_rows * gridDim.x);
     const int ox = (lb0 % gridDim.x) * blockDim.x - radius, oy = (lb0 / gridDim.x) * blockDim.y - radius;
@@ -110,20 +111,28 @@ __global__ void __launch_bounds__(256) k_gen_edge_inform(const PassConst* __rest
       s_tile[t] = v;
     }
     __syncthreads();
+    // the window counts are separable: each (tile row, output column) sums its 2r + 1 flags, packed
+    // as edge | label 0 << 10 | inside << 20 (each count <= 17 x 17 < 1024), then a pixel adds 2r + 1
+    // row sums -- the same integer counts as the 2-D loop
+    for (int t = threadIdx.y * blockDim.x + threadIdx.x; t < th * 16; t += blockDim.x * blockDim.y) {
+      const uint8_t* row = s_tile + (t / 16) * tw + t % 16;
+      uint32_t acc = 0;
+      for (int i = 0; i <= 2 * radius; i++) {
+        const uint32_t v = row[i];
+        acc += (v & 1u) | ((v & 2u) << 9) | ((v & 4u) << 18);
+      }
+      s_hs[t / 16][t % 16] = acc;
+    }
+    __syncthreads();
   }
   PIX2D_FULL();
   const int W = pc.W, H = pc.H;
   if (pc.P.use_edge) {   // the 8 edge rays come from k_edge_rays
     int edge_pix = 0, tot_pix = 0, bound_pix = 0;
     if (tiled) {
-      const int tw = blockDim.x + 2 * radius;
-      for (int j = 0; j <= 2 * radius; j++) {
-        const uint8_t* row = s_tile + (threadIdx.y + j) * tw + threadIdx.x;
-        for (int i = 0; i <= 2 * radius; i++) {
-          const int v = row[i];
-          edge_pix += v & 1; bound_pix += (v >> 1) & 1; tot_pix += v >> 2;
-        }
-      }
+      uint32_t acc = 0;
+      for (int j = 0; j <= 2 * radius; j++) acc += s_hs[threadIdx.y + j][threadIdx.x];
+      edge_pix = (int)(acc & 1023u); bound_pix = (int)((acc >> 10) & 1023u); tot_pix = (int)(acc >> 20);
     } else {
       for (int i = -radius; i <= radius; i++)
         for (int j = -radius; j <= radius; j++) {
